@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPT-2-small-shape LM training throughput on MI355X.
+
+Metric (BASELINE.json): "training tokens/sec (whole node), GPT-2-small config
+at 1/2/4/8 MI355X".  Model: 12 layers, d_model 768, 12 heads, SwiGLU d_ff 2048,
+RoPE, RMSNorm, vocab 50257, seq 1024, bf16 compute with fp32 master weights
+and fp32 optimizer state; random-init weights, synthetic uniform token data.
+Every timed step is a full training step: forward, fused LM-head+CE,
+backward, RCCL bucketed all-reduce (N>1), global-norm clip, AdamW update.
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29511 bench.py --gpus 8 --steps 20 --warmup 5
+
+Weak scaling: the per-GPU micro-batch is fixed, global batch = N * micro-batch.
+Rank 0 prints one JSON line; the time is the MAX over ranks of K steps
+bracketed by barrier + device synchronize.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+
+METRIC = "training tokens/sec (whole node), GPT-2-small config at 1/2/4/8 MI355X"
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16, help="per-GPU micro-batch (sequences)")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--model", default="gpt2-small")
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+
+    from bpe_transformer.data import synthetic_tokens
+    from bpe_transformer.models import TransformerLM, get_preset
+    from bpe_transformer.parallel import all_reduce_max, barrier, cleanup, init_distributed
+    from bpe_transformer.train.engine import TrainEngine
+
+    info = init_distributed("cuda")
+    if args.gpus != info.world_size:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
+    dev = info.device
+    torch.manual_seed(1234)  # identical init on every rank (rank-0 broadcast also enforces it)
+    cfg = get_preset(args.model, context_length=args.seq)
+    model = TransformerLM.from_config(cfg, device=dev, dtype=torch.bfloat16)
+    engine = TrainEngine(model, info, lr=3e-4, weight_decay=0.1, max_grad_norm=1.0, bucket_mb=args.bucket_mb)
+
+    # synthetic token stream, different per rank; batches staged on the device up front
+    data = synthetic_tokens(cfg.vocab_size, args.batch * (args.seq + 1) * 8, seed=1000 + info.rank)
+    data_t = torch.from_numpy(data.astype("int64")).to(dev)
+    nwin = len(data) // (args.seq + 1)
+
+    def batch(i: int):
+        j = (i * args.batch) % (nwin - args.batch)
+        w = data_t[j * (args.seq + 1) : (j + args.batch) * (args.seq + 1)].view(args.batch, args.seq + 1)
+        return [(w[:, :-1].contiguous(), w[:, 1:].contiguous())]
+
+    for i in range(args.warmup):
+        engine.train_step(batch(i))
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = None
+    for i in range(args.steps):
+        loss = engine.train_step(batch(args.warmup + i))
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = all_reduce_max(dt, dev)
+    loss_v = float(loss.item()) if loss is not None else float("nan")
+
+    n = info.world_size
+    tokens = args.steps * args.batch * args.seq * n
+    value = tokens / dt
+    flops_tok = cfg.train_flops_per_token(args.seq)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "tokens/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1000.0, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (uniform random tokens, random-init weights)",
+        "config": {
+            "model": f"{args.model} ({cfg.num_layers}L/{cfg.d_model}d/{cfg.num_heads}H, RoPE+SwiGLU+RMSNorm, "
+                     f"vocab {cfg.vocab_size})",
+            "global_batch": args.batch * n,
+            "seq_len": args.seq,
+            "parallelism": f"dp{n}",
+            "micro_batch_per_gpu": args.batch,
+        },
+        "mfu_bf16_dense_2.5PF": round(value / n * flops_tok / 2.5e15, 4),
+        "final_loss": round(loss_v, 4),
+    }
+    if info.is_main:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    cleanup()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,119 @@
+"""Decoder-only Transformer language model (reference contract K12,
+``tests/adapters.py:282-361``).
+
+``TransformerLM.forward(ids)`` returns logits ``[B, S, V]`` (the contract).
+``TransformerLM.loss(ids, targets)`` is the training entry point: on the GPU
+it fuses the LM head with softmax-cross-entropy (``ops.lm_head_cross_entropy``)
+so the ``[tokens, vocab]`` logits are written once and overwritten in place by
+their gradient.
+"""
+
+from __future__ import annotations
+
+import torch
+from torch import Tensor, nn
+
+from .. import ops
+from .config import ModelConfig
+from .layers import Embedding, Linear, RMSNorm, TransformerBlock
+
+
+class TransformerLM(nn.Module):
+    def __init__(
+        self,
+        vocab_size: int,
+        context_length: int,
+        d_model: int,
+        num_layers: int,
+        num_heads: int,
+        d_ff: int,
+        rope_theta: float = 10000.0,
+        num_kv_heads: int | None = None,
+        remove_rmsnorm: bool = False,
+        use_post_norm: bool = False,
+        remove_rope: bool = False,
+        ffn_type: str | None = None,
+        eps: float = 1e-5,
+        device=None,
+        dtype=None,
+    ):
+        super().__init__()
+        self.config = ModelConfig(
+            vocab_size=vocab_size, context_length=context_length, d_model=d_model, num_layers=num_layers,
+            num_heads=num_heads, d_ff=d_ff, rope_theta=rope_theta, num_kv_heads=num_kv_heads,
+            remove_rmsnorm=remove_rmsnorm, use_post_norm=use_post_norm, remove_rope=remove_rope, ffn_type=ffn_type,
+            eps=eps,
+        )
+        self.context_length = context_length
+        self.token_embeddings = Embedding(vocab_size, d_model, device=device, dtype=dtype)
+        self.layers = nn.ModuleList(
+            TransformerBlock(
+                d_model, num_heads, d_ff, context_length, rope_theta, num_kv_heads=num_kv_heads,
+                remove_rmsnorm=remove_rmsnorm, use_post_norm=use_post_norm, remove_rope=remove_rope,
+                ffn_type=ffn_type, eps=eps, device=device, dtype=dtype,
+            )
+            for _ in range(num_layers)
+        )
+        self.ln_final = RMSNorm(d_model, eps, device=device, dtype=dtype) if not remove_rmsnorm else nn.Identity()
+        self.lm_head = Linear(d_model, vocab_size, device=device, dtype=dtype)
+
+    @classmethod
+    def from_config(cls, cfg: ModelConfig, device=None, dtype=None) -> "TransformerLM":
+        return cls(
+            cfg.vocab_size, cfg.context_length, cfg.d_model, cfg.num_layers, cfg.num_heads, cfg.d_ff, cfg.rope_theta,
+            num_kv_heads=cfg.num_kv_heads, remove_rmsnorm=cfg.remove_rmsnorm, use_post_norm=cfg.use_post_norm,
+            remove_rope=cfg.remove_rope, ffn_type=cfg.ffn_type, eps=cfg.eps, device=device, dtype=dtype,
+        )
+
+    def hidden_states(self, in_indices: Tensor) -> Tensor:
+        assert in_indices.shape[-1] <= self.context_length, "sequence longer than context_length"
+        x = self.token_embeddings(in_indices)
+        for layer in self.layers:
+            x = layer(x)
+        return self.ln_final(x)
+
+    def forward(self, in_indices: Tensor) -> Tensor:
+        return self.lm_head(self.hidden_states(in_indices))
+
+    def loss(self, in_indices: Tensor, targets: Tensor, ignore_index: int = ops.IGNORE_INDEX) -> Tensor:
+        """Mean next-token cross-entropy; fused LM head + CE on the GPU."""
+        h = self.hidden_states(in_indices)
+        return ops.lm_head_cross_entropy(h, self.lm_head.weight, targets, ignore_index)
+
+    def load_reference_state_dict(self, state_dict: dict, strict: bool = True):
+        """Load a reference-format state dict (strips ``torch.compile``'s ``_orig_mod.`` prefix,
+        ``tests/conftest.py:201`` in the reference)."""
+        sd = {k.replace("_orig_mod.", ""): v for k, v in state_dict.items()}
+        return self.load_state_dict(sd, strict=strict)
+
+    @torch.no_grad()
+    def generate(
+        self,
+        prompt: Tensor,
+        max_new_tokens: int,
+        temperature: float = 1.0,
+        top_p: float | None = None,
+        eos_token_id: int | None = None,
+        generator: torch.Generator | None = None,
+    ) -> Tensor:
+        """Autoregressive sampling (temperature + nucleus).  ``prompt``: ``[S]`` or ``[B, S]``."""
+        squeeze = prompt.dim() == 1
+        ids = prompt.unsqueeze(0) if squeeze else prompt
+        for _ in range(max_new_tokens):
+            ctx = ids[:, -self.context_length :]
+            logits = self.forward(ctx)[:, -1, :].float()
+            if temperature <= 0:
+                nxt = logits.argmax(-1, keepdim=True)
+            else:
+                probs = torch.softmax(logits / temperature, dim=-1)
+                if top_p is not None and top_p < 1.0:
+                    sp, si = probs.sort(dim=-1, descending=True)
+                    keep = sp.cumsum(-1) - sp < top_p
+                    sp = sp * keep
+                    probs = torch.zeros_like(probs).scatter_(-1, si, sp)
+                    probs = probs / probs.sum(-1, keepdim=True)
+                nxt = torch.multinomial(probs, 1, generator=generator)
+            ids = torch.cat([ids, nxt], dim=1)
+            if eos_token_id is not None and bool((nxt == eos_token_id).all()):
+                break
+        return ids[0] if squeeze else ids

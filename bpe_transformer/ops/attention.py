@@ -1,0 +1,110 @@
+"""Flash attention with fused RoPE (``csrc/flash_attn.hip``).
+
+``flash_attention_qkv`` consumes the output of the fused QKV projection
+``[B*S, (H + 2*Hkv) * D]`` directly (no transposes, no separate RoPE pass) and
+returns ``[B*S, H*D]`` ready for the output projection; its backward returns
+the gradient in the same fused layout, feeding the QKV weight-gradient GEMM
+directly.  Reference contracts K7/K9/K10 (``tests/adapters.py:92-184``).
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import Tensor
+
+from . import reference as F
+from ._ext import ops
+
+SUPPORTED_HEAD_DIMS = (64, 128)
+
+_EMPTY: dict[torch.device, Tensor] = {}
+
+
+def _empty(dev: torch.device) -> Tensor:
+    t = _EMPTY.get(dev)
+    if t is None:
+        t = torch.empty(0, 0, device=dev, dtype=torch.float32)
+        _EMPTY[dev] = t
+    return t
+
+
+class _FlashAttnQKVFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv: Tensor, cos, sin, B: int, S: int, H: int, Hkv: int, D: int, causal: bool, scale: float):
+        q = qkv[:, : H * D]
+        k = qkv[:, H * D : (H + Hkv) * D]
+        v = qkv[:, (H + Hkv) * D :]
+        use_rope = cos is not None
+        c = cos if use_rope else _empty(qkv.device)
+        s = sin if use_rope else _empty(qkv.device)
+        o, lse = ops().fa_fwd(q, k, v, c, s, B, S, H, Hkv, D, causal, use_rope, scale)
+        ctx.save_for_backward(qkv, o, lse, c, s)
+        ctx.meta = (B, S, H, Hkv, D, causal, use_rope, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do: Tensor):
+        qkv, o, lse, c, s = ctx.saved_tensors
+        B, S, H, Hkv, D, causal, use_rope, scale = ctx.meta
+        q = qkv[:, : H * D]
+        k = qkv[:, H * D : (H + Hkv) * D]
+        v = qkv[:, (H + Hkv) * D :]
+        dqkv = ops().fa_bwd(do, q, k, v, o, lse, c, s, B, S, H, Hkv, D, causal, use_rope, scale)
+        return dqkv, None, None, None, None, None, None, None, None, None
+
+
+def flash_supported(x: Tensor, head_dim: int) -> bool:
+    return x.is_cuda and x.dtype == torch.bfloat16 and head_dim in SUPPORTED_HEAD_DIMS
+
+
+def flash_attention_qkv(
+    qkv: Tensor,
+    batch: int,
+    seq: int,
+    n_heads: int,
+    n_kv_heads: int,
+    head_dim: int,
+    cos: Tensor | None = None,
+    sin: Tensor | None = None,
+    causal: bool = True,
+    scale: float | None = None,
+) -> Tensor:
+    """Attention over a fused QKV activation.
+
+    qkv: ``[batch*seq, (n_heads + 2*n_kv_heads) * head_dim]`` bf16 on the GPU.
+    cos/sin: fp32 ``[>=seq, head_dim/2]`` RoPE tables (positions ``0..seq-1``),
+    or ``None`` for no RoPE.  Returns ``[batch*seq, n_heads*head_dim]``.
+    """
+    scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
+    if qkv.is_cuda:
+        if qkv.stride(1) != 1 or qkv.stride(0) % 8 != 0:
+            qkv = qkv.contiguous()
+        if cos is not None:
+            cos = cos.float().contiguous()
+            sin = sin.float().contiguous()
+        return _FlashAttnQKVFn.apply(qkv, cos, sin, batch, seq, n_heads, n_kv_heads, head_dim, causal, scale)
+    return attention_qkv_reference(qkv, batch, seq, n_heads, n_kv_heads, head_dim, cos, sin, causal, scale)
+
+
+def attention_qkv_reference(qkv, batch, seq, n_heads, n_kv_heads, head_dim, cos=None, sin=None, causal=True,
+                            scale=None) -> Tensor:
+    """Oracle implementation of :func:`flash_attention_qkv` (fp32 math)."""
+    H, Hkv, D = n_heads, n_kv_heads, head_dim
+    x = qkv.float().view(batch, seq, H + 2 * Hkv, D)
+    q = x[:, :, :H].transpose(1, 2)
+    k = x[:, :, H : H + Hkv].transpose(1, 2)
+    v = x[:, :, H + Hkv :].transpose(1, 2)
+    if cos is not None:
+        q = F.apply_rope(q, cos.float(), sin.float())
+        k = F.apply_rope(k, cos.float(), sin.float())
+    if Hkv != H:
+        k = k.repeat_interleave(H // Hkv, dim=1)
+        v = v.repeat_interleave(H // Hkv, dim=1)
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    s = torch.matmul(q, k.transpose(-1, -2)) * scale
+    if causal:
+        s = s.masked_fill(~F.causal_mask(seq, device=s.device), float("-inf"))
+    o = torch.matmul(F.softmax(s, -1), v)
+    return o.transpose(1, 2).reshape(batch * seq, H * D).to(qkv.dtype)

@@ -1,0 +1,106 @@
+"""In-tree build of the gfx950 HIP kernel library.
+
+``python -m bpe_transformer.ops.build`` compiles every ``csrc/*.hip`` with
+``hipcc --offload-arch=gfx950`` (device code, no torch headers: seconds per
+file), the single torch-binding translation unit, and links
+``bpe_transformer/ops/_bpe_hip.so`` next to this file, so the library travels
+with the source tree (no JIT cache, no site-packages install).  Rebuilds are
+incremental (mtime of each source and every header).
+
+No hipify step and no CUDA sources: the kernels are written for CDNA4 directly.
+"""
+
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+REPO = HERE.parent.parent
+BUILD = REPO / "build" / "hip"
+LIB = HERE / "_bpe_hip.so"
+ARCH = os.environ.get("BPE_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension
+
+    inc = cpp_extension.include_paths()
+    lib = cpp_extension.library_paths()
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _needs_build(obj: Path, src: Path, headers: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"compile failed: {' '.join(cmd[:4])} ...")
+    if verbose and r.stderr.strip():
+        sys.stderr.write(r.stderr)
+
+
+def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    headers = sorted(CSRC.glob("*.h"))
+    hip_srcs = sorted(CSRC.glob("*.hip"))
+    inc, libdirs, abi = _torch_paths()
+    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", str(CSRC)]
+    jobs_list = []
+    objs = []
+    for src in hip_srcs:
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _needs_build(obj, src, headers):
+            jobs_list.append([HIPCC, *common, "-c", str(src), "-o", str(obj)])
+    bind_src = CSRC / "torch_bindings.cpp"
+    bind_obj = BUILD / "torch_bindings.o"
+    objs.append(bind_obj)
+    if force or _needs_build(bind_obj, bind_src, headers):
+        cmd = [HIPCC, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
+               "-I", str(CSRC)]
+        for i in inc:
+            cmd += ["-I", i]
+        cmd += ["-I", sysconfig.get_paths()["include"], "-c", str(bind_src), "-o", str(bind_obj)]
+        jobs_list.append(cmd)
+    if jobs_list:
+        n = jobs or min(8, os.cpu_count() or 4)
+        with cf.ThreadPoolExecutor(n) as ex:
+            list(ex.map(lambda c: _run(c, verbose), jobs_list))
+    if force or jobs_list or not LIB.exists():
+        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(LIB), *map(str, objs)]
+        for d in libdirs:
+            link += ["-L", d, f"-Wl,-rpath,{d}"]
+        link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip"]
+        _run(link, verbose)
+    return LIB
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("-f", "--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args()
+    print(build(verbose=a.verbose, jobs=a.jobs, force=a.force))
+
+
+if __name__ == "__main__":
+    main()

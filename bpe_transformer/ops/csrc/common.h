@@ -1,0 +1,112 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * wave64: lane = threadIdx.x & 63, reductions span 64 lanes.
+//   * bf16 values move as raw 16-bit words (u16) in 16-byte vectors
+//     (8 x bf16 per lane per load) -- hipcc does not auto-vectorise bf16.
+//   * all statistics / accumulations are fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define BPE_WAVE 64
+
+typedef unsigned short u16;
+typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace bpe {
+
+__device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float(((unsigned)h) << 16); }
+// Round-to-nearest-even; hipcc lowers the __bf16 cast to v_cvt_pk_bf16_f32 on gfx950
+// (keeps NaN a NaN, unlike the integer-rounding trick).
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ---- typed 16-byte vector load/store, converting to/from fp32 -------------
+// T = float (4 elems / 16 B) or __bf16 (8 elems / 16 B).
+template <typename T> struct Vec;
+template <> struct Vec<float> {
+    static constexpr int N = 4;
+    float v[4];
+    __device__ __forceinline__ void load(const float* p) {
+        f32x4 t = *reinterpret_cast<const f32x4*>(p);
+        v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    }
+    __device__ __forceinline__ void store(float* p) const {
+        f32x4 t = {v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(p) = t;
+    }
+};
+template <> struct Vec<__bf16> {
+    static constexpr int N = 8;
+    float v[8];
+    __device__ __forceinline__ void load(const __bf16* p) {
+        u16x8 t = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = bf2f(t[i]);
+    }
+    __device__ __forceinline__ void store(__bf16* p) const {
+        u16x8 t;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = f2bf(v[i]);
+        *reinterpret_cast<u16x8*>(p) = t;
+    }
+};
+
+template <typename T> __device__ __forceinline__ float ld1(const T* p);
+template <> __device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld1<__bf16>(const __bf16* p) {
+    return bf2f(*reinterpret_cast<const u16*>(p));
+}
+template <typename T> __device__ __forceinline__ void st1(T* p, float v);
+template <> __device__ __forceinline__ void st1<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void st1<__bf16>(__bf16* p, float v) {
+    *reinterpret_cast<u16*>(p) = f2bf(v);
+}
+
+// Block-wide sum for blockDim.x <= 1024 (multiple of 64). `red` needs 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    float r = 0.f;
+    for (int i = 0; i < nw; ++i) r += red[i];
+    return r;
+}
+__device__ __forceinline__ float block_max(float v, float* red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    v = wave_max(v);
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    float r = -INFINITY;
+    for (int i = 0; i < nw; ++i) r = fmaxf(r, red[i]);
+    return r;
+}
+
+// Grid size for memory-bound grid-stride kernels: enough blocks to fill 256 CUs
+// several times over, capped so per-launch overhead stays low (guide G11).
+__host__ __forceinline__ int stream_grid(size_t work_items, int block, int cap = 2048) {
+    size_t g = (work_items + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > (size_t)cap) g = cap;
+    return (int)g;
+}
+
+}  // namespace bpe

@@ -1,0 +1,79 @@
+// Host-side launcher declarations for the gfx950 kernels.  Every launcher
+// takes raw device pointers plus the HIP stream it must run on and never
+// allocates or synchronises, so callers may capture it in a HIP graph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+enum { DT_F32 = 0, DT_BF16 = 1 };
+
+// rmsnorm.hip
+void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float* rstd, int M, int N, float eps,
+                        hipStream_t s);
+int rmsnorm_bwd_grid(int M);
+void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
+                        float* partial, void* dw, int M, int N, hipStream_t s);
+
+// activations.hip
+void launch_swiglu_fwd(int dtype, const void* gu, void* out, size_t M, int F, hipStream_t s);
+void launch_swiglu_bwd(int dtype, const void* dout, const void* gu, void* dgu, size_t M, int F, hipStream_t s);
+void launch_act_fwd(int dtype, int kind, const void* x, void* y, size_t n, hipStream_t s);
+void launch_act_bwd(int dtype, int kind, const void* dy, const void* x, void* dx, size_t n, hipStream_t s);
+
+// cross_entropy.hip
+void launch_ce_fwd_bwd(int dtype, void* logits, long ld, const int64_t* targets, float* loss, float* lse,
+                       const float* nvalid, int M, int V, long ignore_index, int write_grad, hipStream_t s);
+
+// embedding.hip
+void launch_embed_fwd(int dtype, const void* W, const int64_t* ids, void* out, int M, int D, long vocab,
+                      hipStream_t s);
+void launch_embed_bwd(int dtype, const void* dout, const int64_t* sorted_ids, const int64_t* perm, void* dW, int M,
+                      int D, hipStream_t s);
+
+// optim.hip
+void launch_adamw(int gdtype, float* p, float* m, float* v, const void* g, void* pout_bf16, size_t n, float lr,
+                  float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, const float* gscale,
+                  hipStream_t s);
+void launch_sumsq_partial(int dtype, const void* x, size_t n, float* partial, int nblocks, hipStream_t s);
+void launch_norm_finalize(const float* partial, int np, float max_norm, float* out_norm, float* out_coef,
+                          hipStream_t s);
+void launch_scale(int dtype, void* x, size_t n, const float* coef, hipStream_t s);
+
+// softmax.hip
+void launch_softmax_fwd(int dtype, const void* x, void* y, int M, int N, hipStream_t s);
+void launch_softmax_bwd(int dtype, const void* dy, const void* y, void* dx, int M, int N, hipStream_t s);
+
+// rope.hip
+void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,
+                 size_t R, int H, int D, int inverse, hipStream_t s);
+
+// flash_attn.hip
+struct FaArgs {
+    const __bf16* q;
+    const __bf16* k;
+    const __bf16* v;
+    long ld_q, ld_kv;  // elements between consecutive tokens
+    __bf16* o;         // [B, S, H, D] with row stride ld_o
+    long ld_o;
+    float* lse;        // [B, H, S] base-2 log-sum-exp of the scaled scores
+    const float* cos;  // [S_max, D/2]
+    const float* sin;
+    int B, H, Hkv, S, D;
+    int causal, rope;
+    float scale;
+    // backward only
+    const __bf16* dout;
+    long ld_do;
+    float* delta;   // [B, H, S] scratch
+    float* dq_acc;  // [B, S, H, D] fp32 scratch
+    __bf16* dq;
+    long ld_dq;
+    __bf16* dk;
+    __bf16* dv;
+    long ld_dkv;
+};
+size_t fa_fwd_lds_bytes(int D);
+size_t fa_bwd_lds_bytes(int D);
+void launch_fa_fwd(const FaArgs& a, hipStream_t s);
+void launch_fa_bwd(const FaArgs& a, hipStream_t s);

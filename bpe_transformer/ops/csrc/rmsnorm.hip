@@ -1,0 +1,185 @@
+// RMSNorm forward / backward for gfx950.
+//
+// Parity target: reference contract K4, `tests/adapters.py:364-384`
+// (y = x / sqrt(mean(x^2) + eps) * g, statistics in fp32).
+//
+// Layout: x is [M, N] row-major, one wave64 per row, 16-byte vector accesses
+// (8 bf16 or 4 fp32 per lane).  The backward writes dx directly and produces
+// the weight gradient deterministically: each wave keeps its lane's column
+// partial sums in registers across a grid-stride sweep of rows, the 4 waves of
+// a block combine through LDS, and a second tiny kernel sums the per-block
+// partials in a fixed order (no float atomics, bitwise reproducible).
+#include "common.h"
+#include "kernels.h"
+
+namespace bpe {
+
+template <typename T>
+__global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                          T* __restrict__ y, float* __restrict__ rstd_out,
+                                                          int M, int N, float eps) {
+    constexpr int V = Vec<T>::N;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const T* xr = x + (size_t)row * N;
+    T* yr = y + (size_t)row * N;
+    const int nvec = N / V;
+    float ss = 0.f;
+    for (int i = lane; i < nvec; i += 64) {
+        Vec<T> a;
+        a.load(xr + i * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) ss += a.v[j] * a.v[j];
+    }
+    ss = wave_sum(ss);
+    const float r = rsqrtf(ss / (float)N + eps);
+    if (lane == 0 && rstd_out) rstd_out[row] = r;
+    for (int i = lane; i < nvec; i += 64) {
+        Vec<T> a, g;
+        a.load(xr + i * V);
+        g.load(w + i * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) a.v[j] = a.v[j] * r * g.v[j];
+        a.store(yr + i * V);
+    }
+}
+
+// C = number of 16-byte column chunks each lane owns (ceil(N / V / 64)).
+template <typename T, int C>
+__global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const T* __restrict__ w,
+                                                          const float* __restrict__ rstd, T* __restrict__ dx,
+                                                          float* __restrict__ dw_partial, int M, int N) {
+    constexpr int V = Vec<T>::N;
+    extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][N]
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nvec = N / V;
+    float dwacc[C][V];
+    float wv[C][V];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int i = c * 64 + lane;
+#pragma unroll
+        for (int j = 0; j < V; ++j) { dwacc[c][j] = 0.f; wv[c][j] = 0.f; }
+        if (i < nvec) {
+            Vec<T> g;
+            g.load(w + i * V);
+#pragma unroll
+            for (int j = 0; j < V; ++j) wv[c][j] = g.v[j];
+        }
+    }
+    for (int row = blockIdx.x * 4 + wid; row < M; row += gridDim.x * 4) {
+        const T* xr = x + (size_t)row * N;
+        const T* dyr = dy + (size_t)row * N;
+        const float r = rstd[row];
+        float xs[C][V], gs[C][V];
+        float dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int i = c * 64 + lane;
+            if (i < nvec) {
+                Vec<T> a, b;
+                a.load(xr + i * V);
+                b.load(dyr + i * V);
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    xs[c][j] = a.v[j] * r;  // x_hat
+                    gs[c][j] = b.v[j];
+                    dot += b.v[j] * wv[c][j] * xs[c][j];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < V; ++j) { xs[c][j] = 0.f; gs[c][j] = 0.f; }
+            }
+        }
+        dot = wave_sum(dot) / (float)N;
+        T* dxr = dx + (size_t)row * N;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int i = c * 64 + lane;
+            if (i < nvec) {
+                Vec<T> o;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    o.v[j] = r * (gs[c][j] * wv[c][j] - xs[c][j] * dot);
+                    dwacc[c][j] += gs[c][j] * xs[c][j];
+                }
+                o.store(dxr + i * V);
+            }
+        }
+    }
+    // combine the 4 waves of this block through LDS, then one partial row per block
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int i = c * 64 + lane;
+        if (i < nvec) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) lds[wid * N + i * V + j] = dwacc[c][j];
+        }
+    }
+    __syncthreads();
+    for (int col = threadIdx.x; col < N; col += 256) {
+        float s = lds[col] + lds[N + col] + lds[2 * N + col] + lds[3 * N + col];
+        dw_partial[(size_t)blockIdx.x * N + col] = s;
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ partial, T* __restrict__ out,
+                                                     int rows, int N) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= N) return;
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += partial[(size_t)r * N + col];
+    st1<T>(out + col, s);
+}
+
+}  // namespace bpe
+
+using namespace bpe;
+
+void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float* rstd, int M, int N, float eps,
+                        hipStream_t s) {
+    dim3 grid((M + 3) / 4), block(256);
+    if (dtype == DT_BF16)
+        rmsnorm_fwd_kernel<__bf16><<<grid, block, 0, s>>>((const __bf16*)x, (const __bf16*)w, (__bf16*)y, rstd,
+                                                          M, N, eps);
+    else
+        rmsnorm_fwd_kernel<float><<<grid, block, 0, s>>>((const float*)x, (const float*)w, (float*)y, rstd, M, N,
+                                                         eps);
+}
+
+template <typename T>
+static void rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* rstd, T* dx, float* partial,
+                             int grid, int M, int N, hipStream_t s) {
+    constexpr int V = Vec<T>::N;
+    const int chunks = (N / V + 63) / 64;
+    const size_t lds = (size_t)4 * N * sizeof(float);
+#define RMS_CASE(CC)                                                                                    \
+    if (chunks <= CC) {                                                                                 \
+        rmsnorm_bwd_kernel<T, CC><<<grid, 256, lds, s>>>(dy, x, w, rstd, dx, partial, M, N);            \
+        return;                                                                                         \
+    }
+    RMS_CASE(1) RMS_CASE(2) RMS_CASE(4) RMS_CASE(8)
+#undef RMS_CASE
+}
+
+int rmsnorm_bwd_grid(int M) {
+    int g = (M + 3) / 4;
+    return g < 512 ? g : 512;
+}
+
+void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
+                        float* partial, void* dw, int M, int N, hipStream_t s) {
+    const int grid = rmsnorm_bwd_grid(M);
+    if (dtype == DT_BF16) {
+        rms_bwd_dispatch<__bf16>((const __bf16*)dy, (const __bf16*)x, (const __bf16*)w, rstd, (__bf16*)dx, partial,
+                                 grid, M, N, s);
+        colsum_kernel<__bf16><<<(N + 255) / 256, 256, 0, s>>>(partial, (__bf16*)dw, grid, N);
+    } else {
+        rms_bwd_dispatch<float>((const float*)dy, (const float*)x, (const float*)w, rstd, (float*)dx, partial, grid,
+                                M, N, s);
+        colsum_kernel<float><<<(N + 255) / 256, 256, 0, s>>>(partial, (float*)dw, grid, N);
+    }
+}

@@ -1,0 +1,58 @@
+// Standalone rotary positional embedding (interleaved pairs) for gfx950.
+//
+// Parity target: reference contract K8, `tests/adapters.py:187-206`; pairing
+// verified against `tests/_snapshots/test_rope.npz`: pairs are
+// (x[2i], x[2i+1]), inv_freq_i = theta^(-2i/d), angle = pos * inv_freq_i.
+//
+// In the training hot path RoPE is fused into the attention kernels (applied
+// while Q/K tiles are staged); this kernel serves the standalone op and its
+// backward (inverse rotation).  cos/sin come from a host-precomputed fp32
+// table [max_seq, d/2] (guide App. B: no on-device trig in memory-bound ops).
+// x is [R, H, D] contiguous, position of row r = pos[r].
+#include "common.h"
+#include "kernels.h"
+
+namespace bpe {
+
+template <typename T>
+__global__ void __launch_bounds__(256) rope_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                   const int64_t* __restrict__ pos, const float* __restrict__ cosT,
+                                                   const float* __restrict__ sinT, size_t R, int H, int D,
+                                                   float sign) {
+    constexpr int V = Vec<T>::N;
+    const int dv = D / V;
+    const size_t total = R * (size_t)H * dv;
+    const int half = D / 2;
+    for (size_t idx = blockIdx.x * (size_t)256 + threadIdx.x; idx < total; idx += (size_t)gridDim.x * 256) {
+        const size_t r = idx / ((size_t)H * dv);
+        const int d0 = (int)(idx % dv) * V;
+        const long p = pos[r];
+        const float* c = cosT + p * half + d0 / 2;
+        const float* s = sinT + p * half + d0 / 2;
+        Vec<T> a;
+        a.load(x + idx * V);
+#pragma unroll
+        for (int j = 0; j < V; j += 2) {
+            const float cc = c[j / 2], ss = sign * s[j / 2];
+            const float x1 = a.v[j], x2 = a.v[j + 1];
+            a.v[j] = x1 * cc - x2 * ss;
+            a.v[j + 1] = x1 * ss + x2 * cc;
+        }
+        a.store(y + idx * V);
+    }
+}
+
+}  // namespace bpe
+
+using namespace bpe;
+
+void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,
+                 size_t R, int H, int D, int inverse, hipStream_t s) {
+    const int V = dtype == DT_BF16 ? 8 : 4;
+    const int grid = stream_grid(R * H * (size_t)(D / V), 256, 4096);
+    const float sign = inverse ? -1.f : 1.f;
+    if (dtype == DT_BF16)
+        rope_kernel<__bf16><<<grid, 256, 0, s>>>((const __bf16*)x, (__bf16*)y, pos, cosT, sinT, R, H, D, sign);
+    else
+        rope_kernel<float><<<grid, 256, 0, s>>>((const float*)x, (float*)y, pos, cosT, sinT, R, H, D, sign);
+}

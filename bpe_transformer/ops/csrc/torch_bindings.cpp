@@ -1,0 +1,374 @@
+// PyTorch operator registrations for the gfx950 HIP kernels.
+//
+// Ops live in the `bpe_hip` namespace (torch.ops.bpe_hip.*) and are registered
+// for the CUDA dispatch key, which is what ROCm PyTorch uses for HIP device
+// tensors.  Each op validates shapes/dtypes on the host (so no kernel ever
+// sees a shape it was not written for), allocates outputs through the caching
+// allocator and launches on the current HIP stream -- no syncs, so the ops are
+// safe inside HIP-graph capture.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "kernels.h"
+
+#include <algorithm>
+
+namespace {
+
+// ROCm PyTorch exposes HIP devices under the CUDA device type ("masquerading"),
+// so guards and streams must come from the masquerading variants.
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+using DevGuard = at::hip::HIPGuardMasqueradingAsCUDA;
+
+int dt_code(const at::Tensor& t) {
+    if (t.scalar_type() == at::kBFloat16) return DT_BF16;
+    if (t.scalar_type() == at::kFloat) return DT_F32;
+    TORCH_CHECK(false, "bpe_hip: only float32 / bfloat16 tensors are supported, got ", t.scalar_type());
+    return -1;
+}
+int vec_elems(const at::Tensor& t) { return dt_code(t) == DT_BF16 ? 8 : 4; }
+
+void check_cuda(const at::Tensor& t, const char* name) {
+    TORCH_CHECK(t.is_cuda(), "bpe_hip: ", name, " must be a GPU tensor");
+}
+void check_aligned(const at::Tensor& t, const char* name) {
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "bpe_hip: ", name,
+                " must be 16-byte aligned");
+}
+
+// ---------------------------------------------------------------- RMSNorm
+std::tuple<at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "rmsnorm: contiguous inputs required");
+    TORCH_CHECK(x.scalar_type() == w.scalar_type(), "rmsnorm: x and weight dtypes differ");
+    const int N = (int)x.size(-1);
+    TORCH_CHECK(w.numel() == N, "rmsnorm: weight size mismatch");
+    TORCH_CHECK(N % vec_elems(x) == 0, "rmsnorm: last dim must be a multiple of 8 (bf16) / 4 (fp32)");
+    check_aligned(x, "x");
+    const int M = (int)(x.numel() / N);
+    DevGuard g(x.device());
+    auto y = at::empty_like(x);
+    auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+    launch_rmsnorm_fwd(dt_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(), M, N, (float)eps,
+                       cur_stream());
+    return {y, rstd};
+}
+
+std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                               const at::Tensor& rstd) {
+    check_cuda(x, "x");
+    auto dyc = dy.contiguous();
+    const int N = (int)x.size(-1);
+    const int M = (int)(x.numel() / N);
+    TORCH_CHECK(N <= 8 * 64 * vec_elems(x), "rmsnorm bwd: hidden size too large");
+    TORCH_CHECK(dyc.scalar_type() == x.scalar_type(), "rmsnorm bwd: dtype mismatch");
+    DevGuard g(x.device());
+    auto dx = at::empty_like(x);
+    auto dw = at::empty_like(w);
+    const int grid = rmsnorm_bwd_grid(M);
+    auto partial = at::empty({grid, N}, x.options().dtype(at::kFloat));
+    launch_rmsnorm_bwd(dt_code(x), dyc.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dx.data_ptr(),
+                       partial.data_ptr<float>(), dw.data_ptr(), M, N, cur_stream());
+    return {dx, dw};
+}
+
+// ---------------------------------------------------------------- activations
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+    check_cuda(gu, "gu");
+    TORCH_CHECK(gu.is_contiguous(), "swiglu: contiguous input required");
+    const int64_t F2 = gu.size(-1);
+    TORCH_CHECK(F2 % (2 * vec_elems(gu)) == 0, "swiglu: hidden size must be a multiple of 8/16");
+    const int F = (int)(F2 / 2);
+    const size_t M = gu.numel() / F2;
+    auto sizes = gu.sizes().vec();
+    sizes.back() = F;
+    DevGuard g(gu.device());
+    auto out = at::empty(sizes, gu.options());
+    launch_swiglu_fwd(dt_code(gu), gu.data_ptr(), out.data_ptr(), M, F, cur_stream());
+    return out;
+}
+
+at::Tensor swiglu_bwd(const at::Tensor& dout, const at::Tensor& gu) {
+    check_cuda(gu, "gu");
+    auto d = dout.contiguous();
+    const int64_t F2 = gu.size(-1);
+    const int F = (int)(F2 / 2);
+    const size_t M = gu.numel() / F2;
+    DevGuard g(gu.device());
+    auto dgu = at::empty_like(gu);
+    launch_swiglu_bwd(dt_code(gu), d.data_ptr(), gu.data_ptr(), dgu.data_ptr(), M, F, cur_stream());
+    return dgu;
+}
+
+at::Tensor act_fwd(const at::Tensor& x, int64_t kind) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.is_contiguous() && x.numel() % vec_elems(x) == 0, "act: contiguous, numel multiple of 8/4");
+    DevGuard g(x.device());
+    auto y = at::empty_like(x);
+    launch_act_fwd(dt_code(x), (int)kind, x.data_ptr(), y.data_ptr(), x.numel(), cur_stream());
+    return y;
+}
+
+at::Tensor act_bwd(const at::Tensor& dy, const at::Tensor& x, int64_t kind) {
+    check_cuda(x, "x");
+    auto d = dy.contiguous();
+    DevGuard g(x.device());
+    auto dx = at::empty_like(x);
+    launch_act_bwd(dt_code(x), (int)kind, d.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel(), cur_stream());
+    return dx;
+}
+
+// ---------------------------------------------------------------- cross entropy
+std::tuple<at::Tensor, at::Tensor> ce_fwd_bwd(at::Tensor logits, const at::Tensor& targets, int64_t ignore_index,
+                                              bool write_grad) {
+    check_cuda(logits, "logits");
+    TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "ce: logits must be [M, V] with unit column stride");
+    TORCH_CHECK(targets.scalar_type() == at::kLong && targets.is_contiguous(), "ce: targets must be int64");
+    const int M = (int)logits.size(0), V = (int)logits.size(1);
+    TORCH_CHECK(targets.numel() == M, "ce: targets size mismatch");
+    DevGuard g(logits.device());
+    auto loss = at::empty({M}, logits.options().dtype(at::kFloat));
+    auto lse = at::empty({M}, logits.options().dtype(at::kFloat));
+    auto nvalid = targets.ne(ignore_index).sum().to(at::kFloat);
+    launch_ce_fwd_bwd(dt_code(logits), logits.data_ptr(), logits.stride(0), targets.data_ptr<int64_t>(),
+                      loss.data_ptr<float>(), lse.data_ptr<float>(), nvalid.data_ptr<float>(), M, V, ignore_index,
+                      write_grad ? 1 : 0, cur_stream());
+    return {loss, lse};
+}
+
+// ---------------------------------------------------------------- embedding
+at::Tensor embed_fwd(const at::Tensor& W, const at::Tensor& ids) {
+    check_cuda(W, "weight");
+    TORCH_CHECK(W.dim() == 2 && W.is_contiguous(), "embed: weight must be contiguous [V, D]");
+    TORCH_CHECK(ids.scalar_type() == at::kLong, "embed: ids must be int64");
+    const int D = (int)W.size(1);
+    TORCH_CHECK(D % vec_elems(W) == 0 && (D * W.element_size()) % 16 == 0, "embed: D must be a multiple of 16 bytes");
+    auto idc = ids.contiguous();
+    const int M = (int)idc.numel();
+    auto sizes = idc.sizes().vec();
+    sizes.push_back(D);
+    DevGuard g(W.device());
+    auto out = at::empty(sizes, W.options());
+    launch_embed_fwd(dt_code(W), W.data_ptr(), idc.data_ptr<int64_t>(), out.data_ptr(), M, D, W.size(0), cur_stream());
+    return out;
+}
+
+at::Tensor embed_bwd(const at::Tensor& dout, const at::Tensor& ids, int64_t vocab) {
+    check_cuda(dout, "dout");
+    const int D = (int)dout.size(-1);
+    TORCH_CHECK(D <= 16 * 64 * vec_elems(dout), "embed bwd: D too large");
+    auto d = dout.contiguous().view({-1, D});
+    auto flat = ids.contiguous().view({-1});
+    DevGuard g(dout.device());
+    auto sorted = at::sort(flat, /*stable=*/true, /*dim=*/0, /*descending=*/false);
+    auto dW = at::zeros({vocab, D}, dout.options());
+    launch_embed_bwd(dt_code(dout), d.data_ptr(), std::get<0>(sorted).data_ptr<int64_t>(),
+                     std::get<1>(sorted).data_ptr<int64_t>(), dW.data_ptr(), (int)flat.numel(), D, cur_stream());
+    return dW;
+}
+
+// ---------------------------------------------------------------- optimizer
+void adamw_step(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& grad, const c10::optional<at::Tensor>& pout,
+                double lr, double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt,
+                const c10::optional<at::Tensor>& gscale) {
+    check_cuda(p, "param");
+    TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+                "adamw: master param / moments must be fp32");
+    TORCH_CHECK(p.is_contiguous() && m.is_contiguous() && v.is_contiguous() && grad.is_contiguous(),
+                "adamw: contiguous buffers required");
+    TORCH_CHECK(p.numel() == grad.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adamw: size mismatch");
+    void* po = nullptr;
+    if (pout.has_value() && pout->defined()) {
+        TORCH_CHECK(pout->scalar_type() == at::kBFloat16 && pout->numel() == p.numel() && pout->is_contiguous(),
+                    "adamw: param copy-out must be contiguous bf16");
+        po = pout->data_ptr();
+    }
+    const float* gs = nullptr;
+    if (gscale.has_value() && gscale->defined()) gs = gscale->data_ptr<float>();
+    DevGuard g(p.device());
+    launch_adamw(dt_code(grad), p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(), po,
+                 p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, gs,
+                 cur_stream());
+}
+
+std::tuple<at::Tensor, at::Tensor> grad_norm(at::TensorList tensors, double max_norm) {
+    TORCH_CHECK(!tensors.empty(), "grad_norm: empty list");
+    DevGuard g(tensors[0].device());
+    constexpr int NB = 256;
+    auto partial = at::zeros({(int64_t)tensors.size() * NB}, tensors[0].options().dtype(at::kFloat));
+    for (size_t i = 0; i < tensors.size(); ++i) {
+        auto t = tensors[i];
+        TORCH_CHECK(t.is_contiguous(), "grad_norm: contiguous tensors required");
+        check_aligned(t, "grad");
+        launch_sumsq_partial(dt_code(t), t.data_ptr(), t.numel(), partial.data_ptr<float>() + i * NB, NB,
+                             cur_stream());
+    }
+    auto norm = at::empty({}, partial.options());
+    auto coef = at::empty({}, partial.options());
+    launch_norm_finalize(partial.data_ptr<float>(), (int)partial.numel(), (float)max_norm, norm.data_ptr<float>(),
+                         coef.data_ptr<float>(), cur_stream());
+    return {norm, coef};
+}
+
+void scale_(at::Tensor x, const at::Tensor& coef) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.is_contiguous(), "scale_: contiguous tensor required");
+    check_aligned(x, "x");
+    DevGuard g(x.device());
+    launch_scale(dt_code(x), x.data_ptr(), x.numel(), coef.data_ptr<float>(), cur_stream());
+}
+
+// ---------------------------------------------------------------- softmax
+at::Tensor softmax_fwd(const at::Tensor& x) {
+    check_cuda(x, "x");
+    auto xc = x.contiguous();
+    const int N = (int)xc.size(-1);
+    const int M = (int)(xc.numel() / std::max(N, 1));
+    DevGuard g(x.device());
+    auto y = at::empty_like(xc);
+    launch_softmax_fwd(dt_code(xc), xc.data_ptr(), y.data_ptr(), M, N, cur_stream());
+    return y;
+}
+
+at::Tensor softmax_bwd(const at::Tensor& dy, const at::Tensor& y) {
+    check_cuda(y, "y");
+    auto d = dy.contiguous();
+    const int N = (int)y.size(-1);
+    const int M = (int)(y.numel() / std::max(N, 1));
+    DevGuard g(y.device());
+    auto dx = at::empty_like(y);
+    launch_softmax_bwd(dt_code(y), d.data_ptr(), y.data_ptr(), dx.data_ptr(), M, N, cur_stream());
+    return dx;
+}
+
+// ---------------------------------------------------------------- RoPE
+at::Tensor rope(const at::Tensor& x, const at::Tensor& pos, const at::Tensor& cos, const at::Tensor& sin,
+                bool inverse) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.is_contiguous() && x.dim() == 3, "rope: x must be contiguous [R, H, D]");
+    TORCH_CHECK(pos.scalar_type() == at::kLong && pos.numel() == x.size(0), "rope: pos must be int64 [R]");
+    const int D = (int)x.size(2);
+    TORCH_CHECK(D % vec_elems(x) == 0, "rope: head dim must be a multiple of 8 (bf16) / 4 (fp32)");
+    TORCH_CHECK(cos.size(1) == D / 2 && cos.scalar_type() == at::kFloat, "rope: cos table must be fp32 [S, D/2]");
+    DevGuard g(x.device());
+    auto y = at::empty_like(x);
+    auto p = pos.contiguous();
+    launch_rope(dt_code(x), x.data_ptr(), y.data_ptr(), p.data_ptr<int64_t>(), cos.data_ptr<float>(),
+                sin.data_ptr<float>(), x.size(0), (int)x.size(1), D, inverse ? 1 : 0, cur_stream());
+    return y;
+}
+
+// ---------------------------------------------------------------- flash attention
+void check_qkv(const at::Tensor& t, int64_t rows, int64_t cols, const char* name) {
+    check_cuda(t, name);
+    TORCH_CHECK(t.scalar_type() == at::kBFloat16, "flash attention: ", name, " must be bf16");
+    TORCH_CHECK(t.dim() == 2 && t.size(0) == rows && t.size(1) == cols && t.stride(1) == 1, "flash attention: ",
+                name, " must be a [B*S, heads*D] view with unit column stride");
+    TORCH_CHECK(t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "flash attention: ",
+                name, " rows must be 16-byte aligned");
+}
+
+std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                          const at::Tensor& cos, const at::Tensor& sin, int64_t B, int64_t S, int64_t H,
+                                          int64_t Hkv, int64_t D, bool causal, bool use_rope, double scale) {
+    TORCH_CHECK(D == 64 || D == 128, "flash attention: head dim must be 64 or 128");
+    TORCH_CHECK(H % Hkv == 0, "flash attention: H must be a multiple of Hkv");
+    check_qkv(q, B * S, H * D, "q");
+    check_qkv(k, B * S, Hkv * D, "k");
+    check_qkv(v, B * S, Hkv * D, "v");
+    TORCH_CHECK(k.stride(0) == v.stride(0), "flash attention: k and v must share a row stride");
+    if (use_rope)
+        TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.size(0) >= S && cos.size(1) == D / 2 && cos.is_contiguous()
+                        && sin.is_contiguous(), "flash attention: rope tables must be fp32 [>=S, D/2]");
+    DevGuard g(q.device());
+    auto o = at::empty({B * S, H * D}, q.options());
+    auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+    FaArgs a{};
+    a.q = (const __bf16*)q.data_ptr(); a.k = (const __bf16*)k.data_ptr(); a.v = (const __bf16*)v.data_ptr();
+    a.ld_q = q.stride(0); a.ld_kv = k.stride(0);
+    a.o = (__bf16*)o.data_ptr(); a.ld_o = H * D; a.lse = lse.data_ptr<float>();
+    a.cos = use_rope ? cos.data_ptr<float>() : nullptr; a.sin = use_rope ? sin.data_ptr<float>() : nullptr;
+    a.B = (int)B; a.H = (int)H; a.Hkv = (int)Hkv; a.S = (int)S; a.D = (int)D;
+    a.causal = causal; a.rope = use_rope; a.scale = (float)scale;
+    launch_fa_fwd(a, cur_stream());
+    return {o, lse};
+}
+
+// Returns dqkv = [B*S, (H + 2*Hkv) * D]: dq | dk | dv in the fused QKV-projection layout.
+at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                  const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cos, const at::Tensor& sin, int64_t B,
+                  int64_t S, int64_t H, int64_t Hkv, int64_t D, bool causal, bool use_rope, double scale) {
+    TORCH_CHECK(D == 64 || D == 128, "flash attention: head dim must be 64 or 128");
+    check_qkv(q, B * S, H * D, "q");
+    check_qkv(k, B * S, Hkv * D, "k");
+    check_qkv(v, B * S, Hkv * D, "v");
+    auto d = dout.contiguous();
+    check_qkv(d, B * S, H * D, "dout");
+    check_qkv(o, B * S, H * D, "o");
+    DevGuard g(q.device());
+    const int64_t W = (H + 2 * Hkv) * D;
+    auto dqkv = at::empty({B * S, W}, q.options());
+    auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+    auto dq_acc = at::empty({B * S, H * D}, q.options().dtype(at::kFloat));
+    FaArgs a{};
+    a.q = (const __bf16*)q.data_ptr(); a.k = (const __bf16*)k.data_ptr(); a.v = (const __bf16*)v.data_ptr();
+    a.ld_q = q.stride(0); a.ld_kv = k.stride(0);
+    a.o = (__bf16*)o.data_ptr(); a.ld_o = o.stride(0); a.lse = lse.data_ptr<float>();
+    a.cos = use_rope ? cos.data_ptr<float>() : nullptr; a.sin = use_rope ? sin.data_ptr<float>() : nullptr;
+    a.B = (int)B; a.H = (int)H; a.Hkv = (int)Hkv; a.S = (int)S; a.D = (int)D;
+    a.causal = causal; a.rope = use_rope; a.scale = (float)scale;
+    a.dout = (const __bf16*)d.data_ptr(); a.ld_do = d.stride(0);
+    a.delta = delta.data_ptr<float>(); a.dq_acc = dq_acc.data_ptr<float>();
+    __bf16* base = (__bf16*)dqkv.data_ptr();
+    a.dq = base; a.ld_dq = W;
+    a.dk = base + H * D; a.dv = base + (H + Hkv) * D; a.ld_dkv = W;
+    launch_fa_bwd(a, cur_stream());
+    return dqkv;
+}
+
+}  // namespace
+
+TORCH_LIBRARY(bpe_hip, m) {
+    m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
+    m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd) -> (Tensor, Tensor)");
+    m.def("swiglu_fwd(Tensor gu) -> Tensor");
+    m.def("swiglu_bwd(Tensor dout, Tensor gu) -> Tensor");
+    m.def("act_fwd(Tensor x, int kind) -> Tensor");
+    m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");
+    m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index, bool write_grad) -> (Tensor, Tensor)");
+    m.def("embed_fwd(Tensor weight, Tensor ids) -> Tensor");
+    m.def("embed_bwd(Tensor dout, Tensor ids, int vocab) -> Tensor");
+    m.def("adamw_step(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor grad, Tensor(d!)? pout, float lr, float b1, "
+          "float b2, float eps, float wd, float bc1, float bc2_sqrt, Tensor? gscale) -> ()");
+    m.def("grad_norm(Tensor[] tensors, float max_norm) -> (Tensor, Tensor)");
+    m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
+    m.def("softmax_fwd(Tensor x) -> Tensor");
+    m.def("softmax_bwd(Tensor dy, Tensor y) -> Tensor");
+    m.def("rope(Tensor x, Tensor pos, Tensor cos, Tensor sin, bool inverse) -> Tensor");
+    m.def("fa_fwd(Tensor q, Tensor k, Tensor v, Tensor cos, Tensor sin, int B, int S, int H, int Hkv, int D, "
+          "bool causal, bool rope, float scale) -> (Tensor, Tensor)");
+    m.def("fa_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor cos, Tensor sin, int B, "
+          "int S, int H, int Hkv, int D, bool causal, bool rope, float scale) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
+    m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+    m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+    m.impl("swiglu_fwd", &swiglu_fwd);
+    m.impl("swiglu_bwd", &swiglu_bwd);
+    m.impl("act_fwd", &act_fwd);
+    m.impl("act_bwd", &act_bwd);
+    m.impl("ce_fwd_bwd", &ce_fwd_bwd);
+    m.impl("embed_fwd", &embed_fwd);
+    m.impl("embed_bwd", &embed_bwd);
+    m.impl("adamw_step", &adamw_step);
+    m.impl("grad_norm", &grad_norm);
+    m.impl("scale_", &scale_);
+    m.impl("softmax_fwd", &softmax_fwd);
+    m.impl("softmax_bwd", &softmax_bwd);
+    m.impl("rope", &rope);
+    m.impl("fa_fwd", &fa_fwd);
+    m.impl("fa_bwd", &fa_bwd);
+}

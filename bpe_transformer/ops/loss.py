@@ -1,0 +1,80 @@
+"""Cross-entropy ops (``csrc/cross_entropy.hip``).
+
+``lm_head_cross_entropy`` fuses the LM-head GEMM with softmax-CE: the logits
+buffer is written once by the GEMM, read by the CE kernel which overwrites it
+IN PLACE with ``(softmax - onehot) / n``, and the backward is two GEMMs scaled
+by the incoming gradient (applied to the small GEMM outputs, never to the
+[tokens, vocab] buffer).  At GPT-2 shape that is one 1.6 GB bf16 buffer per
+step instead of logits + probabilities + gradient.
+
+Reference contract K13 (``tests/adapters.py:440-455``).
+"""
+
+from __future__ import annotations
+
+import torch
+from torch import Tensor
+
+from . import reference as F
+from ._ext import ops
+
+IGNORE_INDEX = -100
+
+
+class _LMHeadCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h: Tensor, w: Tensor, targets: Tensor, ignore_index: int):
+        logits = torch.matmul(h, w.t())  # hipBLASLt
+        loss_rows, _ = ops().ce_fwd_bwd(logits, targets, ignore_index, True)
+        nvalid = (targets != ignore_index).sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(h, w, logits)
+        return loss_rows.sum() / nvalid
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        h, w, dlogits = ctx.saved_tensors
+        dh = torch.matmul(dlogits, w)
+        dw = torch.matmul(dlogits.t(), h)
+        gg = g.to(dh.dtype)
+        return dh * gg, dw * gg, None, None
+
+
+class _CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits: Tensor, targets: Tensor, ignore_index: int):
+        buf = logits.detach().reshape(-1, logits.shape[-1]).clone()
+        loss_rows, _ = ops().ce_fwd_bwd(buf, targets, ignore_index, True)
+        nvalid = (targets != ignore_index).sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(buf)
+        ctx.shape = logits.shape
+        return loss_rows.sum() / nvalid
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        (buf,) = ctx.saved_tensors
+        return (buf * g.to(buf.dtype)).view(ctx.shape), None, None
+
+
+def cross_entropy(logits: Tensor, targets: Tensor, ignore_index: int = IGNORE_INDEX) -> Tensor:
+    """Mean cross-entropy over all rows of ``logits[..., V]``."""
+    t = targets.reshape(-1)
+    if logits.is_cuda and logits.dtype in (torch.float32, torch.bfloat16):
+        return _CrossEntropyFn.apply(logits, t.long().contiguous(), ignore_index)
+    x = logits.reshape(-1, logits.shape[-1])
+    valid = t != ignore_index
+    if bool(valid.all()):
+        return F.cross_entropy(x, t)
+    return F.cross_entropy(x[valid], t[valid])
+
+
+def lm_head_cross_entropy(h: Tensor, weight: Tensor, targets: Tensor, ignore_index: int = IGNORE_INDEX) -> Tensor:
+    """``cross_entropy(h @ weight.T, targets)`` without keeping separate logits/probs/grad buffers.
+
+    h: ``[..., d]``, weight: ``[V, d]``, targets: ``[...]``.
+    """
+    d = h.shape[-1]
+    h2 = h.reshape(-1, d)
+    t = targets.reshape(-1).long().contiguous()
+    if h.is_cuda and h.dtype in (torch.float32, torch.bfloat16):
+        return _LMHeadCEFn.apply(h2, weight, t, ignore_index)
+    return cross_entropy(h2 @ weight.t(), t, ignore_index)

@@ -1,0 +1,144 @@
+"""Flat parameter / gradient storage and the one-launch optimizer step.
+
+MI355X-first design: all trainable parameters of the model live in ONE
+contiguous buffer (each ``Parameter`` becomes a view into it) and all gradients
+in ONE contiguous buffer laid out identically.  That buys:
+
+  * the optimizer step is a handful of grid-stride launches over HBM
+    (``FlatAdamW``), independent of the number of tensors;
+  * gradient clipping is one two-stage reduction over one buffer, and its
+    coefficient feeds the AdamW kernel on the device (no host sync);
+  * data-parallel gradient buckets are plain slices of the flat gradient
+    buffer, so bucketed RCCL all-reduces need no flatten/unflatten copies
+    (``parallel.ddp``).
+
+Parameters are packed in registration order, each starting at a 64-element
+aligned offset (16-byte vector alignment for every kernel; padding stays 0).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+from torch import Tensor, nn
+
+from ..ops.optim import fused_adamw_step, grad_norm
+
+ALIGN = 64
+
+
+@dataclass
+class Slot:
+    name: str
+    param: nn.Parameter
+    offset: int
+    numel: int
+
+
+class FlatParameters:
+    def __init__(self, named_params: list[tuple[str, nn.Parameter]], grad_dtype: torch.dtype | None = None):
+        assert named_params, "no parameters"
+        dtypes = {p.dtype for _, p in named_params}
+        devices = {p.device for _, p in named_params}
+        assert len(dtypes) == 1 and len(devices) == 1, "flat buffers need one dtype and one device"
+        self.dtype = dtypes.pop()
+        self.device = devices.pop()
+        self.slots: list[Slot] = []
+        off = 0
+        for name, p in named_params:
+            n = p.numel()
+            self.slots.append(Slot(name, p, off, n))
+            off += (n + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.data = torch.zeros(off, dtype=self.dtype, device=self.device)
+        self.grad = torch.zeros(off, dtype=grad_dtype or self.dtype, device=self.device)
+        with torch.no_grad():
+            for s in self.slots:
+                view = self.data[s.offset : s.offset + s.numel].view_as(s.param)
+                view.copy_(s.param.data)
+                s.param.data = view
+                s.param.grad = self.grad[s.offset : s.offset + s.numel].view_as(s.param)
+
+    @classmethod
+    def from_module(cls, module: nn.Module, grad_dtype: torch.dtype | None = None) -> "FlatParameters":
+        return cls([(n, p) for n, p in module.named_parameters() if p.requires_grad], grad_dtype)
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+        for s in self.slots:  # re-attach in case someone set .grad = None
+            if s.param.grad is None or s.param.grad.data_ptr() != self.grad[s.offset :].data_ptr():
+                s.param.grad = self.grad[s.offset : s.offset + s.numel].view_as(s.param)
+
+    def grad_view(self, slot: Slot) -> Tensor:
+        return self.grad[slot.offset : slot.offset + slot.numel]
+
+
+class FlatAdamW:
+    """AdamW over a :class:`FlatParameters` with fp32 master weights and moments.
+
+    Weight decay is applied to params with ``ndim >= 2`` by default (norm gains
+    are not decayed); set ``decay_all=True`` for uniform decay.  Consecutive
+    params with the same decay form one kernel launch.
+    """
+
+    def __init__(self, flat: FlatParameters, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.01, decay_all: bool = False):
+        self.flat = flat
+        self.lr = lr
+        self.betas = betas
+        self.eps = eps
+        self.weight_decay = weight_decay
+        self.step_count = 0
+        self.master = flat.data.float() if flat.dtype != torch.float32 else flat.data
+        self.exp_avg = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
+        self.exp_avg_sq = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
+        # contiguous runs of equal weight decay
+        self.segments: list[tuple[int, int, float]] = []
+        for i, s in enumerate(flat.slots):
+            wd = weight_decay if (decay_all or s.param.dim() >= 2) else 0.0
+            end = flat.slots[i + 1].offset if i + 1 < len(flat.slots) else flat.numel
+            if self.segments and self.segments[-1][2] == wd and self.segments[-1][1] == s.offset:
+                self.segments[-1] = (self.segments[-1][0], end, wd)
+            else:
+                self.segments.append((s.offset, end, wd))
+
+    @torch.no_grad()
+    def clip_grad_norm(self, max_norm: float) -> tuple[Tensor, Tensor]:
+        """Returns (norm, coef) as device scalars; the coef is applied inside :meth:`step`."""
+        return grad_norm([self.flat.grad], max_norm)
+
+    @torch.no_grad()
+    def step(self, lr: float | None = None, grad_scale: Tensor | None = None) -> None:
+        if lr is not None:
+            self.lr = lr
+        self.step_count += 1
+        b1, b2 = self.betas
+        out = self.flat.data if self.flat.dtype == torch.bfloat16 else None
+        for s, e, wd in self.segments:
+            fused_adamw_step(
+                self.master[s:e], self.exp_avg[s:e], self.exp_avg_sq[s:e], self.flat.grad[s:e],
+                out[s:e] if out is not None else None, self.lr, b1, b2, self.eps, wd, self.step_count, grad_scale,
+            )
+        if out is None and self.master is not self.flat.data:
+            self.flat.data.copy_(self.master)
+
+    def state_dict(self) -> dict:
+        return {
+            "step": self.step_count, "lr": self.lr, "betas": tuple(self.betas), "eps": self.eps,
+            "weight_decay": self.weight_decay, "master": self.master, "exp_avg": self.exp_avg,
+            "exp_avg_sq": self.exp_avg_sq,
+        }
+
+    @torch.no_grad()
+    def load_state_dict(self, sd: dict) -> None:
+        self.step_count = int(sd["step"])
+        self.lr = float(sd["lr"])
+        self.betas = tuple(sd["betas"])
+        self.eps = float(sd["eps"])
+        self.weight_decay = float(sd["weight_decay"])
+        self.master.copy_(sd["master"])
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        if self.master is not self.flat.data:
+            self.flat.data.copy_(self.master)

@@ -1,0 +1,79 @@
+"""The training step engine shared by the trainer loop and ``bench.py``.
+
+One step = (micro-batches of) fused forward + LM-head/CE -> backward with the
+bucketed RCCL all-reduce overlapping it -> global-norm clip (coefficient kept
+on the device) -> one flat fused-AdamW pass writing fp32 master + bf16 weights.
+Nothing in the step synchronises the host; the returned loss is a device
+tensor.
+
+Reference: the reference implies this step only through its test utilities
+(``tests/test_optimizer.py:18-25``, ``tests/adapters.py:401-542``).
+"""
+
+from __future__ import annotations
+
+from contextlib import nullcontext
+
+import torch
+from torch import Tensor, nn
+
+from ..optim.flat import FlatAdamW, FlatParameters
+from ..parallel.ddp import BucketedAllReduce
+from ..parallel.dist import DistInfo
+
+
+class TrainEngine:
+    def __init__(
+        self,
+        model: nn.Module,
+        dist_info: DistInfo | None = None,
+        lr: float = 3e-4,
+        betas=(0.9, 0.95),
+        eps: float = 1e-8,
+        weight_decay: float = 0.1,
+        max_grad_norm: float | None = 1.0,
+        bucket_mb: float = 64.0,
+    ):
+        self.model = model
+        self.dist = dist_info or DistInfo()
+        self.flat = FlatParameters.from_module(model)
+        self.opt = FlatAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        self.max_grad_norm = max_grad_norm
+        self.ddp = BucketedAllReduce(self.flat, bucket_mb=bucket_mb) if self.dist.world_size > 1 else None
+        if self.ddp is not None:
+            self.ddp.broadcast_parameters(0)
+            self.opt.master.copy_(self.flat.data)  # keep fp32 master == broadcast weights
+        self.last_grad_norm: Tensor | None = None
+
+    def train_step(self, batches: list[tuple[Tensor, Tensor]], lr: float | None = None) -> Tensor:
+        """Run one optimizer step over ``batches`` (gradient accumulation when > 1).
+
+        Returns the mean loss as a 0-dim device tensor (no host sync).
+        """
+        self.model.train()
+        self.flat.grad.zero_()
+        n = len(batches)
+        total = None
+        for i, (x, y) in enumerate(batches):
+            last = i == n - 1
+            if self.ddp is not None and last:
+                self.ddp.start()
+            ctx = self.ddp.no_sync() if (self.ddp is not None and not last) else nullcontext()
+            with ctx:
+                loss = self.model.loss(x, y)
+                (loss / n if n > 1 else loss).backward()
+            total = loss.detach() if total is None else total + loss.detach()
+        if self.ddp is not None:
+            self.ddp.finish()
+        coef = None
+        if self.max_grad_norm is not None and self.max_grad_norm > 0:
+            norm, coef = self.opt.clip_grad_norm(self.max_grad_norm)
+            self.last_grad_norm = norm
+        self.opt.step(lr, coef)
+        return total / n if n > 1 else total
+
+    def state_dict(self) -> dict:
+        return self.opt.state_dict()
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.opt.load_state_dict(sd)

@@ -1,0 +1,286 @@
+"""gfx950 HIP kernels vs plain-PyTorch fp32 references (forward AND backward).
+
+Every test here runs the hand-written kernel (``torch.ops.bpe_hip.*``) on the
+GPU and compares it against the same op computed in fp32 by the oracle in
+``bpe_transformer.ops.reference`` from the SAME (rounded) inputs.
+"""
+
+from __future__ import annotations
+
+import math
+
+import pytest
+import torch
+
+from bpe_transformer import ops
+from bpe_transformer.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a: torch.Tensor, b: torch.Tensor) -> float:
+    a, b = a.float(), b.float()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+def _ref_grads(fn, inputs, dout):
+    xs = [x.detach().float().cpu().requires_grad_(True) for x in inputs]
+    y = fn(*xs)
+    y.backward(dout.float().cpu())
+    return y.detach(), [x.grad for x in xs]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(64, 768), (3, 5, 2048), (7, 512)])
+def test_rmsnorm(gpu_device, dtype, shape):
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device=gpu_device, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(shape[-1], device=gpu_device, dtype=dtype)).requires_grad_(True)
+    y = ops.rmsnorm(x, w, 1e-5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr, (gx, gw) = _ref_grads(lambda a, b: R.rmsnorm(a, b, 1e-5), [x, w], dy)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(y.cpu(), yr) < tol
+    assert rel(x.grad.cpu(), gx) < tol * 2
+    assert rel(w.grad.cpu(), gw) < tol * 2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_swiglu_gate(gpu_device, dtype):
+    torch.manual_seed(0)
+    gu = torch.randn(33, 2 * 256, device=gpu_device, dtype=dtype, requires_grad=True)
+    a = ops.swiglu_gate(gu)
+    d = torch.randn_like(a)
+    a.backward(d)
+    ar, (g,) = _ref_grads(lambda t: R.silu(t[:, :256]) * t[:, 256:], [gu], d)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(a.cpu(), ar) < tol
+    assert rel(gu.grad.cpu(), g) < tol * 2
+
+
+@pytest.mark.parametrize("kind", ["silu", "gelu"])
+def test_activations(gpu_device, kind):
+    torch.manual_seed(0)
+    x = (4 * torch.randn(1024, device=gpu_device)).requires_grad_(True)
+    f = ops.silu if kind == "silu" else ops.gelu
+    fr = R.silu if kind == "silu" else R.gelu_tanh
+    y = f(x)
+    d = torch.randn_like(y)
+    y.backward(d)
+    yr, (g,) = _ref_grads(fr, [x], d)
+    assert rel(y.cpu(), yr) < 1e-5
+    assert rel(x.grad.cpu(), g) < 1e-4
+    # overflow-safe tanh: the reference Triton kernel returns NaN here
+    big = torch.tensor([100.0, 1e4, -1e4], device=gpu_device)
+    assert torch.isfinite(ops.gelu(big)).all()
+
+
+@pytest.mark.parametrize("V", [50257, 1000, 8])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cross_entropy(gpu_device, V, dtype):
+    torch.manual_seed(0)
+    x = torch.randn(37, V, device=gpu_device, dtype=dtype, requires_grad=True)
+    t = torch.randint(0, V, (37,), device=gpu_device)
+    loss = ops.cross_entropy(x, t)
+    loss.backward()
+    xr = x.detach().float().cpu().requires_grad_(True)
+    lr_ = torch.nn.functional.cross_entropy(xr, t.cpu())
+    lr_.backward()
+    assert abs(loss.item() - lr_.item()) < (1e-5 if dtype == torch.float32 else 2e-2)
+    assert rel(x.grad.cpu(), xr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+    # large-logit stability (tests/test_nn_utils.py:53 in the reference)
+    big = 1000.0 * torch.rand(8, 5, device=gpu_device)
+    tb = torch.randint(0, 5, (8,), device=gpu_device)
+    ref = torch.nn.functional.cross_entropy(big.cpu(), tb.cpu())
+    assert abs(ops.cross_entropy(big, tb).item() - ref.item()) < 1e-3
+
+
+def test_cross_entropy_ignore_index(gpu_device):
+    torch.manual_seed(0)
+    x = torch.randn(16, 100, device=gpu_device, requires_grad=True)
+    t = torch.randint(0, 100, (16,), device=gpu_device)
+    t[::3] = -100
+    loss = ops.cross_entropy(x, t)
+    loss.backward()
+    xr = x.detach().cpu().requires_grad_(True)
+    lr_ = torch.nn.functional.cross_entropy(xr, t.cpu(), ignore_index=-100)
+    lr_.backward()
+    assert abs(loss.item() - lr_.item()) < 1e-5
+    assert rel(x.grad.cpu(), xr.grad) < 1e-4
+
+
+def test_lm_head_cross_entropy(gpu_device):
+    torch.manual_seed(0)
+    h = torch.randn(64, 256, device=gpu_device, dtype=torch.bfloat16, requires_grad=True)
+    w = (0.05 * torch.randn(50257, 256, device=gpu_device, dtype=torch.bfloat16)).requires_grad_(True)
+    t = torch.randint(0, 50257, (64,), device=gpu_device)
+    loss = ops.lm_head_cross_entropy(h, w, t)
+    (2.0 * loss).backward()
+    hr = h.detach().float().cpu().requires_grad_(True)
+    wr = w.detach().float().cpu().requires_grad_(True)
+    lr_ = torch.nn.functional.cross_entropy(hr @ wr.t(), t.cpu())
+    (2.0 * lr_).backward()
+    assert abs(loss.item() - lr_.item()) < 2e-2
+    assert rel(h.grad.cpu(), hr.grad) < 3e-2
+    assert rel(w.grad.cpu(), wr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_embedding(gpu_device, dtype):
+    torch.manual_seed(0)
+    W = torch.randn(1000, 768, device=gpu_device, dtype=dtype, requires_grad=True)
+    ids = torch.randint(0, 50, (4, 300), device=gpu_device)  # many repeats
+    y = ops.embedding(W, ids)
+    d = torch.randn_like(y)
+    y.backward(d)
+    Wr = W.detach().float().cpu().requires_grad_(True)
+    yr = Wr[ids.cpu()]
+    yr.backward(d.float().cpu())
+    assert torch.equal(y.float().cpu(), yr.detach())
+    assert rel(W.grad.cpu(), Wr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+    # deterministic: a second backward gives bitwise-identical gradients
+    g1 = W.grad.clone()
+    W.grad = None
+    ops.embedding(W, ids).backward(d)
+    assert torch.equal(W.grad, g1)
+
+
+def test_softmax(gpu_device):
+    x = torch.tensor([[0.4655, 0.8303, 0.9608, 0.9656, 0.6840], [0.2583, 0.2198, 0.9334, 0.2995, 0.1722]],
+                     device=gpu_device)
+    exp = torch.softmax(x.cpu(), -1)
+    assert torch.allclose(ops.softmax(x, -1).cpu(), exp, atol=1e-6)
+    assert torch.allclose(ops.softmax(x + 100, -1).cpu(), exp, atol=1e-6)
+    z = torch.randn(3, 7, 11, device=gpu_device, requires_grad=True)
+    y = ops.softmax(z, dim=1)
+    d = torch.randn_like(y)
+    y.backward(d)
+    zr = z.detach().cpu().requires_grad_(True)
+    yr = torch.softmax(zr, 1)
+    yr.backward(d.cpu())
+    assert rel(y.cpu(), yr.detach()) < 1e-5 and rel(z.grad.cpu(), zr.grad) < 1e-4
+
+
+def test_rope(gpu_device):
+    torch.manual_seed(0)
+    cos, sin = R.rope_tables(64, 512, 10000.0, device=gpu_device)
+    x = torch.randn(2, 4, 100, 64, device=gpu_device, requires_grad=True)
+    pos = torch.randint(0, 512, (2, 1, 100), device=gpu_device)
+    y = ops.apply_rope(x, cos, sin, pos)
+    d = torch.randn_like(y)
+    y.backward(d)
+    yr, (g,) = _ref_grads(lambda t: R.apply_rope(t, cos.cpu(), sin.cpu(), pos.cpu()), [x], d)
+    assert rel(y.cpu(), yr) < 1e-5 and rel(x.grad.cpu(), g) < 1e-5
+
+
+def test_adamw_matches_torch(gpu_device):
+    from bpe_transformer.optim import AdamW
+
+    torch.manual_seed(0)
+    p1 = torch.randn(1001, device=gpu_device, requires_grad=True)
+    p2 = p1.detach().clone().requires_grad_(True)
+    o1 = AdamW([p1], lr=1e-2, weight_decay=0.1, betas=(0.9, 0.95), eps=1e-8)
+    o2 = torch.optim.AdamW([p2], lr=1e-2, weight_decay=0.1, betas=(0.9, 0.95), eps=1e-8)
+    for _ in range(20):
+        g = torch.randn_like(p1)
+        p1.grad = g.clone()
+        p2.grad = g.clone()
+        o1.step()
+        o2.step()
+    assert rel(p1.detach(), p2.detach()) < 1e-5
+
+
+def test_flat_adamw_bf16_master(gpu_device):
+    from bpe_transformer.optim import FlatAdamW, FlatParameters
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(64, 33, bias=True).to(gpu_device, torch.bfloat16)
+    ref = [p.detach().float().clone().requires_grad_(True) for p in lin.parameters()]
+    flat = FlatParameters.from_module(lin)
+    opt = FlatAdamW(flat, lr=1e-3, weight_decay=0.0)
+    oref = torch.optim.AdamW(ref, lr=1e-3, weight_decay=0.0)
+    for _ in range(5):
+        flat.zero_grad()
+        for p, r in zip(lin.parameters(), ref):
+            g = torch.randn_like(r)
+            p.grad.copy_(g.to(torch.bfloat16))
+            r.grad = g.to(torch.bfloat16).float()
+        opt.step()
+        oref.step()
+    for p, r in zip(lin.parameters(), ref):
+        assert rel(p.detach(), r.detach().to(torch.bfloat16)) < 1e-2
+
+
+def test_grad_norm_clip(gpu_device):
+    torch.manual_seed(0)
+    ts = [torch.randn(n, device=gpu_device) for n in (5, 1000, 3333)]
+    norm, coef = ops.grad_norm(ts, 1.0)
+    exp = torch.sqrt(sum((t.cpu() ** 2).sum() for t in ts))
+    assert abs(norm.item() - exp.item()) / exp.item() < 1e-5
+    assert abs(coef.item() - 1.0 / (exp.item() + 1e-6)) < 1e-6
+    params = [torch.nn.Parameter(t.clone()) for t in ts]
+    refs = [torch.nn.Parameter(t.cpu().clone()) for t in ts]
+    for p, r in zip(params, refs):
+        p.grad = p.detach().clone()
+        r.grad = r.detach().clone()
+    ops.clip_grad_norm_(params, 1e-2)
+    torch.nn.utils.clip_grad_norm_(refs, 1e-2)
+    for p, r in zip(params, refs):
+        assert rel(p.grad.cpu(), r.grad) < 1e-5
+
+
+# ---------------------------------------------------------------- flash attention
+def _fa_case(gpu_device, B, S, H, Hkv, D, rope, causal, seed=0):
+    torch.manual_seed(seed)
+    W = (H + 2 * Hkv) * D
+    qkv = torch.randn(B * S, W, device=gpu_device, dtype=torch.bfloat16).requires_grad_(True)
+    cos = sin = None
+    if rope:
+        cos, sin = R.rope_tables(D, S + 16, 10000.0, device=gpu_device)
+    o = ops.flash_attention_qkv(qkv, B, S, H, Hkv, D, cos, sin, causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr = qkv.detach().float().cpu().requires_grad_(True)
+    orf = ops.attention_qkv_reference(qr, B, S, H, Hkv, D, None if cos is None else cos.cpu(),
+                                      None if sin is None else sin.cpu(), causal)
+    orf.backward(do.float().cpu())
+    return o, qkv.grad, orf.detach(), qr.grad
+
+
+@pytest.mark.parametrize("S", [128, 256, 200, 64])
+@pytest.mark.parametrize("rope", [True, False])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_d64(gpu_device, S, rope, causal):
+    o, g, orf, gr = _fa_case(gpu_device, 2, S, 4, 4, 64, rope, causal)
+    assert rel(o.cpu(), orf) < 2e-2, rel(o.cpu(), orf)
+    HD = 4 * 64
+    for name, sl in (("dq", slice(0, HD)), ("dk", slice(HD, 2 * HD)), ("dv", slice(2 * HD, 3 * HD))):
+        e = rel(g[:, sl].cpu(), gr[:, sl])
+        assert e < 3e-2, (name, e)
+
+
+@pytest.mark.parametrize("D,H,Hkv", [(128, 4, 4), (64, 8, 2)])
+def test_flash_attention_d128_and_gqa(gpu_device, D, H, Hkv):
+    o, g, orf, gr = _fa_case(gpu_device, 2, 192, H, Hkv, D, True, True, seed=1)
+    assert rel(o.cpu(), orf) < 2e-2
+    assert rel(g.cpu(), gr) < 3e-2
+
+
+def test_flash_attention_gpt2_shape(gpu_device):
+    o, g, orf, gr = _fa_case(gpu_device, 1, 1024, 12, 12, 64, True, True, seed=2)
+    assert rel(o.cpu(), orf) < 2e-2
+    assert rel(g.cpu(), gr) < 3e-2
+
+
+def test_flash_attention_large_scores(gpu_device):
+    """Spike one key so the running max jumps mid-sequence (forces the online-softmax rescale)."""
+    torch.manual_seed(3)
+    B, S, H, D = 1, 256, 2, 64
+    qkv = torch.randn(B * S, 3 * H * D, device=gpu_device, dtype=torch.bfloat16)
+    qkv[100, H * D : 2 * H * D] *= 8  # key row 100 large
+    qkv[:, : H * D] *= 3
+    qkv.requires_grad_(True)
+    o = ops.flash_attention_qkv(qkv, B, S, H, H, D, None, None, True)
+    orf = ops.attention_qkv_reference(qkv.detach().float().cpu(), B, S, H, H, D, None, None, True)
+    assert rel(o.detach().cpu(), orf) < 2e-2
