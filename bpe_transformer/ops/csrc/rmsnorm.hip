@@ -125,14 +125,28 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ 
     }
 }
 
+// Column sum of the per-block partials [rows, N] -> dw [N]: 16 waves per block,
+// lane = column (coalesced 256-B rows), waves split the rows, fixed-order LDS
+// combine (deterministic).
 template <typename T>
-__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ partial, T* __restrict__ out,
-                                                     int rows, int N) {
-    const int col = blockIdx.x * 256 + threadIdx.x;
-    if (col >= N) return;
+__global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ partial, T* __restrict__ out,
+                                                      int rows, int N) {
+    __shared__ float red[16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int col = blockIdx.x * 64 + lane;
     float s = 0.f;
-    for (int r = 0; r < rows; ++r) s += partial[(size_t)r * N + col];
-    st1<T>(out + col, s);
+    if (col < N) {
+#pragma unroll 8
+        for (int r = w; r < rows; r += 16) s += partial[(size_t)r * N + col];
+    }
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && col < N) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t += red[i][lane];
+        st1<T>(out + col, t);
+    }
 }
 
 }  // namespace bpe
@@ -167,7 +181,7 @@ static void rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* r
 
 int rmsnorm_bwd_grid(int M) {
     int g = (M + 3) / 4;
-    return g < 512 ? g : 512;
+    return g < 256 ? g : 256;
 }
 
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
@@ -176,10 +190,10 @@ void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w,
     if (dtype == DT_BF16) {
         rms_bwd_dispatch<__bf16>((const __bf16*)dy, (const __bf16*)x, (const __bf16*)w, rstd, (__bf16*)dx, partial,
                                  grid, M, N, s);
-        colsum_kernel<__bf16><<<(N + 255) / 256, 256, 0, s>>>(partial, (__bf16*)dw, grid, N);
+        colsum_kernel<__bf16><<<(N + 63) / 64, 1024, 0, s>>>(partial, (__bf16*)dw, grid, N);
     } else {
         rms_bwd_dispatch<float>((const float*)dy, (const float*)x, (const float*)w, rstd, (float*)dx, partial, grid,
                                 M, N, s);
-        colsum_kernel<float><<<(N + 255) / 256, 256, 0, s>>>(partial, (float*)dw, grid, N);
+        colsum_kernel<float><<<(N + 63) / 64, 1024, 0, s>>>(partial, (float*)dw, grid, N);
     }
 }

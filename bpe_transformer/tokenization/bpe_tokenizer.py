@@ -1,0 +1,201 @@
+"""Byte-level BPE encoder / decoder (reference: ``bpe_transformer/tokenization/bpe_tokenizer.py``).
+
+Public surface of the reference ``BPETokenizer`` (:9): constructor (:38),
+``vocab``/``merges``/``special_tokens`` (:62-75), ``from_files`` (:88),
+``decode`` (:119), ``encode`` (:139), ``load_vocab``/``load_merges`` (:292-337),
+``encode_iterable(iterable, n_workers)`` (:339); plus ``encode_batch`` and
+``encode_file`` (threaded, return numpy for dataset building).
+
+The merge loop is the C++ core: rank-ordered merges on a linked list with a
+min-heap per pre-token (O(n log n); the reference rescans all pairs per merge,
+O(n^2)) and a pre-token cache.  Parallel encoding uses C++ threads on shared
+read-only tables (the reference pickled the whole tokenizer per task and ran
+17x slower than serial).
+
+``encode_iterable`` cuts its buffer only at positions where the
+pre-tokenisation provably cannot change (a lone non-space whitespace
+character between two non-whitespace characters, never inside a special
+token), so streaming output equals ``encode`` of the whole text (the
+reference cut at every newline and could split whitespace tokens).
+"""
+
+from __future__ import annotations
+
+from collections.abc import Iterable, Iterator
+from functools import lru_cache
+from multiprocessing import cpu_count
+from pathlib import Path
+
+import numpy as np
+import regex
+
+from ..settings import ENCODING_STD
+from . import serialization
+from ._native import native
+from .tokenizer import Tokenizer
+
+_SPACE_RX = regex.compile(r"\s")
+_CUT_CHARS = "\n\r\t\x0b\x0c"
+
+
+@lru_cache(maxsize=4096)
+def _is_space(ch: str) -> bool:
+    return _SPACE_RX.match(ch) is not None
+
+
+class BPETokenizer(Tokenizer):
+    def __init__(self, vocab: dict[int, bytes], merges: list[tuple[bytes, bytes]],
+                 special_tokens: list[str] | None = None):
+        self._vocab = dict(vocab)
+        self._merges = list(merges)
+        specials: list[str] = []
+        for s in special_tokens or []:
+            if s not in specials:
+                specials.append(s)
+        self._special_tokens = specials
+        have = set(self._vocab.values())
+        nxt = max(self._vocab) + 1 if self._vocab else 0
+        for s in specials:
+            b = s.encode(ENCODING_STD)
+            if b not in have:
+                self._vocab[nxt] = b
+                have.add(b)
+                nxt += 1
+        self._native = native.Encoder(self._vocab, self._merges, specials)
+        self._bytes_to_id_cache: dict[bytes, int] | None = None
+        self._max_special = max((len(s) for s in specials), default=0)
+
+    # ------------------------------------------------------------ properties
+    @property
+    def vocab(self) -> dict[int, bytes]:
+        return self._vocab
+
+    @property
+    def merges(self) -> list[tuple[bytes, bytes]]:
+        return self._merges
+
+    @property
+    def special_tokens(self) -> list[str]:
+        return list(self._special_tokens)
+
+    @property
+    def _bytes_to_id(self) -> dict[bytes, int]:
+        if self._bytes_to_id_cache is None:
+            self._bytes_to_id_cache = {v: k for k, v in self._vocab.items()}
+        return self._bytes_to_id_cache
+
+    # ------------------------------------------------------------ files
+    @classmethod
+    def from_files(cls, vocab_filepath: Path | str, merges_filepath: Path | str,
+                   special_tokens: list[str] | None = None) -> "BPETokenizer":
+        return cls(vocab=cls.load_vocab(vocab_filepath, special_tokens), merges=cls.load_merges(merges_filepath),
+                   special_tokens=special_tokens)
+
+    @classmethod
+    def from_gpt2_files(cls, vocab_json: Path | str, merges_txt: Path | str,
+                        special_tokens: list[str] | None = None) -> "BPETokenizer":
+        vocab, merges = serialization.load_gpt2_files(vocab_json, merges_txt, special_tokens)
+        return cls(vocab, merges, special_tokens)
+
+    @staticmethod
+    def load_vocab(file_path: Path | str, special_tokens: list[str] | None = None) -> dict[int, bytes]:
+        """Load ``vocab.pkl`` (restricted unpickler) and append missing specials at ``len(vocab)``."""
+        vocab = serialization.load_vocab(file_path)
+        if special_tokens:
+            have = set(vocab.values())
+            for t in special_tokens:
+                b = t.encode(ENCODING_STD)
+                if b not in have:
+                    vocab[len(vocab)] = b
+                    have.add(b)
+        return vocab
+
+    @staticmethod
+    def load_merges(file_path: Path | str) -> list[tuple[bytes, bytes]]:
+        return serialization.load_merges(file_path)
+
+    def save(self, output_dir: Path | str) -> None:
+        out = Path(output_dir)
+        out.mkdir(parents=True, exist_ok=True)
+        serialization.save_vocab(self._vocab, out / "vocab.pkl")
+        serialization.save_merges(self._merges, out / "merges.pkl")
+
+    # ------------------------------------------------------------ encode / decode
+    def encode(self, text: str) -> list[int]:
+        return self._native.encode(text.encode(ENCODING_STD))
+
+    def encode_batch(self, texts: list[str], n_workers: int | None = None) -> list[list[int]]:
+        n = n_workers or cpu_count()
+        return self._native.encode_batch([t.encode(ENCODING_STD) for t in texts], int(n))
+
+    def encode_file(self, path: Path | str, n_workers: int | None = None) -> np.ndarray:
+        """Encode a whole utf-8 file with threads; returns int32 token ids."""
+        return self._native.encode_file(str(path), int(n_workers or cpu_count()))
+
+    def decode(self, ids: list[int]) -> str:
+        """Concatenate token bytes (unknown ids -> U+FFFD) and decode utf-8 with replacement."""
+        return self._native.decode([int(i) for i in ids]).decode(ENCODING_STD, errors="replace")
+
+    def decode_bytes(self, ids: list[int]) -> bytes:
+        return self._native.decode([int(i) for i in ids])
+
+    # ------------------------------------------------------------ streaming
+    def _inside_special(self, text: str, cut: int) -> bool:
+        if not self._special_tokens:
+            return False
+        window = text[max(0, cut - self._max_special + 1): cut + self._max_special - 1]
+        off = max(0, cut - self._max_special + 1)
+        for s in self._special_tokens:
+            start = 0
+            while True:
+                p = window.find(s, start)
+                if p < 0:
+                    break
+                if off + p < cut < off + p + len(s):
+                    return True
+                start = p + 1
+        return False
+
+    def _safe_cut(self, text: str, lo: int = 0) -> int:
+        """Largest p > lo such that encode(text[:p]) + encode(text[p:]) == encode(text), else -1."""
+        p = len(text) - 1
+        while p >= max(lo, 2):
+            # last candidate whitespace char at p-1
+            q = max(text.rfind(c, 0, p) for c in _CUT_CHARS)
+            if q < 1:
+                return -1
+            p = q + 1
+            if p < len(text) and not _is_space(text[p]) and not _is_space(text[p - 2]) \
+                    and not self._inside_special(text, p):
+                return p
+            p -= 1
+        return -1
+
+    def encode_iterable(self, iterable: Iterable[str], n_workers: int | None = None) -> Iterator[int]:
+        """Lazily encode an iterable of strings (e.g. a file object); memory stays O(chunk)."""
+        parallel = n_workers is not None and n_workers > 1
+        buf = ""
+        batch: list[str] = []
+        batch_chars = 0
+        for chunk in iterable:
+            buf += chunk
+            if len(buf) < 1024 and "\n" not in chunk:
+                continue
+            cut = self._safe_cut(buf)
+            if cut <= 0:
+                continue
+            piece, buf = buf[:cut], buf[cut:]
+            if not parallel:
+                yield from self.encode(piece)
+                continue
+            batch.append(piece)
+            batch_chars += len(piece)
+            if batch_chars >= (1 << 22):
+                for ids in self.encode_batch(batch, n_workers):
+                    yield from ids
+                batch, batch_chars = [], 0
+        if batch:
+            for ids in self.encode_batch(batch, n_workers):
+                yield from ids
+        if buf:
+            yield from self.encode(buf)

@@ -1,0 +1,160 @@
+"""BPE encode / decode: GPT-2 parity, round trips, specials, streaming, artifacts.
+
+The reference checks parity against ``tiktoken`` (``tests/test_tokenizer.py``),
+which cannot be installed offline; ``tests/gpt2_oracle.py`` is an independent
+pure-Python GPT-2 BPE over the same vocab/merges fixtures.
+"""
+
+from __future__ import annotations
+
+import io
+import pickle
+
+import pytest
+
+from bpe_transformer.tokenization import BPETokenizer
+from bpe_transformer.tokenization.serialization import load_gpt2_files
+
+from .adapters import get_tokenizer
+from .conftest import FIXTURES
+from .gpt2_oracle import GPT2Oracle
+
+EOT = "<|endoftext|>"
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return GPT2Oracle()
+
+
+@pytest.fixture(scope="module")
+def gpt2_files():
+    return load_gpt2_files(FIXTURES / "gpt2_vocab.json", FIXTURES / "gpt2_merges.txt", [EOT])
+
+
+@pytest.fixture(scope="module")
+def tok(gpt2_files):
+    return get_tokenizer(*gpt2_files, special_tokens=[EOT])
+
+
+@pytest.fixture(scope="module")
+def tok_plain():
+    return get_tokenizer(*load_gpt2_files(FIXTURES / "gpt2_vocab.json", FIXTURES / "gpt2_merges.txt"))
+
+
+STRINGS = [
+    "", "s", "🙃", "Hello, how are you?", "Héllò hôw are ü? 🙃",
+    "Hello, how <|endoftext|><|endoftext|> are you?<|endoftext|>",
+    "x  \n\n y\n", "  leading and trailing  ", "tabs\tand\r\nCRLF\n\n\n", "numbers 12345 and ١٢٣ and ²",
+    "don't can't we'll they've you're I'm he'd", "'s 's''s", "日本語のテキスト", "a" * 300, " " * 50 + "x",
+]
+
+
+@pytest.mark.parametrize("text", STRINGS)
+def test_roundtrip(tok, text):
+    assert tok.decode(tok.encode(text)) == text
+
+
+@pytest.mark.parametrize("text", [s for s in STRINGS if EOT not in s])
+def test_matches_gpt2_without_specials(tok_plain, oracle, text):
+    assert tok_plain.encode(text) == oracle.encode(text)
+
+
+@pytest.mark.parametrize("text", STRINGS)
+def test_matches_gpt2_with_specials(tok, oracle, text):
+    assert tok.encode(text) == oracle.encode(text, allowed_special={EOT})
+
+
+@pytest.mark.parametrize("name", ["address.txt", "german.txt", "tinystories_sample.txt",
+                                  "special_token_trailing_newlines.txt",
+                                  "special_token_double_newlines_non_whitespace.txt", "corpus.en"])
+def test_fixture_files_match_gpt2(tok, oracle, name):
+    text = (FIXTURES / name).read_text(encoding="utf-8")
+    ids = tok.encode(text)
+    assert ids == oracle.encode(text, allowed_special={EOT})
+    assert tok.decode(ids) == text
+
+
+def test_overlapping_special_tokens(gpt2_files):
+    vocab, merges = gpt2_files
+    specials = [EOT, EOT + EOT]
+    t = get_tokenizer(dict(vocab), merges, specials)
+    s = "Hello, how <|endoftext|><|endoftext|> are you?<|endoftext|>"
+    ids = t.encode(s)
+    toks = [t.decode([i]) for i in ids]
+    assert toks.count(EOT) == 1 and toks.count(EOT + EOT) == 1
+    assert t.decode(ids) == s
+
+
+def test_special_tokens_kept_whole(tok):
+    ids = tok.encode("a<|endoftext|>b")
+    assert [tok.decode([i]) for i in ids] == ["a", EOT, "b"]
+
+
+@pytest.mark.parametrize("name", ["tinystories_sample.txt", "german.txt", "address.txt", "corpus.en"])
+@pytest.mark.parametrize("workers", [None, 4])
+def test_encode_iterable_equals_encode(tok, name, workers):
+    path = FIXTURES / name
+    whole = tok.encode(path.read_text(encoding="utf-8"))
+    with open(path, encoding="utf-8") as f:
+        assert list(tok.encode_iterable(f, n_workers=workers)) == whole
+
+
+def test_encode_iterable_whitespace_boundary(tok):
+    """The reference's streaming encode split '\\n\\n' across lines."""
+    text = "x  \n\n y\n"
+    assert list(tok.encode_iterable(io.StringIO(text))) == tok.encode(text)
+    lines = ["x  \n", "\n", " y\n"]
+    assert list(tok.encode_iterable(lines)) == tok.encode(text)
+
+
+def test_encode_iterable_specials_split_across_chunks(tok):
+    text = "one\nmore <|endoftext|>\nline\n" * 50
+    pieces = [text[i:i + 3] for i in range(0, len(text), 3)]
+    assert list(tok.encode_iterable(pieces)) == tok.encode(text)
+
+
+def test_encode_batch_and_file(tok):
+    import numpy as np
+
+    texts = [(FIXTURES / n).read_text(encoding="utf-8") for n in ("german.txt", "address.txt")]
+    assert tok.encode_batch(texts, 2) == [tok.encode(t) for t in texts]
+    arr = tok.encode_file(FIXTURES / "corpus.en", 4)
+    assert isinstance(arr, np.ndarray)
+    assert arr.tolist() == tok.encode((FIXTURES / "corpus.en").read_text(encoding="utf-8"))
+
+
+def test_decode_unknown_id(tok):
+    assert tok.decode([99999999]) == "�"
+
+
+def test_from_files_roundtrip(tmp_path, gpt2_files):
+    vocab, merges = gpt2_files
+    t = BPETokenizer(vocab, merges, [EOT])
+    t.save(tmp_path)
+    t2 = BPETokenizer.from_files(tmp_path / "vocab.pkl", tmp_path / "merges.pkl", [EOT, "<|pad|>"])
+    s = "Hi <|pad|> there<|endoftext|>"
+    assert t2.decode(t2.encode(s)) == s
+    assert t2.encode("Hello world") == t.encode("Hello world")
+
+
+def test_restricted_unpickler_refuses_code(tmp_path):
+    class Evil:
+        def __reduce__(self):
+            return (print, ("pwned",))
+
+    p = tmp_path / "vocab.pkl"
+    with open(p, "wb") as f:
+        pickle.dump({0: Evil()}, f)
+    with pytest.raises(pickle.UnpicklingError):
+        BPETokenizer.load_vocab(p)
+
+
+def test_trained_tokenizer_end_to_end(tmp_path):
+    from bpe_transformer import train_bpe
+
+    vocab, merges = train_bpe(FIXTURES / "tinystories_sample.txt", 400, [EOT])
+    t = BPETokenizer(vocab, merges, [EOT])
+    text = (FIXTURES / "tinystories_sample.txt").read_text(encoding="utf-8")
+    ids = t.encode(text)
+    assert t.decode(ids) == text and len(ids) < len(text.encode())
