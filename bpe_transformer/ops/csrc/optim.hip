@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float
                                                     const GT* __restrict__ g, __bf16* __restrict__ pout, size_t n,
                                                     AdamArgs a, const float* __restrict__ gscale) {
     const float sc = gscale ? *gscale : 1.f;
+    if (!(sc >= 0.f)) return;  // non-finite gradient norm: the step is skipped on the device (no host sync)
     const size_t n4 = n / 4;
     const size_t stride = (size_t)gridDim.x * 256;
     for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += stride) {
@@ -114,7 +115,8 @@ __global__ void __launch_bounds__(256) norm_finalize_kernel(const float* __restr
         out_norm[0] = nrm;
         if (out_coef) {
             float c = max_norm / (nrm + 1e-6f);
-            out_coef[0] = c < 1.f ? c : 1.f;
+            c = c < 1.f ? c : 1.f;
+            out_coef[0] = isfinite(nrm) ? c : -1.f;  // -1 = "skip this step" sentinel for adamw_kernel
         }
     }
 }
@@ -123,7 +125,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) scale_kernel(T* __restrict__ x, size_t n, const float* __restrict__ coef) {
     constexpr int V = Vec<T>::N;
     const float c = *coef;
-    if (c == 1.f) return;
+    if (c == 1.f || !(c >= 0.f)) return;
     const size_t nv = n / V;
     for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < nv; i += (size_t)gridDim.x * 256) {
         Vec<T> a;

@@ -28,6 +28,7 @@ def grad_norm(tensors: list[Tensor], max_norm: float = float("inf")) -> tuple[Te
         return z, torch.ones(())
     total = torch.sqrt(sum((t.detach().float() ** 2).sum() for t in tensors))
     coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    coef = torch.where(torch.isfinite(total), coef, torch.full_like(coef, -1.0))  # -1: skip-step sentinel
     return total, coef
 
 
@@ -48,7 +49,7 @@ def clip_grad_norm_(parameters: Iterable[torch.nn.Parameter], max_l2_norm: float
                 ops().scale_(g, coef)
             else:
                 g.mul_(coef.to(g.dtype))
-    else:
+    elif bool(coef >= 0):  # coef -1 marks a non-finite norm: leave the gradients as they are
         for g in grads:
             g.mul_(coef.to(g.dtype))
     return norm
@@ -82,6 +83,8 @@ def fused_adamw_step(
         return
     g = grad.float()
     if grad_scale is not None:
+        if not bool(grad_scale >= 0):  # non-finite grad norm: skip (same rule as the kernel)
+            return
         g = g * grad_scale
     param_fp32.mul_(1.0 - lr * weight_decay)
     exp_avg.mul_(beta1).add_(g, alpha=1.0 - beta1)
