@@ -1,0 +1,168 @@
+"""Whole-block forward/backward for the GPU training path (pre-norm, RoPE, SwiGLU, causal).
+
+One ``autograd.Function`` per transformer block instead of ~10 autograd nodes:
+
+forward::
+
+    h1 = rmsnorm(x; ln1)              HIP
+    qkv = h1 @ [Wq;Wk;Wv]^T           hipBLASLt (one GEMM)
+    o = flash_attn(qkv) (+RoPE)       HIP
+    xm = x + o @ Wo^T                 hipBLASLt addmm (residual folded into the GEMM)
+    h2 = rmsnorm(xm; ln2)             HIP
+    gu = h2 @ [W1;W3]^T               hipBLASLt (one GEMM)
+    a = silu(g) * u                   HIP
+    y = xm + a @ W2^T                 hipBLASLt addmm
+
+backward: the mirror image, with
+  * weight gradients ACCUMULATED IN PLACE into the flat gradient buffer
+    (``param.main_grad``, set by the training engine) by ``addmm_`` with
+    beta = 1 -- no temporary dW, no AccumulateGrad add kernels;
+  * the fused [Wq;Wk;Wv] and [W1;W3] weights and their gradients as zero-copy
+    views of the flat buffers when the parameters are adjacent there (no
+    torch.cat / split);
+  * both residual-gradient additions folded into the RMSNorm backward kernel;
+  * a data-parallel "gradient ready" notification per parameter right after
+    its gradient lands, so bucketed all-reduces start while the rest of the
+    backward runs.
+
+Without ``main_grad`` (e.g. a plain module, tests) the same function returns
+ordinary per-parameter gradients.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import Tensor
+
+from ..ops._ext import ops as hip
+from ..ops.gemm import accumulate_weight_grad
+
+
+def _adjacent_view(ts: list[Tensor]) -> Tensor | None:
+    """[t0; t1; ...] along dim 0 as a view if the tensors are consecutive in one storage."""
+    t0 = ts[0]
+    es = t0.element_size()
+    base = t0.untyped_storage().data_ptr()
+    for a, b in zip(ts, ts[1:]):
+        if not (a.is_contiguous() and b.is_contiguous() and a.shape[1:] == b.shape[1:]
+                and b.untyped_storage().data_ptr() == base  # same allocation, not just neighbours
+                and a.data_ptr() + a.numel() * es == b.data_ptr()):
+            return None
+    rows = sum(t.shape[0] for t in ts)
+    return t0.as_strided((rows, *t0.shape[1:]), t0.stride())
+
+
+def _cat_weights(ts: list[Tensor]) -> Tensor:
+    v = _adjacent_view([t.detach() for t in ts])
+    return v if v is not None else torch.cat([t.detach() for t in ts], 0)
+
+
+def _notify(p: Tensor) -> None:
+    cb = getattr(p, "_bpe_grad_ready", None)
+    if cb is not None:
+        cb(p)
+
+
+class FusedBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2, ln1, wq, wk, wv, wo, ln2, w1, w3, w2, cos, sin, meta):
+        B, S, H, Hkv, D, eps, use_rope = meta
+        scale = 1.0 / math.sqrt(D)
+        w_qkv = _cat_weights([wq, wk, wv])
+        w_13 = _cat_weights([w1, w3])
+        h1, r1 = hip().rmsnorm_fwd(x2, ln1, eps)
+        qkv = torch.matmul(h1, w_qkv.t())
+        q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
+        o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale)
+        xm = torch.addmm(x2, o, wo.t())
+        h2, r2 = hip().rmsnorm_fwd(xm, ln2, eps)
+        gu = torch.matmul(h2, w_13.t())
+        a = hip().swiglu_fwd(gu)
+        y = torch.addmm(xm, a, w2.t())
+        ctx.save_for_backward(x2, r1, h1, qkv, o, lse, xm, r2, h2, gu, a, cos, sin)
+        ctx.params = (ln1, wq, wk, wv, wo, ln2, w1, w3, w2)
+        ctx.meta = meta
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, r1, h1, qkv, o, lse, xm, r2, h2, gu, a, cos, sin = ctx.saved_tensors
+        ln1, wq, wk, wv, wo, ln2, w1, w3, w2 = ctx.params
+        B, S, H, Hkv, D, eps, use_rope = ctx.meta
+        scale = 1.0 / math.sqrt(D)
+        dy = dy.contiguous()
+        params = ctx.params
+        main = all(hasattr(p, "main_grad") for p in params)
+        grads: dict[int, Tensor] = {}
+
+        def acc_weight(ps: list[Tensor], g_out: Tensor, x_in: Tensor) -> None:
+            """dW = g_out^T x_in for the row-stacked weights ``ps``."""
+            if main:
+                view = _adjacent_view([p.main_grad for p in ps])
+                if view is not None:
+                    accumulate_weight_grad(view, g_out, x_in)
+                else:
+                    off = 0
+                    for p in ps:
+                        n = p.shape[0]
+                        accumulate_weight_grad(p.main_grad, g_out[:, off : off + n], x_in)
+                        off += n
+                for p in ps:
+                    _notify(p)
+            else:
+                dw = torch.matmul(g_out.t(), x_in)
+                off = 0
+                for p in ps:
+                    n = p.shape[0]
+                    grads[id(p)] = dw[off : off + n]
+                    off += n
+
+        # ---- FFN
+        acc_weight([w2], dy, a)
+        da = torch.matmul(dy, w2.detach())
+        dgu = hip().swiglu_bwd(da, gu)
+        acc_weight([w1, w3], dgu, h2)
+        dh2 = torch.matmul(dgu, _cat_weights([w1, w3]))
+        dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dy)
+        # ---- attention
+        acc_weight([wo], dxm, o)
+        do = torch.matmul(dxm, wo.detach())
+        q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
+        dqkv = hip().fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, use_rope, scale)
+        acc_weight([wq, wk, wv], dqkv, h1)
+        dh1 = torch.matmul(dqkv, _cat_weights([wq, wk, wv]))
+        dx, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm)
+        if main:
+            ln2.main_grad.add_(dln2)
+            ln1.main_grad.add_(dln1)
+            _notify(ln2)
+            _notify(ln1)
+            return (dx,) + (None,) * 12
+        grads[id(ln1)] = dln1
+        grads[id(ln2)] = dln2
+        return (dx, grads[id(ln1)], grads[id(wq)], grads[id(wk)], grads[id(wv)], grads[id(wo)], grads[id(ln2)],
+                grads[id(w1)], grads[id(w3)], grads[id(w2)], None, None, None)
+
+
+_EMPTY: dict = {}
+
+
+def fused_block_forward(block, x: Tensor) -> Tensor:
+    """Run ``block`` (a TransformerBlock) through :class:`FusedBlockFn`; x: [B, S, d] bf16 on the GPU."""
+    B, S, d = x.shape
+    attn, ffn = block.attn, block.ffn
+    if attn.rope is not None:
+        cos, sin, use_rope = attn.rope.cos, attn.rope.sin, True
+    else:
+        key = x.device
+        if key not in _EMPTY:
+            _EMPTY[key] = torch.empty(0, 0, device=x.device, dtype=torch.float32)
+        cos = sin = _EMPTY[key]
+        use_rope = False
+    meta = (B, S, attn.num_heads, attn.num_kv_heads, attn.d_k, block.ln1.eps, use_rope)
+    y = FusedBlockFn.apply(x.reshape(B * S, d).contiguous(), block.ln1.weight, attn.q_proj.weight,
+                           attn.k_proj.weight, attn.v_proj.weight, attn.output_proj.weight, block.ln2.weight,
+                           ffn.w1.weight, ffn.w3.weight, ffn.w2.weight, cos, sin, meta)
+    return y.view(B, S, d)

@@ -103,9 +103,10 @@ class SwiGLU(nn.Module):
 
     def __init__(self, d_model: int, d_ff: int, device=None, dtype=None):
         super().__init__()
+        # registration order w1, w3, w2 keeps [W1; W3] adjacent in the flat parameter buffer
         self.w1 = Linear(d_model, d_ff, device=device, dtype=dtype)
-        self.w2 = Linear(d_ff, d_model, device=device, dtype=dtype)
         self.w3 = Linear(d_model, d_ff, device=device, dtype=dtype)
+        self.w2 = Linear(d_ff, d_model, device=device, dtype=dtype)
 
     def fused_gate_up(self, x2: Tensor) -> Tensor:
         gu = torch.matmul(x2, torch.cat([self.w1.weight, self.w3.weight], 0).t())
@@ -272,6 +273,12 @@ class TransformerBlock(nn.Module):
         return x + self.ffn(self.ln2(x))
 
     def _forward_fused(self, x: Tensor) -> Tensor:
+        from .fused_block import fused_block_forward
+
+        return fused_block_forward(self, x)
+
+    def _forward_fused_unfused_ops(self, x: Tensor) -> Tensor:
+        """Same math as :meth:`_forward_fused` through per-op autograd (kept for A/B and debugging)."""
         B, S, d = x.shape
         x2 = x.reshape(B * S, d)
         o = self.attn.attend(self.ln1(x2), B, S)

@@ -1,0 +1,436 @@
+// Flash attention backward with fused RoPE, gfx950 (MI355X).
+//
+// Parity target: the gradient of reference contracts K7/K10
+// (`tests/adapters.py:92-184`); checked against autograd of the fp32 oracle.
+//
+// Structure: one workgroup = NW waves x 32 keys of one (batch, kv-head)
+// (NW = 8 -> 256 keys for D = 64; NW = 4 -> 128 keys for D = 128, where LDS
+// is the limit).  Each wave keeps its 32 keys' K and V rows as MFMA B-operand
+// fragments in registers and its dK^T / dV^T tiles in accumulators for the
+// whole sweep over query tiles (64 queries per step), so dK and dV never need
+// a cross-workgroup sum.  Per query tile:
+//   S  = Q.K^T   and  dP = dO.V^T      (key on the lane, queries in registers;
+//                                        A operands: Q / dO rows, ds_read_b128)
+//   P  = exp2(S * scale*log2e - LSE2),  dS = P * (dP - delta)
+//   dV^T += dO^T.P,  dK^T += Q^T.dS     (B operands straight from the P / dS
+//                                        accumulators; A = dO^T / Q^T via
+//                                        ds_read_b64_tr_b16 of the same images)
+//   dS^T -> LDS (8-byte writes), then dQ = dS.K for the workgroup's keys:
+//   2 x (D/32) output tiles of 32x32 spread over the waves; when there are
+//   more waves than tiles the key range is split and the partial tiles are
+//   summed through LDS first.  The dQ tile is then added to an fp32 buffer with
+//   float atomics shaped as two 128-byte row segments per wave instruction
+//   (guide G12).  256-key workgroups halve the atomic bytes of a 128-key
+//   design; at ~1.3 TB/s chip-wide those bytes set this kernel's floor.
+// RoPE: Q tiles are rotated while staged, K once at the start; dK is
+// un-rotated in the epilogue and dQ in the convert kernel.  GQA: a workgroup
+// sweeps every query head of its kv head.  Order: heaviest key blocks first.
+#include "fa_common.h"
+#include "kernels.h"
+
+#include <algorithm>
+
+namespace bpe {
+namespace fa {
+
+template <int D> struct BwdCfg {
+    static constexpr int NW = (D == 64) ? 8 : 4;                        // waves per workgroup
+    static constexpr int KB = 32 * NW;                                  // keys per workgroup
+    static constexpr int RB = D * 2;
+    static constexpr int QT = 64 * RB;                                  // bytes per 64-query tile
+    static constexpr int DT = D / 32;
+    static constexpr int OUT_TILES = 2 * DT;                            // 32x32 dQ tiles per query tile
+    static constexpr int KSPLIT = NW > OUT_TILES ? NW / OUT_TILES : 1;  // key-range split of the dQ product
+    static constexpr int TPW = OUT_TILES > NW ? OUT_TILES / NW : 1;     // dQ tiles per wave
+    static constexpr size_t LDS_Q = 2 * QT, LDS_DO = 2 * QT;
+    static constexpr size_t LDS_K = (size_t)KB * RB;  // K (roped) and V of the workgroup's keys, each
+    static constexpr size_t LDS_DST = (size_t)KB * 128;
+    static constexpr size_t LDS_X = KSPLIT > 1 ? (size_t)(KSPLIT - 1) * OUT_TILES * 16 * 64 * 4 : 0;
+    static constexpr size_t LDS_STATS = 4 * 64 * 4;
+    static constexpr size_t LDS = LDS_Q + LDS_DO + 2 * LDS_K + LDS_DST + LDS_X + LDS_STATS;
+};
+
+// delta = rowsum(dO * O) per (b, h, s)
+template <int D>
+__global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const __bf16* __restrict__ O, long ld_o,
+                                                         const __bf16* __restrict__ dO, long ld_do,
+                                                         float* __restrict__ delta, int B, int H, int S) {
+    constexpr int LPR = D / 8;
+    const long row = ((long)blockIdx.x * 256 + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
+    const long total = (long)B * S * H;
+    float acc = 0.f;
+    const bool ok = row < total;
+    long bs = 0;
+    int h = 0;
+    if (ok) {
+        bs = row / H;
+        h = (int)(row % H);
+        u16x8 a = *reinterpret_cast<const u16x8*>(O + bs * ld_o + (long)h * D + sub * 8);
+        u16x8 g = *reinterpret_cast<const u16x8*>(dO + bs * ld_do + (long)h * D + sub * 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc += bf2f(a[i]) * bf2f(g[i]);
+    }
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (ok && sub == 0) {
+        const long b = bs / S, s = bs % S;
+        delta[(b * H + h) * S + s] = acc;
+    }
+}
+
+template <int D, bool CAUSAL, bool ROPE>
+__global__ void __launch_bounds__(BwdCfg<D>::NW * 64, 1)
+fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv, long ld_q,
+              long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
+              const float* __restrict__ DELTA, float* __restrict__ dQacc, __bf16* __restrict__ dK,
+              __bf16* __restrict__ dV, long ld_dkv, const float* __restrict__ cosT, const float* __restrict__ sinT,
+              int B, int H, int Hkv, int S, float scale_log2, float scale) {
+    using C = BwdCfg<D>;
+    constexpr int NW = C::NW, NT = NW * 64, RB = C::RB, CPR = D / 8, QT = C::QT;
+    constexpr int SPT = (64 * CPR + NT - 1) / NT;  // staged chunks per thread per tile (Q and dO each)
+    constexpr int KS = D / 16, DT = C::DT;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Qs = smem;                                  // [2][64][D]
+    char* dOs = Qs + C::LDS_Q;                        // [2][64][D]
+    char* Kl = dOs + C::LDS_DO;                       // [KB][D]  roped K of this workgroup's keys
+    char* Vl = Kl + C::LDS_K;                         // [KB][D]  V of this workgroup's keys
+    char* dST = Vl + C::LDS_K;                        // [KB keys][64 q] bf16
+    float* xch = reinterpret_cast<float*>(dST + C::LDS_DST);              // dQ partial exchange
+    float* lseS = reinterpret_cast<float*>(dST + C::LDS_DST + C::LDS_X);  // [2][64]
+    float* dltS = lseS + 128;                                              // [2][64]
+
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    const int BHk = B * Hkv;
+    const int kb = (int)(blockIdx.x / BHk);
+    const int bhk = blockIdx.x % BHk;
+    const int b = bhk / Hkv, hk = bhk % Hkv;
+    const int G = H / Hkv;
+    const int kb0 = kb * C::KB, kw0 = kb0 + 32 * w;
+    const int key = kw0 + l31;
+    const bool key_ok = key < S;
+    const long kpos = key_ok ? key : 0;
+
+    // ---- this wave's K (roped) and V rows -> LDS (B operands of S / dP re-read per query tile,
+    //      K also the B operand of dQ); nothing stays pinned in registers across the sweep
+    {
+        const __bf16* kp = K + ((long)b * S + kpos) * ld_kv + (long)hk * D;
+        const __bf16* vp = Vv + ((long)b * S + kpos) * ld_kv + (long)hk * D;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int d0 = 16 * ks + 8 * hh;
+            u16x8 tk = key_ok ? *reinterpret_cast<const u16x8*>(kp + d0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            u16x8 tv = key_ok ? *reinterpret_cast<const u16x8*>(vp + d0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            if (ROPE) tk = rope_u16x8(tk, cosT + kpos * (D / 2) + d0 / 2, sinT + kpos * (D / 2) + d0 / 2, 1.f);
+            *reinterpret_cast<u16x8*>(Kl + swz<RB>(32 * w + l31, 2 * ks + hh)) = tk;
+            *reinterpret_cast<u16x8*>(Vl + swz<RB>(32 * w + l31, 2 * ks + hh)) = tv;
+        }
+    }
+
+    f32x16 dk[DT], dv[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+
+    const int m_start = CAUSAL ? kb0 : 0;  // kb0 is a multiple of 128 -> 64-aligned
+    const int nqt = (S - m_start + 63) / 64;
+    const int total_it = nqt * G;
+
+    u16x8 qreg[SPT], oreg[SPT];
+    float lreg = 0.f, dreg = 0.f;
+    auto load_tile = [&](int it) {
+        const int h = hk * G + it / nqt;
+        const int m0 = m_start + (it % nqt) * 64;
+        const __bf16* qb = Q + (long)b * S * ld_q + (long)h * D;
+        const __bf16* ob = dO + (long)b * S * ld_do + (long)h * D;
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int e = tid + NT * i, row = e / CPR, c = e % CPR;
+            const int qq = m0 + row;
+            if (e < 64 * CPR && qq < S) {
+                qreg[i] = *reinterpret_cast<const u16x8*>(qb + (long)qq * ld_q + c * 8);
+                oreg[i] = *reinterpret_cast<const u16x8*>(ob + (long)qq * ld_do + c * 8);
+            } else {
+                qreg[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+                oreg[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            }
+        }
+        if (tid < 64) {
+            const int qq = m0 + tid;
+            const long idx = ((long)b * H + h) * S + qq;
+            lreg = qq < S ? LSE[idx] : INFINITY;
+            dreg = qq < S ? DELTA[idx] : 0.f;
+        }
+    };
+    auto write_tile = [&](int it, int buf) {
+        const int m0 = m_start + (it % nqt) * 64;
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int e = tid + NT * i, row = e / CPR, c = e % CPR;
+            if (e >= 64 * CPR) break;
+            u16x8 qv = qreg[i];
+            if (ROPE) {
+                const long qq = min(m0 + row, S - 1);
+                qv = rope_u16x8(qv, cosT + qq * (D / 2) + c * 4, sinT + qq * (D / 2) + c * 4, 1.f);
+            }
+            *reinterpret_cast<u16x8*>(Qs + buf * QT + swz<RB>(row, c)) = qv;
+            *reinterpret_cast<u16x8*>(dOs + buf * QT + swz<RB>(row, c)) = oreg[i];
+        }
+        if (tid < 64) {
+            lseS[buf * 64 + tid] = lreg;
+            dltS[buf * 64 + tid] = dreg;
+        }
+    };
+
+    load_tile(0);
+    write_tile(0, 0);
+    __syncthreads();
+
+    const int trow = 4 * hh + ((l & 15) >> 2);          // tr-read row inside a 16-row k-step
+    const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);  // tr-read column inside a 32-wide tile
+
+    for (int it = 0; it < total_it; ++it) {
+        const int cur = it & 1;
+        const int h = hk * G + it / nqt;
+        const int m0 = m_start + (it % nqt) * 64;
+        if (it + 1 < total_it) load_tile(it + 1);
+        char* Qc = Qs + cur * QT;
+        char* Oc = dOs + cur * QT;
+        const float* lc = lseS + cur * 64;
+        const float* dc = dltS + cur * 64;
+        const bool active = !CAUSAL || (m0 + 63 >= kw0);
+        if (active) {
+            bf16x8 kf[KS], vf[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int off = swz<RB>(32 * w + l31, 2 * ks + hh);
+                kf[ks] = lds_row16(Kl, off);
+                vf[ks] = lds_row16(Vl, off);
+            }
+            f32x16 sp[2], dp[2];
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) { sp[qt][r] = 0.f; dp[qt][r] = 0.f; }
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
+                    sp[qt] = mfma(lds_row16(Qc, off), kf[ks], sp[qt]);
+                    dp[qt] = mfma(lds_row16(Oc, off), vf[ks], dp[qt]);
+                }
+            }
+            const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + 64 > S) || !key_ok;
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int qi = qt * 32 + 8 * i + 4 * hh;  // rows qi..qi+3
+                    const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
+                    const f32x4 dlt = *reinterpret_cast<const f32x4*>(dc + qi);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = 4 * i + j;
+                        float p = fast_exp2(sp[qt][r] * scale_log2 - lv[j]);
+                        if (need_mask) {
+                            const int qg = m0 + qi + j;
+                            if ((CAUSAL && key > qg) || qg >= S || !key_ok) p = 0.f;
+                        }
+                        sp[qt][r] = p;
+                        dp[qt][r] = p * (dp[qt][r] - dlt[j]);
+                    }
+                }
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    bf16x8 pb, db;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        pb[j] = (__bf16)sp[qt][8 * ss + j];
+                        db[j] = (__bf16)dp[qt][8 * ss + j];
+                    }
+                    const int qr = qt * 32 + 16 * ss;
+#pragma unroll
+                    for (int dt = 0; dt < DT; ++dt) {
+                        const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
+                        const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
+                        dv[dt] = mfma(lds_tr_pair(Oc, o0, o1), pb, dv[dt]);
+                        dk[dt] = mfma(lds_tr_pair(Qc, o0, o1), db, dk[dt]);
+                    }
+                }
+            // dS^T -> LDS [key row][q]: registers 4i..4i+3 are 4 consecutive queries
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    u16x4 t = {f2bf(dp[qt][4 * i]), f2bf(dp[qt][4 * i + 1]), f2bf(dp[qt][4 * i + 2]),
+                               f2bf(dp[qt][4 * i + 3])};
+                    *reinterpret_cast<u16x4*>(dST + swz<128>(32 * w + l31, qt * 4 + i) + 8 * hh) = t;
+                }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                *reinterpret_cast<u16x8*>(dST + swz<128>(32 * w + l31, 2 * c + hh)) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+        __syncthreads();
+        // ---- dQ = dS.K over this workgroup's keys
+        {
+            constexpr int KPART = C::KB / C::KSPLIT;  // keys per part
+            const int part = w / C::OUT_TILES;        // 0 when KSPLIT == 1
+            const int krow0 = part * KPART;
+            f32x16 acc[C::TPW];
+#pragma unroll
+            for (int tt = 0; tt < C::TPW; ++tt) {
+                const int tile = (C::TPW == 1) ? (w % C::OUT_TILES) : (w * C::TPW + tt);
+                const int qt2 = tile / DT, dt2 = tile % DT;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[tt][r] = 0.f;
+#pragma unroll
+                for (int ks = 0; ks < KPART / 16; ++ks) {
+                    const int kr = krow0 + 16 * ks + 8 * hh + ((l & 15) >> 2);
+                    const int qc = qt2 * 32 + tcol;
+                    const int dc2 = dt2 * 32 + tcol;
+                    const bf16x8 a = lds_tr_pair(dST, tr_off<128>(kr, qc), tr_off<128>(kr + 4, qc));
+                    const bf16x8 bb = lds_tr_pair(Kl, tr_off<RB>(kr, dc2), tr_off<RB>(kr + 4, dc2));
+                    acc[tt] = mfma(a, bb, acc[tt]);
+                }
+            }
+            if constexpr (C::KSPLIT > 1) {
+                const int tile = w % C::OUT_TILES;
+                if (part > 0) {
+                    float* dst = xch + ((size_t)(part - 1) * C::OUT_TILES + tile) * 16 * 64;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) dst[r * 64 + l] = acc[0][r];
+                }
+                __syncthreads();
+                if (part == 0) {
+#pragma unroll
+                    for (int pp = 1; pp < C::KSPLIT; ++pp) {
+                        const float* src = xch + ((size_t)(pp - 1) * C::OUT_TILES + tile) * 16 * 64;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[0][r] += src[r * 64 + l];
+                    }
+                }
+            }
+            if (part == 0) {
+#pragma unroll
+                for (int tt = 0; tt < C::TPW; ++tt) {
+                    const int tile = (C::TPW == 1) ? (w % C::OUT_TILES) : (w * C::TPW + tt);
+                    const int qt2 = tile / DT, dt2 = tile % DT;
+                    float* dqp = dQacc + ((long)b * S) * H * D + (long)h * D + dt2 * 32 + l31;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int qg = m0 + qt2 * 32 + acc_row(r, hh);
+                        if (qg < S) atomicAdd(dqp + (long)qg * H * D, acc[tt][r]);
+                    }
+                }
+            }
+        }
+        if (it + 1 < total_it) write_tile(it + 1, cur ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: dK = scale * R(-pos) dK^T, dV = dV^T  (key on the lane, d in registers)
+    if (key_ok) {
+        __bf16* dkp = dK + ((long)b * S + key) * ld_dkv + (long)hk * D;
+        __bf16* dvp = dV + ((long)b * S + key) * ld_dkv + (long)hk * D;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d0 = dt * 32 + 8 * i + 4 * hh;
+                float x[4] = {dk[dt][4 * i] * scale, dk[dt][4 * i + 1] * scale, dk[dt][4 * i + 2] * scale,
+                              dk[dt][4 * i + 3] * scale};
+                if (ROPE) {
+#pragma unroll
+                    for (int pr = 0; pr < 2; ++pr) {
+                        const float c = cosT[kpos * (D / 2) + d0 / 2 + pr];
+                        const float s = sinT[kpos * (D / 2) + d0 / 2 + pr];
+                        const float a = x[2 * pr], bb = x[2 * pr + 1];
+                        x[2 * pr] = a * c + bb * s;
+                        x[2 * pr + 1] = -a * s + bb * c;
+                    }
+                }
+                u16x4 tk = {f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+                u16x4 tv = {f2bf(dv[dt][4 * i]), f2bf(dv[dt][4 * i + 1]), f2bf(dv[dt][4 * i + 2]),
+                            f2bf(dv[dt][4 * i + 3])};
+                *reinterpret_cast<u16x4*>(dkp + d0) = tk;
+                *reinterpret_cast<u16x4*>(dvp + d0) = tv;
+            }
+    }
+}
+
+// dQ (fp32, roped space, unscaled) -> bf16 output slice: dq = scale * R(-pos) dQacc
+template <int D, bool ROPE>
+__global__ void __launch_bounds__(256) fa_dq_convert_kernel(const float* __restrict__ dQacc, __bf16* __restrict__ dq,
+                                                            long ld_dq, const float* __restrict__ cosT,
+                                                            const float* __restrict__ sinT, int B, int H, int S,
+                                                            float scale) {
+    const long total = (long)B * S * H * (D / 4);
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const long row = i / (D / 4);  // (b, s, h)
+        const int d0 = (int)(i % (D / 4)) * 4;
+        const long bs = row / H;
+        const int h = (int)(row % H);
+        const long s = bs % S;
+        f32x4 v = *reinterpret_cast<const f32x4*>(dQacc + row * D + d0);
+        float x[4] = {v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale};
+        if (ROPE) {
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+                const float c = cosT[s * (D / 2) + d0 / 2 + pr];
+                const float sn = sinT[s * (D / 2) + d0 / 2 + pr];
+                const float a = x[2 * pr], bb = x[2 * pr + 1];
+                x[2 * pr] = a * c + bb * sn;
+                x[2 * pr + 1] = -a * sn + bb * c;
+            }
+        }
+        u16x4 t = {f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+        *reinterpret_cast<u16x4*>(dq + bs * ld_dq + (long)h * D + d0) = t;
+    }
+}
+
+}  // namespace fa
+}  // namespace bpe
+
+using namespace bpe;
+using namespace bpe::fa;
+
+size_t fa_bwd_lds_bytes(int D) { return D == 64 ? BwdCfg<64>::LDS : BwdCfg<128>::LDS; }
+
+template <int D, bool C, bool R>
+static void bwd_launch(const FaArgs& a, hipStream_t s) {
+    using Cfg = BwdCfg<D>;
+    {
+        const long rows = (long)a.B * a.S * a.H;
+        const long threads = rows * (D / 8);
+        fa_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(a.o, a.ld_o, a.dout, a.ld_do, a.delta,
+                                                                               a.B, a.H, a.S);
+    }
+    (void)hipMemsetAsync(a.dq_acc, 0, (size_t)a.B * a.S * a.H * D * sizeof(float), s);
+    const int nkb = (a.S + Cfg::KB - 1) / Cfg::KB;
+    static bool lds_attr = false;  // > 64 KiB of dynamic LDS: opt in once (before any graph capture)
+    if (!lds_attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fa_bwd_kernel<D, C, R>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+        lds_attr = true;
+    }
+    fa_bwd_kernel<D, C, R><<<nkb * a.B * a.Hkv, Cfg::NW * 64, Cfg::LDS, s>>>(
+        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv, a.cos, a.sin,
+        a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale);
+    const long total = (long)a.B * a.S * a.H * (D / 4);
+    const int grid = (int)std::min<long>((total + 255) / 256, 4096);
+    fa_dq_convert_kernel<D, R><<<grid, 256, 0, s>>>(a.dq_acc, a.dq, a.ld_dq, a.cos, a.sin, a.B, a.H, a.S, a.scale);
+}
+
+void launch_fa_bwd(const FaArgs& a, hipStream_t s) {
+#define BWD_CASE(DD)                                                                                        \
+    if (a.D == DD) {                                                                                        \
+        if (a.causal) { if (a.rope) bwd_launch<DD, true, true>(a, s); else bwd_launch<DD, true, false>(a, s); } \
+        else { if (a.rope) bwd_launch<DD, false, true>(a, s); else bwd_launch<DD, false, false>(a, s); }     \
+        return;                                                                                             \
+    }
+    BWD_CASE(64) BWD_CASE(128)
+#undef BWD_CASE
+}

@@ -13,7 +13,7 @@ void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float*
                         hipStream_t s);
 int rmsnorm_bwd_grid(int M);
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                        float* partial, void* dw, int M, int N, hipStream_t s);
+                        float* partial, void* dw, const void* dres, int M, int N, hipStream_t s);
 
 // activations.hip
 void launch_swiglu_fwd(int dtype, const void* gu, void* out, size_t M, int F, hipStream_t s);
@@ -43,6 +43,12 @@ void launch_scale(int dtype, void* x, size_t n, const float* coef, hipStream_t s
 // softmax.hip
 void launch_softmax_fwd(int dtype, const void* x, void* y, int M, int N, hipStream_t s);
 void launch_softmax_bwd(int dtype, const void* dy, const void* y, void* dx, int M, int N, hipStream_t s);
+
+// gemm.hip
+size_t gemm_lds_bytes();
+bool gemm_shape_ok(int Mo, int No, int R, int splits);
+void launch_gemm(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
+                 float beta, int Mo, int No, int R, int splits, float* slab, hipStream_t s);
 
 // rope.hip
 void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,

@@ -50,7 +50,8 @@ template <typename T, int C>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const T* __restrict__ w,
                                                           const float* __restrict__ rstd, T* __restrict__ dx,
-                                                          float* __restrict__ dw_partial, int M, int N) {
+                                                          float* __restrict__ dw_partial,
+                                                          const T* __restrict__ dres, int M, int N) {
     constexpr int V = Vec<T>::N;
     extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][N]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -104,6 +105,12 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ 
                 for (int j = 0; j < V; ++j) {
                     o.v[j] = r * (gs[c][j] * wv[c][j] - xs[c][j] * dot);
                     dwacc[c][j] += gs[c][j] * xs[c][j];
+                }
+                if (dres) {  // fused residual-branch gradient: dx += dres
+                    Vec<T> rr;
+                    rr.load(dres + (size_t)row * N + i * V);
+#pragma unroll
+                    for (int j = 0; j < V; ++j) o.v[j] += rr.v[j];
                 }
                 o.store(dxr + i * V);
             }
@@ -166,13 +173,13 @@ void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float*
 
 template <typename T>
 static void rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* rstd, T* dx, float* partial,
-                             int grid, int M, int N, hipStream_t s) {
+                             const T* dres, int grid, int M, int N, hipStream_t s) {
     constexpr int V = Vec<T>::N;
     const int chunks = (N / V + 63) / 64;
     const size_t lds = (size_t)4 * N * sizeof(float);
 #define RMS_CASE(CC)                                                                                    \
     if (chunks <= CC) {                                                                                 \
-        rmsnorm_bwd_kernel<T, CC><<<grid, 256, lds, s>>>(dy, x, w, rstd, dx, partial, M, N);            \
+        rmsnorm_bwd_kernel<T, CC><<<grid, 256, lds, s>>>(dy, x, w, rstd, dx, partial, dres, M, N);      \
         return;                                                                                         \
     }
     RMS_CASE(1) RMS_CASE(2) RMS_CASE(4) RMS_CASE(8)
@@ -181,19 +188,19 @@ static void rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* r
 
 int rmsnorm_bwd_grid(int M) {
     int g = (M + 3) / 4;
-    return g < 256 ? g : 256;
+    return g < 1024 ? g : 1024;
 }
 
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                        float* partial, void* dw, int M, int N, hipStream_t s) {
+                        float* partial, void* dw, const void* dres, int M, int N, hipStream_t s) {
     const int grid = rmsnorm_bwd_grid(M);
     if (dtype == DT_BF16) {
         rms_bwd_dispatch<__bf16>((const __bf16*)dy, (const __bf16*)x, (const __bf16*)w, rstd, (__bf16*)dx, partial,
-                                 grid, M, N, s);
+                                 (const __bf16*)dres, grid, M, N, s);
         colsum_kernel<__bf16><<<(N + 63) / 64, 1024, 0, s>>>(partial, (__bf16*)dw, grid, N);
     } else {
-        rms_bwd_dispatch<float>((const float*)dy, (const float*)x, (const float*)w, rstd, (float*)dx, partial, grid,
-                                M, N, s);
+        rms_bwd_dispatch<float>((const float*)dy, (const float*)x, (const float*)w, rstd, (float*)dx, partial,
+                                (const float*)dres, grid, M, N, s);
         colsum_kernel<float><<<(N + 63) / 64, 1024, 0, s>>>(partial, (float*)dw, grid, N);
     }
 }

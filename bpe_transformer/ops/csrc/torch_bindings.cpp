@@ -57,7 +57,7 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Te
 }
 
 std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
-                                               const at::Tensor& rstd) {
+                                               const at::Tensor& rstd, const c10::optional<at::Tensor>& dres) {
     check_cuda(x, "x");
     auto dyc = dy.contiguous();
     const int N = (int)x.size(-1);
@@ -69,8 +69,15 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     auto dw = at::empty_like(w);
     const int grid = rmsnorm_bwd_grid(M);
     auto partial = at::empty({grid, N}, x.options().dtype(at::kFloat));
+    const void* rp = nullptr;
+    at::Tensor rc;
+    if (dres.has_value() && dres->defined()) {
+        rc = dres->contiguous();
+        TORCH_CHECK(rc.numel() == x.numel() && rc.scalar_type() == x.scalar_type(), "rmsnorm bwd: bad residual grad");
+        rp = rc.data_ptr();
+    }
     launch_rmsnorm_bwd(dt_code(x), dyc.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dx.data_ptr(),
-                       partial.data_ptr<float>(), dw.data_ptr(), M, N, cur_stream());
+                       partial.data_ptr<float>(), dw.data_ptr(), rp, M, N, cur_stream());
     return {dx, dw};
 }
 
@@ -243,6 +250,29 @@ at::Tensor softmax_bwd(const at::Tensor& dy, const at::Tensor& y) {
     return dx;
 }
 
+// ---------------------------------------------------------------- GEMM (split-K, transposed-LDS operands)
+// C[Mo, No] = beta * C + op(A) . op(B); A is [Mo, R] (a_kmajor) or [R, Mo]; B is [No, R] (b_kmajor) or [R, No].
+void gemm(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor, at::Tensor C, double beta,
+          int64_t splits) {
+    check_cuda(C, "C");
+    TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
+                    C.scalar_type() == at::kBFloat16, "gemm: bf16 operands required");
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
+                    C.stride(1) == 1, "gemm: 2-D row-major operands required");
+    const int Mo = (int)C.size(0), No = (int)C.size(1);
+    const int R = (int)(a_kmajor ? A.size(1) : A.size(0));
+    TORCH_CHECK((a_kmajor ? A.size(0) : A.size(1)) == Mo, "gemm: A / C shape mismatch");
+    TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == No && (b_kmajor ? B.size(1) : B.size(0)) == R,
+                "gemm: B shape mismatch");
+    TORCH_CHECK(gemm_shape_ok(Mo, No, R, (int)splits), "gemm: Mo/No must be multiples of 128 and R of 64*splits");
+    TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 && C.stride(0) % 4 == 0, "gemm: 16-byte row alignment");
+    DevGuard g(C.device());
+    at::Tensor slab;
+    if (splits > 1) slab = at::empty({splits, Mo, No}, C.options().dtype(at::kFloat));
+    launch_gemm(a_kmajor, b_kmajor, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
+                (float)beta, Mo, No, R, (int)splits, splits > 1 ? slab.data_ptr<float>() : nullptr, cur_stream());
+}
+
 // ---------------------------------------------------------------- RoPE
 at::Tensor rope(const at::Tensor& x, const at::Tensor& pos, const at::Tensor& cos, const at::Tensor& sin,
                 bool inverse) {
@@ -332,7 +362,7 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
 
 TORCH_LIBRARY(bpe_hip, m) {
     m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
-    m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd) -> (Tensor, Tensor)");
+    m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
     m.def("swiglu_fwd(Tensor gu) -> Tensor");
     m.def("swiglu_bwd(Tensor dout, Tensor gu) -> Tensor");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");
@@ -344,6 +374,7 @@ TORCH_LIBRARY(bpe_hip, m) {
           "float b2, float eps, float wd, float bc1, float bc2_sqrt, Tensor? gscale) -> ()");
     m.def("grad_norm(Tensor[] tensors, float max_norm) -> (Tensor, Tensor)");
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
+    m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits) -> ()");
     m.def("softmax_fwd(Tensor x) -> Tensor");
     m.def("softmax_bwd(Tensor dy, Tensor y) -> Tensor");
     m.def("rope(Tensor x, Tensor pos, Tensor cos, Tensor sin, bool inverse) -> Tensor");
@@ -366,6 +397,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("adamw_step", &adamw_step);
     m.impl("grad_norm", &grad_norm);
     m.impl("scale_", &scale_);
+    m.impl("gemm", &gemm);
     m.impl("softmax_fwd", &softmax_fwd);
     m.impl("softmax_bwd", &softmax_bwd);
     m.impl("rope", &rope);

@@ -67,6 +67,8 @@ class BucketedAllReduce:
         if overlap and self.world > 1:
             for s in slots:
                 self._hooks.append(s.param.register_post_accumulate_grad_hook(self._on_grad))
+                # kernels that accumulate into param.main_grad themselves call this instead
+                s.param._bpe_grad_ready = self._on_grad
 
     # -- hooks -------------------------------------------------------------
     def _on_grad(self, p: torch.Tensor) -> None:

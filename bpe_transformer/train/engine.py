@@ -37,6 +37,8 @@ class TrainEngine:
         self.model = model
         self.dist = dist_info or DistInfo()
         self.flat = FlatParameters.from_module(model)
+        for slot in self.flat.slots:  # fused blocks accumulate weight grads straight into the flat buffer
+            slot.param.main_grad = self.flat.grad_view(slot).view_as(slot.param)
         self.opt = FlatAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         self.max_grad_norm = max_grad_norm
         self.ddp = BucketedAllReduce(self.flat, bucket_mb=bucket_mb) if self.dist.world_size > 1 else None

@@ -230,6 +230,34 @@ def test_grad_norm_clip(gpu_device):
         assert rel(p.grad.cpu(), r.grad) < 1e-5
 
 
+# ---------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_gemm_layouts(gpu_device, a_k, b_k, splits):
+    torch.manual_seed(0)
+    Mo, No, R = 256, 384, 1024
+    A = torch.randn(Mo, R, device=gpu_device, dtype=torch.bfloat16)
+    B = torch.randn(No, R, device=gpu_device, dtype=torch.bfloat16)
+    Am = A if a_k else A.t().contiguous()
+    Bm = B if b_k else B.t().contiguous()
+    C = torch.randn(Mo, No, device=gpu_device, dtype=torch.bfloat16)
+    ref = C.float() * 0.5 + A.float() @ B.float().t()
+    torch.ops.bpe_hip.gemm(Am, a_k, Bm, b_k, C, 0.5, splits)
+    assert rel(C.cpu(), ref.cpu()) < 1e-2
+
+
+def test_weight_grad_accumulate(gpu_device):
+    from bpe_transformer.ops.gemm import accumulate_weight_grad
+
+    torch.manual_seed(0)
+    dy = torch.randn(4096, 768, device=gpu_device, dtype=torch.bfloat16)
+    x = torch.randn(4096, 2304, device=gpu_device, dtype=torch.bfloat16)
+    g = torch.randn(768, 2304, device=gpu_device, dtype=torch.bfloat16)
+    ref = g.float() + dy.float().t() @ x.float()
+    accumulate_weight_grad(g, dy, x)
+    assert rel(g.cpu(), ref.cpu()) < 1e-2
+
+
 # ---------------------------------------------------------------- flash attention
 def _fa_case(gpu_device, B, S, H, Hkv, D, rope, causal, seed=0):
     torch.manual_seed(seed)

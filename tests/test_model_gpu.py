@@ -44,6 +44,26 @@ def test_loss_and_grads_match_oracle(gpu_device):
         assert e < 0.08, (n, float(e))
 
 
+def test_main_grad_path_matches_autograd(gpu_device):
+    """Fused blocks accumulating into the flat buffer (main_grad) == per-parameter autograd grads."""
+    from bpe_transformer.optim.flat import FlatParameters
+
+    _, a = _pair(gpu_device)
+    b = copy.deepcopy(a)
+    flat = FlatParameters.from_module(a)
+    for s in flat.slots:
+        s.param.main_grad = flat.grad_view(s).view_as(s.param)
+    ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    for _ in range(2):  # accumulation over two micro-batches
+        a.loss(ids, tgt).backward()
+        b.loss(ids, tgt).backward()
+    for s, (n, pb) in zip(flat.slots, b.named_parameters()):
+        ga = flat.grad_view(s).view_as(pb).float()
+        e = (ga - pb.grad.float()).norm() / pb.grad.float().norm().clamp_min(1e-12)
+        assert e < 1e-2, (n, float(e))
+
+
 def test_train_engine_reduces_loss(gpu_device):
     from bpe_transformer.train.engine import TrainEngine
 
