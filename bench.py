@@ -30,6 +30,29 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 import torch  # noqa: E402
 
 METRIC = "training tokens/sec (whole node), GPT-2-small config at 1/2/4/8 MI355X"
+TUNING_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bpe_transformer", "ops", "tuning")
+
+
+def load_gemm_tuning(spec: str, model: str, batch: int, seq: int) -> str | None:
+    """Point PyTorch's TunableOp at a pre-measured hipBLASLt/rocBLAS solution table (no tuning at run time).
+
+    The tables in ``bpe_transformer/ops/tuning`` were produced on MI355X by running this benchmark with
+    ``PYTORCH_TUNABLEOP_TUNING=1``; they only choose among the libraries' own GEMM solutions.
+    """
+    if spec == "off":
+        return None
+    path = spec
+    if spec == "auto":
+        path = os.path.join(TUNING_DIR, f"{model}_b{batch}_s{seq}.csv")
+    if not os.path.exists(path):
+        return None
+    import torch.cuda.tunable as tunable
+
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.record_untuned_enable(False)
+    tunable.read_file(path)
+    return os.path.basename(path)
 
 
 def main() -> int:
@@ -37,10 +60,13 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=16, help="per-GPU micro-batch (sequences)")
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU micro-batch (sequences)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--gemm-tuning", default="auto",
+                    help="hipBLASLt/rocBLAS solution table (TunableOp CSV) for the library GEMMs; 'auto' = the "
+                         "shipped table for this model/batch if present, 'off' = library heuristics")
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args()
 
@@ -50,6 +76,7 @@ def main() -> int:
     from bpe_transformer.train.engine import TrainEngine
 
     info = init_distributed("cuda")
+    tuning = load_gemm_tuning(args.gemm_tuning, args.model, args.batch, args.seq)
     if args.gpus != info.world_size:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
     dev = info.device
@@ -111,6 +138,7 @@ def main() -> int:
         },
         "mfu_bf16_dense_2.5PF": round(value / n * flops_tok / 2.5e15, 4),
         "final_loss": round(loss_v, 4),
+        "gemm_tuning": tuning,
     }
     if info.is_main:
         line = json.dumps(out)

@@ -3,12 +3,16 @@ hand-written split-K MFMA kernel (ops/csrc/gemm.hip), GPT-2-small shapes.  Rando
 median of interleaved timed rounds in one process (guide §5.4 rule 24)."""
 import argparse
 import json
+import os
 import statistics
+import sys
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from bpe_transformer import ops  # noqa: F401  (loads the HIP library)
-from bpe_transformer.ops.gemm import accumulate_weight_grad, choose_splits
+import torch  # noqa: E402
+
+from bpe_transformer import ops  # noqa: E402,F401  (loads the HIP library)
+from bpe_transformer.ops.gemm import accumulate_weight_grad, choose_splits, matmul_nt  # noqa: E402
 
 
 def bench(fn, iters=20):
@@ -46,6 +50,20 @@ def main():
                      "ours_ms": round(mo, 4), "hipblaslt_tflops": round(fl / mb / 1e9, 1),
                      "ours_tflops": round(fl / mo / 1e9, 1), "speedup": round(mb / mo, 3)}
         print(json.dumps({name: out[name]}), flush=True)
+    # forward-shaped products Y = X W^T (both operands K-major): hipBLASLt vs the same kernel
+    for name, (n, k) in shapes.items():
+        x = torch.randn(T, k, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(n, k, device="cuda", dtype=torch.bfloat16)
+        y = torch.empty(T, n, device="cuda", dtype=torch.bfloat16)
+        tb, to = [], []
+        for _ in range(a.rounds):
+            tb.append(bench(lambda: torch.matmul(x, w.t(), out=y)))
+            to.append(bench(lambda: matmul_nt(x, w, out=y)))
+        fl = 2.0 * n * k * T
+        mb, mo = statistics.median(tb), statistics.median(to)
+        print(json.dumps({"fwd_" + name: {"hipblaslt_tflops": round(fl / mb / 1e9, 1),
+                                          "ours_tflops": round(fl / mo / 1e9, 1), "speedup": round(mb / mo, 3)}}),
+              flush=True)
 
 
 if __name__ == "__main__":

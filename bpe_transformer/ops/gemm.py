@@ -36,8 +36,17 @@ def choose_splits(n: int, k: int, t: int, target: int = _TARGET_WGS, min_iters: 
     return best
 
 
+_MAX_TILES = int(os.environ.get("BPE_DW_GEMM_MAX_TILES", "160"))
+
+
 def supported(n: int, k: int, t: int) -> bool:
-    return n % 128 == 0 and k % 128 == 0 and t % 64 == 0
+    """Shapes routed to the split-K kernel: tile-aligned and with few output tiles.
+
+    Measured on MI355X (benchmarks/gemm_bench.py, 16k and 64k tokens): the split-K kernel beats hipBLASLt
+    1.25-1.67x on the 768x768 / 2304x768 / 768x2048 gradients (36-108 tiles of 128x128) and loses ~10% on
+    the 4096x768 one (192 tiles), where the library's own tiles already fill the chip.
+    """
+    return n % 128 == 0 and k % 128 == 0 and t % 64 == 0 and (n // 128) * (k // 128) <= _MAX_TILES
 
 
 def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
