@@ -67,6 +67,8 @@ def main() -> int:
     ap.add_argument("--gemm-tuning", default="auto",
                     help="hipBLASLt/rocBLAS solution table (TunableOp CSV) for the library GEMMs; 'auto' = the "
                          "shipped table for this model/batch if present, 'off' = library heuristics")
+    ap.add_argument("--precision", choices=["bf16", "fp8"], default="bf16",
+                    help="fp8 = block projections' forward GEMMs in e4m3fn with delayed scaling (bf16 backward)")
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args()
 
@@ -83,6 +85,8 @@ def main() -> int:
     torch.manual_seed(1234)  # identical init on every rank (rank-0 broadcast also enforces it)
     cfg = get_preset(args.model, context_length=args.seq)
     model = TransformerLM.from_config(cfg, device=dev, dtype=torch.bfloat16)
+    if args.precision == "fp8":
+        model.enable_fp8()
     engine = TrainEngine(model, info, lr=3e-4, weight_decay=0.1, max_grad_norm=1.0, bucket_mb=args.bucket_mb)
 
     # synthetic token stream, different per rank; batches staged on the device up front
@@ -126,7 +130,7 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "bf16" if args.precision == "bf16" else "fp8(e4m3 fwd GEMMs)+bf16",
         "data": "synthetic (uniform random tokens, random-init weights)",
         "config": {
             "model": f"{args.model} ({cfg.num_layers}L/{cfg.d_model}d/{cfg.num_heads}H, RoPE+SwiGLU+RMSNorm, "

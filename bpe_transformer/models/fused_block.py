@@ -68,19 +68,30 @@ def _notify(p: Tensor) -> None:
 class FusedBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, ln1, wq, wk, wv, wo, ln2, w1, w3, w2, cos, sin, meta):
-        B, S, H, Hkv, D, eps, use_rope = meta
+        B, S, H, Hkv, D, eps, use_rope = meta[:7]
+        fp8 = meta[7] if len(meta) > 7 else None  # (Fp8State, first slot) or None
         scale = 1.0 / math.sqrt(D)
         w_qkv = _cat_weights([wq, wk, wv])
         w_13 = _cat_weights([w1, w3])
         h1, r1 = hip().rmsnorm_fwd(x2, ln1, eps)
-        qkv = torch.matmul(h1, w_qkv.t())
+        if fp8 is not None:
+            st, s0 = fp8  # slots s0..s0+3: activations, s0+4..s0+7: weights
+            qkv = st.matmul(h1, w_qkv, s0, s0 + 4)
+        else:
+            qkv = torch.matmul(h1, w_qkv.t())
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale)
-        xm = torch.addmm(x2, o, wo.t())
+        if fp8 is not None:
+            xm = x2 + st.matmul(o, wo.detach(), s0 + 1, s0 + 5)
+        else:
+            xm = torch.addmm(x2, o, wo.t())
         h2, r2 = hip().rmsnorm_fwd(xm, ln2, eps)
-        gu = torch.matmul(h2, w_13.t())
+        gu = st.matmul(h2, w_13, s0 + 2, s0 + 6) if fp8 is not None else torch.matmul(h2, w_13.t())
         a = hip().swiglu_fwd(gu)
-        y = torch.addmm(xm, a, w2.t())
+        if fp8 is not None:
+            y = xm + st.matmul(a, w2.detach(), s0 + 3, s0 + 7)
+        else:
+            y = torch.addmm(xm, a, w2.t())
         ctx.save_for_backward(x2, r1, h1, qkv, o, lse, xm, r2, h2, gu, a, cos, sin)
         ctx.params = (ln1, wq, wk, wv, wo, ln2, w1, w3, w2)
         ctx.meta = meta
@@ -90,7 +101,7 @@ class FusedBlockFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, r1, h1, qkv, o, lse, xm, r2, h2, gu, a, cos, sin = ctx.saved_tensors
         ln1, wq, wk, wv, wo, ln2, w1, w3, w2 = ctx.params
-        B, S, H, Hkv, D, eps, use_rope = ctx.meta
+        B, S, H, Hkv, D, eps, use_rope = ctx.meta[:7]
         scale = 1.0 / math.sqrt(D)
         dy = dy.contiguous()
         params = ctx.params
@@ -162,6 +173,9 @@ def fused_block_forward(block, x: Tensor) -> Tensor:
         cos = sin = _EMPTY[key]
         use_rope = False
     meta = (B, S, attn.num_heads, attn.num_kv_heads, attn.d_k, block.ln1.eps, use_rope)
+    fp8 = getattr(block, "fp8", None)
+    if fp8 is not None:
+        meta = meta + (fp8,)
     y = FusedBlockFn.apply(x.reshape(B * S, d).contiguous(), block.ln1.weight, attn.q_proj.weight,
                            attn.k_proj.weight, attn.v_proj.weight, attn.output_proj.weight, block.ln2.weight,
                            ffn.w1.weight, ffn.w3.weight, ffn.w2.weight, cos, sin, meta)

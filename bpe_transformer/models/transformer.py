@@ -65,6 +65,23 @@ class TransformerLM(nn.Module):
             remove_rope=cfg.remove_rope, ffn_type=cfg.ffn_type, eps=cfg.eps, device=device, dtype=dtype,
         )
 
+    fp8_state = None
+
+    def enable_fp8(self, history: int = 16, margin: float = 1.0):
+        """Run the block projections' forward GEMMs in fp8 (e4m3fn, delayed scaling).
+
+        Only the fused GPU block path quantises (``models/fused_block.py``); every
+        block owns 8 scale slots (4 activations + 4 weights).  The training engine
+        calls ``fp8_state.update()`` once per optimizer step.
+        """
+        from ..ops.fp8 import Fp8State
+
+        dev = self.lm_head.weight.device
+        self.fp8_state = Fp8State(8 * len(self.layers), dev, history=history, margin=margin)
+        for i, layer in enumerate(self.layers):
+            layer.fp8 = (self.fp8_state, 8 * i)
+        return self.fp8_state
+
     def hidden_states(self, in_indices: Tensor) -> Tensor:
         assert in_indices.shape[-1] <= self.context_length, "sequence longer than context_length"
         x = self.token_embeddings(in_indices)

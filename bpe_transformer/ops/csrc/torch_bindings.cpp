@@ -273,6 +273,30 @@ void gemm(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor
                 (float)beta, Mo, No, R, (int)splits, splits > 1 ? slab.data_ptr<float>() : nullptr, cur_stream());
 }
 
+// ---------------------------------------------------------------- FP8 quantisation (delayed scaling)
+void cast_fp8(const at::Tensor& x, const at::Tensor& scale, at::Tensor out, at::Tensor amax_bits) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && out.numel() == x.numel() && out.element_size() == 1,
+                "cast_fp8: contiguous x and a same-size 1-byte output required");
+    TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1, "cast_fp8: scale must be one fp32");
+    TORCH_CHECK(amax_bits.scalar_type() == at::kInt && amax_bits.numel() == 1, "cast_fp8: amax slot must be int32");
+    check_aligned(x, "x");
+    DevGuard g(x.device());
+    launch_cast_fp8(dt_code(x), x.data_ptr(), x.numel(), scale.data_ptr<float>(), out.data_ptr(),
+                    reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
+}
+
+void update_scales(at::Tensor amax_bits, at::Tensor hist, at::Tensor scale, at::Tensor inv_scale, int64_t pos,
+                   double margin) {
+    check_cuda(hist, "hist");
+    const int n = (int)hist.size(0), H = (int)hist.size(1);
+    TORCH_CHECK(amax_bits.numel() == n && scale.numel() == n && inv_scale.numel() == n, "update_scales: sizes");
+    DevGuard g(hist.device());
+    launch_update_scales(reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), hist.data_ptr<float>(),
+                         scale.data_ptr<float>(), inv_scale.data_ptr<float>(), n, H, (int)(pos % H), (float)margin,
+                         cur_stream());
+}
+
 // ---------------------------------------------------------------- RoPE
 at::Tensor rope(const at::Tensor& x, const at::Tensor& pos, const at::Tensor& cos, const at::Tensor& sin,
                 bool inverse) {
@@ -375,6 +399,9 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("grad_norm(Tensor[] tensors, float max_norm) -> (Tensor, Tensor)");
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits) -> ()");
+    m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
+    m.def("update_scales(Tensor(a!) amax_bits, Tensor(b!) hist, Tensor(c!) scale, Tensor(d!) inv_scale, int pos, "
+          "float margin) -> ()");
     m.def("softmax_fwd(Tensor x) -> Tensor");
     m.def("softmax_bwd(Tensor dy, Tensor y) -> Tensor");
     m.def("rope(Tensor x, Tensor pos, Tensor cos, Tensor sin, bool inverse) -> Tensor");
@@ -398,6 +425,8 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("grad_norm", &grad_norm);
     m.impl("scale_", &scale_);
     m.impl("gemm", &gemm);
+    m.impl("cast_fp8", &cast_fp8);
+    m.impl("update_scales", &update_scales);
     m.impl("softmax_fwd", &softmax_fwd);
     m.impl("softmax_bwd", &softmax_bwd);
     m.impl("rope", &rope);

@@ -72,6 +72,12 @@ class TrainEngine:
             norm, coef = self.opt.clip_grad_norm(self.max_grad_norm)
             self.last_grad_norm = norm
         self.opt.step(lr, coef)
+        fp8 = getattr(self.model, "fp8_state", None)
+        if fp8 is not None:
+            if self.ddp is not None:
+                # identical scales on every rank: amax bit patterns order like the (non-negative) floats
+                torch.distributed.all_reduce(fp8.amax, op=torch.distributed.ReduceOp.MAX)
+            fp8.update()
         return total / n if n > 1 else total
 
     def state_dict(self) -> dict:

@@ -30,6 +30,7 @@ _GROUPS = [
     ("cross_entropy", ("ce_fwd", "softmax")),
     ("optimizer", ("adamw", "sumsq", "norm_finalize", "scale_kernel")),
     ("embedding", ("embed_",)),
+    ("fp8 quant", ("cast_fp8", "update_scales")),
     ("rope", ("rope_kernel",)),
     ("comm", ("nccl", "rccl", "Reduce", "AllReduce")),
 ]
@@ -42,8 +43,28 @@ def classify_kernel(name: str) -> str:
     return "elementwise/other"
 
 
+def _load_stats(path: str | Path) -> list[dict]:
+    """Per-kernel rows from a ``*_kernel_stats.csv`` or a rocpd SQLite ``*_results.db`` (rocprofv3's
+    default output format on ROCm 7)."""
+    path = Path(path)
+    if path.suffix != ".db":
+        return list(csv.DictReader(open(path)))
+    import sqlite3
+
+    con = sqlite3.connect(f"file:{path}?mode=ro", uri=True)
+    try:
+        q = "select name, count(*), sum(duration), avg(duration) from kernels group by name"  # ns
+        rows = [{"Name": n, "Calls": c, "TotalDurationNs": t, "AverageNs": a} for n, c, t, a in con.execute(q)]
+    finally:
+        con.close()
+    tot = sum(r["TotalDurationNs"] for r in rows) or 1
+    for r in rows:
+        r["Percentage"] = 100.0 * r["TotalDurationNs"] / tot
+    return rows
+
+
 def summarize_rocprof_stats(csv_path: str | Path, steps: int | None = None) -> str:
-    rows = list(csv.DictReader(open(csv_path)))
+    rows = _load_stats(csv_path)
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     groups: dict[str, float] = defaultdict(float)
     for r in rows:

@@ -82,3 +82,40 @@ def test_generate(gpu_device):
     _, gpu = _pair(gpu_device)
     out = gpu.generate(torch.tensor([1, 2, 3], device=gpu_device), 8, temperature=0.0)
     assert out.shape == (11,)
+
+
+def test_fp8_forward_close_to_bf16(gpu_device):
+    """fp8 (e4m3, delayed scaling) block projections: loss and grads stay close to the bf16 path."""
+    _, a = _pair(gpu_device)
+    b = copy.deepcopy(a)
+    st = b.enable_fp8()
+    ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    with torch.no_grad():  # calibration pass: record amaxes, derive scales
+        b.loss(ids, tgt)
+    st.update()
+    assert bool((st.scale > 1).all()), st.scale  # small activations/weights -> scales above 1
+    la = a.loss(ids, tgt)
+    la.backward()
+    lb = b.loss(ids, tgt)
+    lb.backward()
+    assert abs(la.item() - lb.item()) < 2e-2, (la.item(), lb.item())
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        e = (pb.grad.float() - pa.grad.float()).norm() / pa.grad.float().norm().clamp_min(1e-12)
+        assert e < 0.15, (n, float(e))
+
+
+def test_fp8_engine_reduces_loss(gpu_device):
+    from bpe_transformer.train.engine import TrainEngine
+
+    torch.manual_seed(0)
+    model = TransformerLM(1000, 128, 256, 2, 4, 512, device=gpu_device, dtype=torch.bfloat16)
+    model.enable_fp8()
+    eng = TrainEngine(model, lr=3e-3, weight_decay=0.0, max_grad_norm=1.0)
+    x = torch.randint(0, 1000, (4, 128), device=gpu_device)
+    y = torch.roll(x, -1, 1)
+    first = eng.train_step([(x, y)]).item()
+    for _ in range(30):
+        last = eng.train_step([(x, y)]).item()
+    assert last < first - 1.0, (first, last)
+    assert model.fp8_state.pos == 31
