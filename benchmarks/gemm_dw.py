@@ -1,0 +1,54 @@
+"""Weight-gradient GEMM microbenchmark (dW += dY^T X) at the GPT-2-small and Llama-1.1B shapes:
+hipBLASLt vs the 256-tile kernel (routing of ops.gemm), TFLOP/s.  Set BPE_G256_VARIANT to A/B kernel
+variants (one per process)."""
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from bpe_transformer.ops._ext import ops as hip  # noqa: E402
+from bpe_transformer.ops.gemm import choose_splits_256  # noqa: E402
+
+SHAPES = {"gpt2": (65536, [(2304, 768), (768, 768), (4096, 768), (768, 2048)]),
+          "llama": (16384, [(2560, 2048), (2048, 2048), (11264, 2048), (2048, 5632)])}
+
+
+def bench(fn, iters=10):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    out = {"variant": os.environ.get("BPE_G256_VARIANT", "0")}
+    for model, (T, shapes) in SHAPES.items():
+        tot_b = tot_o = 0.0
+        for n, k in shapes:
+            dy = torch.randn(T, n, device="cuda", dtype=torch.bfloat16)
+            x = torch.randn(T, k, device="cuda", dtype=torch.bfloat16)
+            g = torch.zeros(n, k, device="cuda", dtype=torch.bfloat16)
+            sp = choose_splits_256(n, k, T)
+            tb, to = [], []
+            for _ in range(3):
+                tb.append(bench(lambda: g.addmm_(dy.t(), x)))
+                to.append(bench(lambda: hip().gemm(dy, False, x, False, g, 1.0, sp, 256)))
+            mb, mo = statistics.median(tb), statistics.median(to)
+            fl = 2.0 * n * k * T
+            out[f"{model}_{n}x{k}"] = {"blas_tf": round(fl / mb / 1e9), "ours_tf": round(fl / mo / 1e9), "splits": sp}
+            tot_b += mb
+            tot_o += mo
+        out[f"{model}_layer_ms"] = {"blas": round(tot_b, 4), "ours": round(tot_o, 4)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -21,7 +21,8 @@ import torch  # noqa: E402
 
 from bpe_transformer import ops  # noqa: E402,F401
 from bpe_transformer.models import get_preset  # noqa: E402
-from bpe_transformer.ops.gemm import accumulate_weight_grad, supported  # noqa: E402
+from bpe_transformer.ops._ext import ops as hip  # noqa: E402
+from bpe_transformer.ops.gemm import choose_splits, choose_splits_256, use_tile256  # noqa: E402
 
 
 def bench(fn, iters=10):
@@ -57,8 +58,10 @@ def main():
         dx = torch.empty(T, k, device="cuda", dtype=bf)
         wt = w.t().contiguous()
         g = torch.zeros(n, k, device="cuda", dtype=bf)
-        r = {k_: [] for k_ in ("fwd", "dX", "dXt", "tr", "dW_blas", "dW_ours")}
-        ours_ok = supported(n, k, T) if name != "lm_head" else False
+        r = {k_: [] for k_ in ("fwd", "dX", "dXt", "tr", "dW_blas", "dW_ours", "dW_256")}
+        ours_ok = n % 128 == 0 and k % 128 == 0
+        s128 = choose_splits(n, k, T)
+        s256 = choose_splits_256(n, k, T) if use_tile256(n, k, T) else None
         for _ in range(a.rounds):
             r["fwd"].append(bench(lambda: torch.matmul(x, w.t(), out=y)))
             r["dX"].append(bench(lambda: torch.matmul(dy, w, out=dx)))
@@ -66,22 +69,30 @@ def main():
             r["tr"].append(bench(lambda: wt.copy_(w.t())))
             r["dW_blas"].append(bench(lambda: g.addmm_(dy.t(), x)))
             if ours_ok:
-                r["dW_ours"].append(bench(lambda: accumulate_weight_grad(g, dy, x)))
+                r["dW_ours"].append(bench(lambda: hip().gemm(dy, False, x, False, g, 1.0, s128, 128)))
+            if s256:
+                r["dW_256"].append(bench(lambda: hip().gemm(dy, False, x, False, g, 1.0, s256, 256)))
         med = {k_: statistics.median(v) for k_, v in r.items() if v}
         fl = 2.0 * n * k * T
-        row = {"shape": [n, k, T]}
+        row = {"shape": [n, k, T], "splits128": s128, "splits256": s256}
         for k_, v in med.items():
             row[k_ + "_ms"] = round(v, 4)
             if k_ != "tr":
                 row[k_ + "_tflops"] = round(fl / v / 1e9, 1)
         print(json.dumps({name: row}), flush=True)
+        if s256:  # calibrate the split model
+            sweep = {}
+            for sp in (1, 2, 4, 8, 16, 32):
+                if (T // 64) % sp == 0 and T // 64 // sp >= 4:
+                    sweep[sp] = round(bench(lambda: hip().gemm(dy, False, x, False, g, 1.0, sp, 256)), 4)
+            print(json.dumps({name + "_sweep256_ms": sweep}), flush=True)
         if name == "lm_head":
             continue
         tot["fwd"] += med["fwd"]
         tot["dX"] += med["dX"]
         tot["dXt"] += med["dXt"] + med["tr"]
         tot["dW_blas"] += med["dW_blas"]
-        tot["dW_best"] += min(med["dW_blas"], med.get("dW_ours", 1e9))
+        tot["dW_best"] += min(med["dW_blas"], med.get("dW_ours", 1e9), med.get("dW_256", 1e9))
     print(json.dumps({"per_layer_ms": {k_: round(v, 4) for k_, v in tot.items()}}), flush=True)
 
 

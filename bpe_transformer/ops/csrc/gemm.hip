@@ -26,6 +26,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace bpe {
 namespace gemm {
@@ -189,6 +190,246 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Weight-gradient kernel: dW[Mo, No] (+)= A^T B with A [R, Mo], B [R, No] both
+// token-major (MN-major), R = tokens.  256 x 256 output tile, 8 waves (2 x 4,
+// each 128 x 64 = 4 x 2 MFMA 32x32x16), one workgroup per CU.
+//
+// Operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4): the LDS
+// image is lane-linear, so the XOR swizzle is applied to the SOURCE address
+// and the same involution on the fragment read (guide §5.4 rule 21).  Tiles
+// are [32 tokens][256 cols] (16 KiB per operand), 4 stages (128 KiB) with TWO
+// stages in flight while the MFMAs consume a third: one LDS-DMA takes ~1 us
+// to land, longer than one 64-deep step of MFMA work, so a single stage of
+// prefetch (measured: 660-985 TF) leaves the matrix cores waiting on every
+// barrier.  The wait is a counted `s_waitcnt vmcnt(8)` (the two newer stages
+// stay in flight) before a raw s_barrier -- __syncthreads() would drain every
+// DMA (guide §5 "Pipelining across barriers").
+namespace g256 {
+
+constexpr int BM = 256, BN = 256, BK = 32, NT = 512, NSTAGE = 4;
+constexpr int TILE_BYTES = BK * 256 * 2;  // 16 KiB per operand per stage
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+constexpr int LDS_BYTES = NSTAGE * STAGE_BYTES;  // 128 KiB
+
+// 512-byte rows: chunk c of row r stored at c ^ sigma(r); the 4 rows r0..r0+3 read by one
+// ds_read_b64_tr_b16 half-wave (64 contiguous bytes each) land in the 4 distinct 64-byte quarters of the
+// 256-byte bank row (conflict-free).
+__device__ __forceinline__ int sig512(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+// Per-thread source offsets (elements, relative to the tile's first token row) of the 2 chunks it DMAs per tile.
+__device__ __forceinline__ void dma_offsets(long ld, int c0, int w, int l, long (&off)[2]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int e = q * NT + w * 64 + l;
+        const int row = e >> 5, lc = (e & 31) ^ sig512(row);
+        off[q] = (long)row * ld + c0 + lc * 8;
+    }
+}
+
+// DMA one [32 r][256 cols] operand tile (1024 16-byte chunks, 2 per thread) into a lane-linear LDS image;
+// `tile0` = base + r0 * ld (wave-uniform).
+__device__ __forceinline__ void dma_tile(const __bf16* tile0, const long (&off)[2], char* lds, int w) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        __builtin_amdgcn_global_load_lds((gbl_void*)(tile0 + off[q]), (lds_void*)(lds + (q * NT + w * 64) * 16), 16,
+                                         0, 0);
+}
+
+// MFMA operands by two transposed reads (ds_read_b64_tr_b16; lane groups of 16 read 4 k-rows x 16 columns and
+// receive one column each).  32x32x16: lane l holds X[k = 8(l>>5) + j][t0 + (l&31)] of k-step ks (16 deep);
+// 16x16x32: lane l holds X[k = 8(l>>4) + j][t0 + (l&15)] (32 deep).
+__device__ __forceinline__ int off512(int r, int c) { return r * 512 + (((c >> 3) ^ sig512(r)) << 4) + ((c & 7) << 1); }
+
+__device__ __forceinline__ bf16x8 frag32(char* lds, int t0, int ks, int l) {
+    const int r = 16 * ks + 8 * (l >> 5) + ((l & 15) >> 2);
+    const int c = t0 + 16 * ((l >> 4) & 1) + 4 * (l & 3);
+    return lds_tr_pair(lds, off512(r, c), off512(r + 4, c));
+}
+
+__device__ __forceinline__ bf16x8 frag16(char* lds, int t0, int l) {
+    const int r = 8 * (l >> 4) + ((l & 15) >> 2);
+    const int c = t0 + 4 * (l & 3);
+    return lds_tr_pair(lds, off512(r, c), off512(r + 4, c));
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Accumulators of one wave's 128 x 64 output block.
+template <int MF>
+struct Acc;
+template <>
+struct Acc<32> {
+    f32x16 v[4][2];
+};
+template <>
+struct Acc<16> {
+    f32x4 v[8][4];
+};
+
+// One K-step: DMA a future stage, then fragments + MFMAs on the current one.  The two stages are __restrict__
+// parameters so that, once inlined, the LDS reads carry alias-scope metadata proving they do not touch the DMA
+// destination; without it the compiler's wait-count pass drains the DMA (vmcnt(0)) before the first fragment read.
+// PRIO: all fragments first, then the MFMA cluster between s_setprio(1)/(0) (keeps hipcc from moving MFMAs
+// across the barriers; guide T5).
+template <int MF, bool PRIO>
+__device__ __forceinline__ void kstep(char* __restrict__ cur, char* __restrict__ nxt, const __bf16* an,
+                                      const long (&oa)[2], const __bf16* bn, const long (&ob)[2], int wr, int wc,
+                                      int w, int l, Acc<MF>& acc) {
+    dma_tile(an, oa, nxt, w);
+    dma_tile(bn, ob, nxt + TILE_BYTES, w);
+    __builtin_amdgcn_sched_barrier(0);  // issue the DMA first: it needs all the MFMA time to land
+    char* Bs = cur + TILE_BYTES;
+    if constexpr (MF == 32) {
+        if constexpr (PRIO) {
+            bf16x8 fa[2][4], fb[2][2];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                fb[ks][0] = frag32(Bs, wc, ks, l);
+                fb[ks][1] = frag32(Bs, wc + 32, ks, l);
+#pragma unroll
+                for (int a = 0; a < 4; ++a) fa[ks][a] = frag32(cur, wr + 32 * a, ks, l);
+            }
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    acc.v[a][0] = mfma(fa[ks][a], fb[ks][0], acc.v[a][0]);
+                    acc.v[a][1] = mfma(fa[ks][a], fb[ks][1], acc.v[a][1]);
+                }
+            __builtin_amdgcn_s_setprio(0);
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8 fb0 = frag32(Bs, wc, ks, l), fb1 = frag32(Bs, wc + 32, ks, l);
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    bf16x8 fa = frag32(cur, wr + 32 * a, ks, l);
+                    acc.v[a][0] = mfma(fa, fb0, acc.v[a][0]);
+                    acc.v[a][1] = mfma(fa, fb1, acc.v[a][1]);
+                }
+            }
+        }
+    } else {
+        bf16x8 fb[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) fb[b] = frag16(Bs, wc + 16 * b, l);
+        if constexpr (PRIO) {
+            bf16x8 fa[8];
+#pragma unroll
+            for (int a = 0; a < 8; ++a) fa[a] = frag16(cur, wr + 16 * a, l);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int a = 0; a < 8; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc.v[a][b] = mfma16(fa[a], fb[b], acc.v[a][b]);
+            __builtin_amdgcn_s_setprio(0);
+        } else {
+#pragma unroll
+            for (int a = 0; a < 8; ++a) {
+                bf16x8 fa = frag16(cur, wr + 16 * a, l);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc.v[a][b] = mfma16(fa, fb[b], acc.v[a][b]);
+            }
+        }
+    }
+}
+
+// Epilogue element visitor: f(i_local, j_local, value) for every accumulator element of the wave.
+template <typename F>
+__device__ __forceinline__ void for_each_acc(const Acc<32>& acc, int l, F&& f) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) f(a * 32 + acc_row(r, l >> 5), b * 32 + (l & 31), acc.v[a][b][r]);
+}
+template <typename F>
+__device__ __forceinline__ void for_each_acc(const Acc<16>& acc, int l, F&& f) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) f(a * 16 + 4 * (l >> 4) + r, b * 16 + (l & 15), acc.v[a][b][r]);
+}
+
+template <int MF, bool PRIO>
+__global__ void __launch_bounds__(NT, 1)
+gemm256_tn_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
+                  float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int Mo, int No, int R,
+                  int splits) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+    // XCD-aware bijective remap: consecutive work ids (same split, neighbouring tiles sharing token rows)
+    // run on one XCD and its L2 (guide §5 "XCD swizzle must be bijective").
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    const int tiles_n = No / BN;
+    const int ntiles = (Mo / BM) * tiles_n;
+    const int split = wid / ntiles, tile = wid % ntiles;
+    const int i0 = (tile / tiles_n) * BM, j0 = (tile % tiles_n) * BN;
+    const int rlen = R / splits;
+    const int rbeg = split * rlen;
+    const int nk = rlen / BK;  // >= NSTAGE - 1 (host-checked)
+    const int rlast = rbeg + (nk - 1) * BK;
+    const int wr = (w >> 2) * 128, wc = (w & 3) * 64;
+
+    Acc<MF> acc;
+    {
+        float* z = reinterpret_cast<float*>(&acc);
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(acc) / 4); ++i) z[i] = 0.f;
+    }
+
+    long oa[2], ob[2];
+    dma_offsets(lda, i0, w, l, oa);
+    dma_offsets(ldb, j0, w, l, ob);
+    // prologue: stages 0, 1, 2 in flight; retire stage 0
+#pragma unroll
+    for (int st = 0; st < NSTAGE - 1; ++st) {
+        char* d = smem + st * STAGE_BYTES;
+        dma_tile(A + (long)(rbeg + st * BK) * lda, oa, d, w);
+        dma_tile(B + (long)(rbeg + st * BK) * ldb, ob, d + TILE_BYTES, w);
+    }
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+        char* cur = smem + (kt & (NSTAGE - 1)) * STAGE_BYTES;
+        char* nxt = smem + ((kt + NSTAGE - 1) & (NSTAGE - 1)) * STAGE_BYTES;
+        // every step issues exactly one stage so the counted wait below stays exact; past the end it re-loads
+        // the last stage into a buffer nobody reads again
+        const int rn = min(rbeg + (kt + NSTAGE - 1) * BK, rlast);
+        kstep<MF, PRIO>(cur, nxt, A + (long)rn * lda, oa, B + (long)rn * ldb, ob, wr, wc, w, l, acc);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage kt+1 landed; kt+2, kt+3 stay in flight
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (splits == 1) {
+        for_each_acc(acc, l, [&](int il, int jl, float v) {
+            const long i = i0 + wr + il, j = j0 + wc + jl;
+            if (beta != 0.f) v += beta * bf2f(*reinterpret_cast<const u16*>(C + i * ldc + j));
+            *reinterpret_cast<u16*>(C + i * ldc + j) = f2bf(v);
+        });
+    } else {
+        float* sp = slab + (long)split * Mo * No;
+        for_each_acc(acc, l, [&](int il, int jl, float v) {
+            sp[(long)(i0 + wr + il) * No + j0 + wc + jl] = v;
+        });
+    }
+}
+
+}  // namespace g256
 }  // namespace gemm
 }  // namespace bpe
 
@@ -196,21 +437,57 @@ using namespace bpe::gemm;
 
 size_t gemm_lds_bytes() { return 4 * (size_t)TILE_BYTES; }
 
-bool gemm_shape_ok(int Mo, int No, int R, int splits) {
+bool gemm_shape_ok(int Mo, int No, int R, int splits, int tile) {
+    if (tile == 256)
+        return Mo % 256 == 0 && No % 256 == 0 && splits >= 1 && R % (g256::BK * splits) == 0 &&
+               R / splits >= g256::BK * (g256::NSTAGE - 1);
     return Mo % BM == 0 && No % BN == 0 && splits >= 1 && R % (BK * splits) == 0;
 }
 
+template <int MF, bool PRIO>
+static void launch_g256_v(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
+                          float beta, int Mo, int No, int R, int splits, hipStream_t s) {
+    static bool attr = false;  // > 64 KiB dynamic LDS must be opted into once per instantiation
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)g256::gemm256_tn_kernel<MF, PRIO>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, g256::LDS_BYTES);
+        attr = true;
+    }
+    const int grid = (Mo / 256) * (No / 256) * splits;
+    g256::gemm256_tn_kernel<MF, PRIO><<<grid, g256::NT, g256::LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, Mo,
+                                                                                No, R, splits);
+}
+
+// variant (BPE_G256_VARIANT, read once): bit 0 = 16x16x32 MFMA, bit 1 = setprio'd MFMA cluster
+static void launch_g256(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
+                        float beta, int Mo, int No, int R, int splits, hipStream_t s) {
+    static int variant = [] {
+        const char* e = getenv("BPE_G256_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    switch (variant & 3) {
+        case 0: launch_g256_v<32, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;
+        case 1: launch_g256_v<16, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;
+        case 2: launch_g256_v<32, true>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;
+        default: launch_g256_v<16, true>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;
+    }
+}
+
 void launch_gemm(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-                 float beta, int Mo, int No, int R, int splits, float* slab, hipStream_t s) {
-    const int grid = (Mo / BM) * (No / BN) * splits;
-    const size_t lds = gemm_lds_bytes();
+                 float beta, int Mo, int No, int R, int splits, float* slab, int tile, hipStream_t s) {
     const __bf16* a = (const __bf16*)A;
     const __bf16* b = (const __bf16*)B;
     __bf16* c = (__bf16*)C;
+    if (tile == 256) {  // token-major operands only (host-checked)
+        launch_g256(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s);
+    } else {
+        const int grid = (Mo / BM) * (No / BN) * splits;
+        const size_t lds = gemm_lds_bytes();
 #define G(AK, BKK) gemm_kernel<AK, BKK><<<grid, 256, lds, s>>>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits)
-    if (a_kmajor) { if (b_kmajor) G(true, true); else G(true, false); }
-    else { if (b_kmajor) G(false, true); else G(false, false); }
+        if (a_kmajor) { if (b_kmajor) G(true, true); else G(true, false); }
+        else { if (b_kmajor) G(false, true); else G(false, false); }
 #undef G
+    }
     if (splits > 1) {
         const long total4 = (long)Mo * No / 4;
         const int g = (int)std::min<long>((total4 + 255) / 256, 2048);

@@ -52,9 +52,9 @@ void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* 
 
 // gemm.hip
 size_t gemm_lds_bytes();
-bool gemm_shape_ok(int Mo, int No, int R, int splits);
+bool gemm_shape_ok(int Mo, int No, int R, int splits, int tile);
 void launch_gemm(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-                 float beta, int Mo, int No, int R, int splits, float* slab, hipStream_t s);
+                 float beta, int Mo, int No, int R, int splits, float* slab, int tile, hipStream_t s);
 
 // rope.hip
 void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,

@@ -253,7 +253,7 @@ at::Tensor softmax_bwd(const at::Tensor& dy, const at::Tensor& y) {
 // ---------------------------------------------------------------- GEMM (split-K, transposed-LDS operands)
 // C[Mo, No] = beta * C + op(A) . op(B); A is [Mo, R] (a_kmajor) or [R, Mo]; B is [No, R] (b_kmajor) or [R, No].
 void gemm(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor, at::Tensor C, double beta,
-          int64_t splits) {
+          int64_t splits, int64_t tile) {
     check_cuda(C, "C");
     TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
                     C.scalar_type() == at::kBFloat16, "gemm: bf16 operands required");
@@ -264,13 +264,17 @@ void gemm(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor
     TORCH_CHECK((a_kmajor ? A.size(0) : A.size(1)) == Mo, "gemm: A / C shape mismatch");
     TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == No && (b_kmajor ? B.size(1) : B.size(0)) == R,
                 "gemm: B shape mismatch");
-    TORCH_CHECK(gemm_shape_ok(Mo, No, R, (int)splits), "gemm: Mo/No must be multiples of 128 and R of 64*splits");
+    TORCH_CHECK(tile == 128 || (tile == 256 && !a_kmajor && !b_kmajor),
+                "gemm: tile must be 128, or 256 with both operands token-major (weight-gradient layout)");
+    TORCH_CHECK(gemm_shape_ok(Mo, No, R, (int)splits, (int)tile),
+                "gemm: Mo/No must be multiples of the tile and R of 64*splits");
     TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 && C.stride(0) % 4 == 0, "gemm: 16-byte row alignment");
     DevGuard g(C.device());
     at::Tensor slab;
     if (splits > 1) slab = at::empty({splits, Mo, No}, C.options().dtype(at::kFloat));
     launch_gemm(a_kmajor, b_kmajor, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
-                (float)beta, Mo, No, R, (int)splits, splits > 1 ? slab.data_ptr<float>() : nullptr, cur_stream());
+                (float)beta, Mo, No, R, (int)splits, splits > 1 ? slab.data_ptr<float>() : nullptr, (int)tile,
+                cur_stream());
 }
 
 // ---------------------------------------------------------------- FP8 quantisation (delayed scaling)
@@ -398,7 +402,7 @@ TORCH_LIBRARY(bpe_hip, m) {
           "float b2, float eps, float wd, float bc1, float bc2_sqrt, Tensor? gscale) -> ()");
     m.def("grad_norm(Tensor[] tensors, float max_norm) -> (Tensor, Tensor)");
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
-    m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits) -> ()");
+    m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
     m.def("update_scales(Tensor(a!) amax_bits, Tensor(b!) hist, Tensor(c!) scale, Tensor(d!) inv_scale, int pos, "
           "float margin) -> ()");

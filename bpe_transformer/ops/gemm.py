@@ -1,13 +1,15 @@
-"""Hand-written gfx950 split-K MFMA GEMM (``csrc/gemm.hip``) for weight gradients.
+"""Hand-written gfx950 split-K MFMA GEMMs (``csrc/gemm.hip``) for weight gradients.
 
 ``accumulate_weight_grad(g, dy, x)`` computes ``g += dy^T @ x`` where
 ``dy: [T, N]`` and ``x: [T, K]`` are token-major activations (T = batch*seq)
 and ``g: [N, K]`` is a view of the flat bf16 gradient buffer.  The reduction
 runs over all T tokens, which for a training step is large (16k-64k) while
 N x K is small: the kernel splits T across workgroups (enough to fill all 256
-CUs) and reduces the fp32 partials deterministically into ``g``.  Shapes the
-kernel does not cover (N or K not a multiple of 128, T not a multiple of
-64 * splits) go to hipBLASLt (``addmm_``).
+CUs) and reduces the fp32 partials deterministically into ``g``.
+
+Two kernels: the 256 x 256 tile (8 waves, LDS-DMA staging, one workgroup per
+CU) for shapes that are multiples of 256, the 128 x 128 tile otherwise.
+Shapes neither covers go to hipBLASLt (``addmm_``).
 """
 
 from __future__ import annotations
@@ -37,6 +39,32 @@ def choose_splits(n: int, k: int, t: int, target: int = _TARGET_WGS, min_iters: 
 
 
 _MAX_TILES = int(os.environ.get("BPE_DW_GEMM_MAX_TILES", "160"))
+_TILE256 = os.environ.get("BPE_GEMM_TILE256", "1") == "1"
+_CUS = 256
+
+
+def choose_splits_256(n: int, k: int, t: int) -> int:
+    """Split count for the 256-tile kernel from a wave-quantised cost model.
+
+    time(s) ~ ceil(tiles*s / CUs) * (t/s/32) * t_kstep  +  (s > 1) * slab traffic (s*n*k fp32 written + read).
+    One workgroup per CU, so the grid runs in ceil(tiles*s/256) waves of equal length.
+    """
+    tiles = (n // 256) * (k // 256)
+    nk = t // 32
+    t_kstep = 0.8e-6  # one 256x256x32 MFMA step at ~50% of the dense bf16 rate
+    best, best_cost = 1, None
+    for s in range(1, 65):
+        if nk % s or nk // s < 8:
+            continue
+        waves = -(-tiles * s // _CUS)
+        cost = waves * (nk // s) * t_kstep + (2 * s * n * k * 4 / 4.0e12 if s > 1 else 0.0)
+        if best_cost is None or cost < best_cost * 0.97:
+            best, best_cost = s, cost
+    return best
+
+
+def use_tile256(n: int, k: int, t: int) -> bool:
+    return _TILE256 and n % 256 == 0 and k % 256 == 0 and t % 256 == 0
 
 
 def supported(n: int, k: int, t: int) -> bool:
@@ -49,16 +77,75 @@ def supported(n: int, k: int, t: int) -> bool:
     return n % 128 == 0 and k % 128 == 0 and t % 64 == 0 and (n // 128) * (k // 128) <= _MAX_TILES
 
 
-def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
-    """``g += dy.T @ x`` (bf16, fp32 accumulation)."""
+_AUTOTUNE = os.environ.get("BPE_GEMM_AUTOTUNE", "1") == "1"
+_route: dict[tuple[int, int, int], str] = {}
+
+
+def _candidates(n: int, k: int, t: int) -> list[str]:
+    c = []
+    if use_tile256(n, k, t):
+        c.append("hip256")
+    elif supported(n, k, t):
+        c.append("hip128")
+    return c + ["blas"]
+
+
+def _run(route: str, g: Tensor, dy: Tensor, x: Tensor) -> None:
     n, k = g.shape
     t = dy.shape[0]
-    if (_ENABLED and g.is_cuda and g.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
-            and x.dtype == torch.bfloat16 and supported(n, k, t) and g.stride(1) == 1 and dy.stride(1) == 1
-            and x.stride(1) == 1):
-        ops().gemm(dy, False, x, False, g, 1.0, choose_splits(n, k, t))
+    if route == "hip256":
+        ops().gemm(dy, False, x, False, g, 1.0, choose_splits_256(n, k, t), 256)
+    elif route == "hip128":
+        ops().gemm(dy, False, x, False, g, 1.0, choose_splits(n, k, t), 128)
     else:
         g.addmm_(dy.t(), x)
+
+
+def _tune(key: tuple[int, int, int], cands: list[str], g: Tensor, dy: Tensor, x: Tensor) -> str:
+    """Time each route once per shape on a scratch output (CUDA events, 3 reps) and keep the fastest."""
+    if not _AUTOTUNE or len(cands) == 1 or torch.cuda.is_current_stream_capturing():
+        return cands[0]
+    scratch = torch.empty_like(g)
+    best, best_t = cands[0], float("inf")
+    for c in cands:
+        _run(c, scratch, dy, x)  # warm (kernel attributes, library heuristics)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(3):
+            _run(c, scratch, dy, x)
+        e.record()
+        e.synchronize()
+        ms = s.elapsed_time(e)
+        if ms < best_t:
+            best, best_t = c, ms
+    return best
+
+
+def weight_grad_route(n: int, k: int, t: int) -> str | None:
+    """The route chosen for a dW shape (None until first use)."""
+    return _route.get((n, k, t))
+
+
+def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
+    """``g += dy.T @ x`` (bf16, fp32 accumulation).
+
+    Routes per shape between the 256-tile HIP kernel, the 128-tile HIP kernel and hipBLASLt; the first call
+    for a shape times the candidates (``BPE_GEMM_AUTOTUNE=0``: take the HIP kernel whenever it applies).
+    Measured (benchmarks/gemm_dw.py): the HIP kernel wins every GPT-2-small dW shape 1.4-2.3x; hipBLASLt
+    keeps Llama's 2048 x 5632 one.
+    """
+    n, k = g.shape
+    t = dy.shape[0]
+    ok = (_ENABLED and g.is_cuda and g.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
+          and x.dtype == torch.bfloat16 and g.stride(1) == 1 and dy.stride(1) == 1 and x.stride(1) == 1)
+    if not ok:
+        g.addmm_(dy.t(), x)
+        return
+    key = (n, k, t)
+    route = _route.get(key)
+    if route is None:
+        route = _route[key] = _tune(key, _candidates(n, k, t), g, dy, x)
+    _run(route, g, dy, x)
 
 
 def matmul_nt(a: Tensor, b: Tensor, out: Tensor | None = None, beta: float = 0.0) -> Tensor:
@@ -68,5 +155,5 @@ def matmul_nt(a: Tensor, b: Tensor, out: Tensor | None = None, beta: float = 0.0
     if out is None:
         out = torch.empty(m, n, device=a.device, dtype=a.dtype)
         beta = 0.0
-    ops().gemm(a, True, b, True, out, beta, choose_splits(m, n, r))
+    ops().gemm(a, True, b, True, out, beta, choose_splits(m, n, r), 128)
     return out

@@ -77,3 +77,25 @@ def test_dp2_matches_single_process(bucket_mb):
     for _ in range(3):
         eng.train_step([(torch.cat([x0, x1]), torch.cat([y0, y1]))])
     torch.testing.assert_close(res[0][0], eng.flat.data, atol=2e-5, rtol=1e-4)
+
+
+def _launched(out_dir):
+    import torch.distributed as dist
+
+    from bpe_transformer.parallel import cleanup, init_distributed
+
+    info = init_distributed("cpu")
+    t = torch.tensor([float(info.rank + 1)])
+    dist.all_reduce(t)
+    with open(os.path.join(out_dir, f"rank{info.rank}.txt"), "w") as f:
+        f.write(f"{info.world_size} {t.item()} {os.environ['MASTER_ADDR']}")
+    cleanup()
+
+
+def test_launcher_spawns_ranks(tmp_path):
+    """parallel.launch: torchrun-style env in every rank, gloo collective across them."""
+    from bpe_transformer.parallel.launch import launch
+
+    launch(_launched, 2, str(tmp_path))
+    for r in range(2):
+        assert (tmp_path / f"rank{r}.txt").read_text() == "2 3.0 127.0.0.1"

@@ -233,17 +233,35 @@ def test_grad_norm_clip(gpu_device):
 # ---------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("splits", [1, 4])
-def test_gemm_layouts(gpu_device, a_k, b_k, splits):
+@pytest.mark.parametrize("tile", [128, 256])
+def test_gemm_layouts(gpu_device, a_k, b_k, splits, tile):
+    if tile == 256 and (a_k or b_k):
+        pytest.skip("the 256-tile kernel serves the weight-gradient (token-major) layout only")
     torch.manual_seed(0)
-    Mo, No, R = 256, 384, 1024
+    Mo, No, R = (256, 384, 1024) if tile == 128 else (512, 768, 1536)
     A = torch.randn(Mo, R, device=gpu_device, dtype=torch.bfloat16)
     B = torch.randn(No, R, device=gpu_device, dtype=torch.bfloat16)
     Am = A if a_k else A.t().contiguous()
     Bm = B if b_k else B.t().contiguous()
     C = torch.randn(Mo, No, device=gpu_device, dtype=torch.bfloat16)
     ref = C.float() * 0.5 + A.float() @ B.float().t()
-    torch.ops.bpe_hip.gemm(Am, a_k, Bm, b_k, C, 0.5, splits)
+    torch.ops.bpe_hip.gemm(Am, a_k, Bm, b_k, C, 0.5, splits, tile)
     assert rel(C.cpu(), ref.cpu()) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2304, 768, 8192), (768, 768, 8192), (11264, 2048, 2048), (2048, 5632, 4096)])
+def test_weight_grad_shapes(gpu_device, shape):
+    """Model dW shapes through the routing in ops.gemm (256-tile kernel, split-K choice)."""
+    from bpe_transformer.ops.gemm import accumulate_weight_grad
+
+    n, k, t = shape
+    torch.manual_seed(0)
+    dy = torch.randn(t, n, device=gpu_device, dtype=torch.bfloat16)
+    x = torch.randn(t, k, device=gpu_device, dtype=torch.bfloat16)
+    g = torch.randn(n, k, device=gpu_device, dtype=torch.bfloat16)
+    ref = g.float() + dy.float().t() @ x.float()
+    accumulate_weight_grad(g, dy, x)
+    assert rel(g, ref) < 1e-2
 
 
 def test_weight_grad_accumulate(gpu_device):
