@@ -23,12 +23,14 @@
 //   (guide G12).  256-key workgroups halve the atomic bytes of a 128-key
 //   design; at ~1.3 TB/s chip-wide those bytes set this kernel's floor.
 // RoPE: Q tiles are rotated while staged, K once at the start; dK is
-// un-rotated in the epilogue and dQ in the convert kernel.  GQA: a workgroup
-// sweeps every query head of its kv head.  Order: heaviest key blocks first.
+// un-rotated in the epilogue and dQ in the convert kernel.  GQA: one
+// workgroup per query head; the G partial dK / dV of a kv head are summed in
+// fp32 by fa_dkv_reduce_kernel.  Order: heaviest key blocks first.
 #include "fa_common.h"
 #include "kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace bpe {
 namespace fa {
@@ -84,8 +86,9 @@ __global__ void __launch_bounds__(BwdCfg<D>::NW * 64, 1)
 fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv, long ld_q,
               long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
               const float* __restrict__ DELTA, float* __restrict__ dQacc, __bf16* __restrict__ dK,
-              __bf16* __restrict__ dV, long ld_dkv, const float* __restrict__ cosT, const float* __restrict__ sinT,
-              int B, int H, int Hkv, int S, float scale_log2, float scale) {
+              __bf16* __restrict__ dV, long ld_dkv, float* __restrict__ dKVpart, const float* __restrict__ cosT,
+              const float* __restrict__ sinT, int B, int H, int Hkv, int S, float scale_log2, float scale,
+              int flags) {
     using C = BwdCfg<D>;
     constexpr int NW = C::NW, NT = NW * 64, RB = C::RB, CPR = D / 8, QT = C::QT;
     constexpr int SPT = (64 * CPR + NT - 1) / NT;  // staged chunks per thread per tile (Q and dO each)
@@ -101,11 +104,15 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     float* dltS = lseS + 128;                                              // [2][64]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
-    const int BHk = B * Hkv;
-    const int kb = (int)(blockIdx.x / BHk);
-    const int bhk = blockIdx.x % BHk;
-    const int b = bhk / Hkv, hk = bhk % Hkv;
+    // one workgroup per (key block, batch, QUERY head): with GQA the G query heads of a kv head run in
+    // parallel (their dK / dV partials are summed by fa_dkv_reduce_kernel) instead of one workgroup sweeping
+    // all G heads -- with causal masking that serial sweep left most CUs idle behind the key-block-0 groups.
+    const int BH = B * H;
+    const int kb = (int)(blockIdx.x / BH);
+    const int bh = blockIdx.x % BH;
+    const int b = bh / H, h = bh % H;
     const int G = H / Hkv;
+    const int hk = h / G;
     const int kb0 = kb * C::KB, kw0 = kb0 + 32 * w;
     const int key = kw0 + l31;
     const bool key_ok = key < S;
@@ -135,13 +142,12 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
 
     const int m_start = CAUSAL ? kb0 : 0;  // kb0 is a multiple of 128 -> 64-aligned
     const int nqt = (S - m_start + 63) / 64;
-    const int total_it = nqt * G;
+    const int total_it = nqt;
 
     u16x8 qreg[SPT], oreg[SPT];
     float lreg = 0.f, dreg = 0.f;
     auto load_tile = [&](int it) {
-        const int h = hk * G + it / nqt;
-        const int m0 = m_start + (it % nqt) * 64;
+        const int m0 = m_start + it * 64;
         const __bf16* qb = Q + (long)b * S * ld_q + (long)h * D;
         const __bf16* ob = dO + (long)b * S * ld_do + (long)h * D;
 #pragma unroll
@@ -164,7 +170,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
         }
     };
     auto write_tile = [&](int it, int buf) {
-        const int m0 = m_start + (it % nqt) * 64;
+        const int m0 = m_start + it * 64;
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int e = tid + NT * i, row = e / CPR, c = e % CPR;
@@ -192,8 +198,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
 
     for (int it = 0; it < total_it; ++it) {
         const int cur = it & 1;
-        const int h = hk * G + it / nqt;
-        const int m0 = m_start + (it % nqt) * 64;
+        const int m0 = m_start + it * 64;
         if (it + 1 < total_it) load_tile(it + 1);
         char* Qc = Qs + cur * QT;
         char* Oc = dOs + cur * QT;
@@ -220,7 +225,12 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                     dp[qt] = mfma(lds_row16(Oc, off), vf[ks], dp[qt]);
                 }
             }
-            const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + 64 > S) || !key_ok;
+            // wave-uniform test (a per-lane one turns every element's mask into an exec-masked branch)
+            const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + 64 > S) || (kw0 + 32 > S);
+            // valid  <=>  key <= q < S  <=>  (unsigned)(q - key) < (unsigned)(S - key); a key past the end gets
+            // klim = S, an empty range
+            const int klim = CAUSAL ? (key_ok ? key : S) : (key_ok ? 0 : S);
+            const unsigned span = (unsigned)(S - klim);
 #pragma unroll
             for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
@@ -232,10 +242,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                     for (int j = 0; j < 4; ++j) {
                         const int r = 4 * i + j;
                         float p = fast_exp2(sp[qt][r] * scale_log2 - lv[j]);
-                        if (need_mask) {
-                            const int qg = m0 + qi + j;
-                            if ((CAUSAL && key > qg) || qg >= S || !key_ok) p = 0.f;
-                        }
+                        if (need_mask) p = ((unsigned)(m0 + qi + j - klim) < span) ? p : 0.f;
                         sp[qt][r] = p;
                         dp[qt][r] = p * (dp[qt][r] - dlt[j]);
                     }
@@ -313,17 +320,18 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                     }
                 }
             }
-            if (part == 0) {
+            // dQacc rows are padded to a multiple of 64 per batch (Spad): rows q >= S of the last tile land
+            // in padding (and carry zeros: P = 0 there), so the atomics need no per-element guard
+            if (part == 0 && !(flags & 1)) {
+                const long HD = (long)H * D;
+                const int Spad = (S + 63) & ~63;
 #pragma unroll
                 for (int tt = 0; tt < C::TPW; ++tt) {
                     const int tile = (C::TPW == 1) ? (w % C::OUT_TILES) : (w * C::TPW + tt);
                     const int qt2 = tile / DT, dt2 = tile % DT;
-                    float* dqp = dQacc + ((long)b * S) * H * D + (long)h * D + dt2 * 32 + l31;
+                    float* dqp = dQacc + ((long)b * Spad + m0 + qt2 * 32 + 4 * hh) * HD + (long)h * D + dt2 * 32 + l31;
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int qg = m0 + qt2 * 32 + acc_row(r, hh);
-                        if (qg < S) atomicAdd(dqp + (long)qg * H * D, acc[tt][r]);
-                    }
+                    for (int r = 0; r < 16; ++r) atomicAdd(dqp + ((r & 3) + 8 * (r >> 2)) * HD, acc[tt][r]);
                 }
             }
         }
@@ -331,6 +339,23 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
         __syncthreads();
     }
 
+    // ---- GQA: fp32 partials of this query head -> [b, s, h, {dK, dV}, D] for the reduce kernel
+    if (G > 1) {
+        if (key_ok) {
+            float* pk = dKVpart + (((long)b * S + key) * H + h) * 2 * D;
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int d0 = dt * 32 + 8 * i + 4 * hh;
+                    *reinterpret_cast<f32x4*>(pk + d0) =
+                        f32x4{dk[dt][4 * i], dk[dt][4 * i + 1], dk[dt][4 * i + 2], dk[dt][4 * i + 3]};
+                    *reinterpret_cast<f32x4*>(pk + D + d0) =
+                        f32x4{dv[dt][4 * i], dv[dt][4 * i + 1], dv[dt][4 * i + 2], dv[dt][4 * i + 3]};
+                }
+        }
+        return;
+    }
     // ---- epilogue: dK = scale * R(-pos) dK^T, dV = dV^T  (key on the lane, d in registers)
     if (key_ok) {
         __bf16* dkp = dK + ((long)b * S + key) * ld_dkv + (long)hk * D;
@@ -361,6 +386,45 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     }
 }
 
+// GQA: dK = scale * R(-pos) sum_g dK_g, dV = sum_g dV_g over the G query heads of each kv head
+template <int D, bool ROPE>
+__global__ void __launch_bounds__(256) fa_dkv_reduce_kernel(const float* __restrict__ part, __bf16* __restrict__ dK,
+                                                            __bf16* __restrict__ dV, long ld_dkv,
+                                                            const float* __restrict__ cosT,
+                                                            const float* __restrict__ sinT, int B, int H, int Hkv,
+                                                            int S, float scale) {
+    const int G = H / Hkv;
+    const long total = (long)B * S * Hkv * (D / 4);
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const long row = i / (D / 4);  // (b, s, hk)
+        const int d0 = (int)(i % (D / 4)) * 4;
+        const long bs = row / Hkv;
+        const int hk = (int)(row % Hkv);
+        const long s = bs % S;
+        const float* p = part + (bs * H + (long)hk * G) * 2 * D + d0;
+        f32x4 k4 = {0.f, 0.f, 0.f, 0.f}, v4 = {0.f, 0.f, 0.f, 0.f};
+        for (int g = 0; g < G; ++g) {
+            k4 += *reinterpret_cast<const f32x4*>(p + (long)g * 2 * D);
+            v4 += *reinterpret_cast<const f32x4*>(p + (long)g * 2 * D + D);
+        }
+        float x[4] = {k4[0] * scale, k4[1] * scale, k4[2] * scale, k4[3] * scale};
+        if (ROPE) {
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+                const float c = cosT[s * (D / 2) + d0 / 2 + pr];
+                const float sn = sinT[s * (D / 2) + d0 / 2 + pr];
+                const float a = x[2 * pr], bb = x[2 * pr + 1];
+                x[2 * pr] = a * c + bb * sn;
+                x[2 * pr + 1] = -a * sn + bb * c;
+            }
+        }
+        *reinterpret_cast<u16x4*>(dK + bs * ld_dkv + (long)hk * D + d0) = u16x4{f2bf(x[0]), f2bf(x[1]), f2bf(x[2]),
+                                                                                 f2bf(x[3])};
+        *reinterpret_cast<u16x4*>(dV + bs * ld_dkv + (long)hk * D + d0) = u16x4{f2bf(v4[0]), f2bf(v4[1]),
+                                                                                 f2bf(v4[2]), f2bf(v4[3])};
+    }
+}
+
 // dQ (fp32, roped space, unscaled) -> bf16 output slice: dq = scale * R(-pos) dQacc
 template <int D, bool ROPE>
 __global__ void __launch_bounds__(256) fa_dq_convert_kernel(const float* __restrict__ dQacc, __bf16* __restrict__ dq,
@@ -374,7 +438,8 @@ __global__ void __launch_bounds__(256) fa_dq_convert_kernel(const float* __restr
         const long bs = row / H;
         const int h = (int)(row % H);
         const long s = bs % S;
-        f32x4 v = *reinterpret_cast<const f32x4*>(dQacc + row * D + d0);
+        const long src = ((bs / S) * ((S + 63) & ~63) + s) * H + h;  // padded dQacc row
+        f32x4 v = *reinterpret_cast<const f32x4*>(dQacc + src * D + d0);
         float x[4] = {v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale};
         if (ROPE) {
 #pragma unroll
@@ -408,7 +473,8 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
         fa_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(a.o, a.ld_o, a.dout, a.ld_do, a.delta,
                                                                                a.B, a.H, a.S);
     }
-    (void)hipMemsetAsync(a.dq_acc, 0, (size_t)a.B * a.S * a.H * D * sizeof(float), s);
+    const size_t spad = (size_t)((a.S + 63) & ~63);
+    (void)hipMemsetAsync(a.dq_acc, 0, (size_t)a.B * spad * a.H * D * sizeof(float), s);
     const int nkb = (a.S + Cfg::KB - 1) / Cfg::KB;
     static bool lds_attr = false;  // > 64 KiB of dynamic LDS: opt in once (before any graph capture)
     if (!lds_attr) {
@@ -416,9 +482,19 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
         lds_attr = true;
     }
-    fa_bwd_kernel<D, C, R><<<nkb * a.B * a.Hkv, Cfg::NW * 64, Cfg::LDS, s>>>(
-        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv, a.cos, a.sin,
-        a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale);
+    static const int dbg = [] {
+        const char* e = getenv("BPE_FA_DEBUG");  // bit 0: skip the dQ atomics (timing diagnostics only)
+        return e ? atoi(e) : 0;
+    }();
+    fa_bwd_kernel<D, C, R><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
+        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv, a.dkv_part,
+        a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, dbg);
+    if (a.Hkv < a.H) {
+        const long tkv = (long)a.B * a.S * a.Hkv * (D / 4);
+        const int g2 = (int)std::min<long>((tkv + 255) / 256, 4096);
+        fa_dkv_reduce_kernel<D, R><<<g2, 256, 0, s>>>(a.dkv_part, a.dk, a.dv, a.ld_dkv, a.cos, a.sin, a.B, a.H, a.Hkv,
+                                                      a.S, a.scale);
+    }
     const long total = (long)a.B * a.S * a.H * (D / 4);
     const int grid = (int)std::min<long>((total + 255) / 256, 4096);
     fa_dq_convert_kernel<D, R><<<grid, 256, 0, s>>>(a.dq_acc, a.dq, a.ld_dq, a.cos, a.sin, a.B, a.H, a.S, a.scale);

@@ -84,6 +84,7 @@ struct FaArgs {
     __bf16* dk;
     __bf16* dv;
     long ld_dkv;
+    float* dkv_part;  // GQA only: [B*S][H][2][D] fp32 per-query-head dK / dV partials
 };
 size_t fa_fwd_lds_bytes(int D);
 size_t fa_bwd_lds_bytes(int D);

@@ -359,6 +359,7 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
                   const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cos, const at::Tensor& sin, int64_t B,
                   int64_t S, int64_t H, int64_t Hkv, int64_t D, bool causal, bool use_rope, double scale) {
     TORCH_CHECK(D == 64 || D == 128, "flash attention: head dim must be 64 or 128");
+    TORCH_CHECK(Hkv > 0 && H % Hkv == 0, "flash attention: H must be a multiple of Hkv");
     check_qkv(q, B * S, H * D, "q");
     check_qkv(k, B * S, Hkv * D, "k");
     check_qkv(v, B * S, Hkv * D, "v");
@@ -369,7 +370,9 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     const int64_t W = (H + 2 * Hkv) * D;
     auto dqkv = at::empty({B * S, W}, q.options());
     auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-    auto dq_acc = at::empty({B * S, H * D}, q.options().dtype(at::kFloat));
+    auto dq_acc = at::empty({B * ((S + 63) / 64 * 64), H * D}, q.options().dtype(at::kFloat));  // rows padded
+    at::Tensor dkv_part;
+    if (Hkv < H) dkv_part = at::empty({B * S, H * 2 * D}, q.options().dtype(at::kFloat));
     FaArgs a{};
     a.q = (const __bf16*)q.data_ptr(); a.k = (const __bf16*)k.data_ptr(); a.v = (const __bf16*)v.data_ptr();
     a.ld_q = q.stride(0); a.ld_kv = k.stride(0);
@@ -382,6 +385,7 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     __bf16* base = (__bf16*)dqkv.data_ptr();
     a.dq = base; a.ld_dq = W;
     a.dk = base + H * D; a.dv = base + (H + Hkv) * D; a.ld_dkv = W;
+    a.dkv_part = Hkv < H ? dkv_part.data_ptr<float>() : nullptr;
     launch_fa_bwd(a, cur_stream());
     return dqkv;
 }

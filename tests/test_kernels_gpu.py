@@ -306,7 +306,7 @@ def test_flash_attention_d64(gpu_device, S, rope, causal):
         assert e < 3e-2, (name, e)
 
 
-@pytest.mark.parametrize("D,H,Hkv", [(128, 4, 4), (64, 8, 2)])
+@pytest.mark.parametrize("D,H,Hkv", [(128, 4, 4), (64, 8, 2), (128, 8, 4), (64, 32, 4)])
 def test_flash_attention_d128_and_gqa(gpu_device, D, H, Hkv):
     o, g, orf, gr = _fa_case(gpu_device, 2, 192, H, Hkv, D, True, True, seed=1)
     assert rel(o.cpu(), orf) < 2e-2
