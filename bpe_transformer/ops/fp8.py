@@ -44,6 +44,21 @@ class Fp8State:
         ops().update_scales(self.amax, self.hist, self.scale, self.inv_scale, self.pos, self.margin)
         self.pos += 1
 
+    def state_dict(self) -> dict:
+        """Scale state for checkpoints (amax history, current scales, ring position)."""
+        return {"hist": self.hist.clone(), "scale": self.scale.clone(), "inv_scale": self.inv_scale.clone(),
+                "pos": self.pos, "margin": self.margin}
+
+    def load_state_dict(self, sd: dict) -> None:
+        if sd["hist"].shape != self.hist.shape:
+            raise ValueError(f"fp8 state shape {tuple(sd['hist'].shape)} != {tuple(self.hist.shape)}")
+        self.hist.copy_(sd["hist"])
+        self.scale.copy_(sd["scale"])
+        self.inv_scale.copy_(sd["inv_scale"])
+        self.amax.zero_()
+        self.pos = int(sd["pos"])
+        self.margin = float(sd["margin"])
+
     def matmul(self, x: Tensor, w: Tensor, x_slot: int, w_slot: int) -> Tensor:
         """``x @ w.T`` in fp8 with bf16 output; x: [M, K] bf16, w: [N, K] bf16."""
         x8 = self.cast(x, x_slot)

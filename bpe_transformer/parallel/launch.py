@@ -9,9 +9,10 @@ MASTER_PORT) in each child before ``fn`` runs, and re-raises the first
 child failure in the parent.  ``fn`` then calls
 :func:`bpe_transformer.parallel.init_distributed` as under torchrun.
 
-CLI (runs a script's ``__main__`` in every rank)::
+CLI (runs a script's, or with ``-m`` a module's, ``__main__`` in every rank)::
 
     python -m bpe_transformer.parallel.launch --nproc 8 train.py --config ...
+    python -m bpe_transformer.parallel.launch --nproc 8 -m bpe_transformer.train --preset gpt2-small
 """
 
 from __future__ import annotations
@@ -50,19 +51,32 @@ def launch(fn: Callable[..., Any], nprocs: int, *args: Any, port: int | None = N
                        start_method="spawn")
 
 
-def _run_script(path: str, argv: list[str]) -> None:
+def _run_script(path: str, argv: list[str], module: bool = False) -> None:
     sys.argv = [path, *argv]
-    runpy.run_path(path, run_name="__main__")
+    if module:
+        runpy.run_module(path, run_name="__main__", alter_sys=True)
+    else:
+        runpy.run_path(path, run_name="__main__")
 
 
 def main(argv: list[str] | None = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--nproc", type=int, default=1)
     ap.add_argument("--port", type=int, default=None)
-    ap.add_argument("script")
-    ap.add_argument("args", nargs=argparse.REMAINDER)
-    a = ap.parse_args(argv)
-    launch(_run_script, a.nproc, a.script, a.args, port=a.port)
+    ap.add_argument("target", help="script path, or -m MODULE")
+    # everything after the script / module name belongs to it
+    split = next((i for i, t in enumerate(argv) if not t.startswith("--") and (i == 0 or argv[i - 1] not in
+                  ("--nproc", "--port"))), len(argv))
+    module = split < len(argv) and argv[split] == "-m"
+    if module:
+        if split + 1 >= len(argv):
+            ap.error("-m needs a module name")
+        own, target, rest = argv[:split], argv[split + 1], argv[split + 2:]
+    else:
+        own, target, rest = argv[:split], (argv[split] if split < len(argv) else None), argv[split + 1:]
+    a = ap.parse_args(own + ([target] if target else []))
+    launch(_run_script, a.nproc, a.target, rest, module, port=a.port)
     return 0
 
 

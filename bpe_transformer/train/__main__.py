@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 
 from ..models.config import get_preset
@@ -36,7 +37,8 @@ def main(argv: list[str] | None = None) -> int:
         print(json.dumps(cfg.to_dict(), indent=2))
         return 0
     out = Trainer(cfg).fit()
-    print(json.dumps(out))
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps(out))
     return 0
 
 

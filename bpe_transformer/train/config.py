@@ -47,6 +47,7 @@ class TrainConfig:
     seed: int = 1234
     device: str = "auto"  # auto | cuda | cpu
     dtype: str = "auto"  # auto (bf16 on GPU, fp32 on CPU) | bf16 | fp32
+    precision: str = "default"  # default | fp8 (block projections' forward GEMMs in e4m3, delayed scaling; GPU)
     bucket_mb: float = 64.0
     log_every: int = 10
     eval_every: int = 0

@@ -57,6 +57,10 @@ class Trainer:
         self.dtype = dtype
         torch.manual_seed(cfg.seed)  # identical init everywhere; rank 0 is broadcast anyway
         self.model = TransformerLM.from_config(cfg.model, device=dev, dtype=dtype)
+        if cfg.precision == "fp8":
+            if dev.type != "cuda":
+                raise ValueError("precision=fp8 needs the GPU path (MI355X fp8 MFMA)")
+            self.model.enable_fp8()
         o = cfg.optim
         self.engine = TrainEngine(self.model, self.info, lr=o.lr, betas=o.betas, eps=o.eps,
                                   weight_decay=o.weight_decay, max_grad_norm=o.max_grad_norm,
@@ -81,8 +85,11 @@ class Trainer:
         return Path(self.cfg.ckpt_dir) / f"ckpt_{it:08d}.pt"
 
     def save(self, it: int) -> None:
+        extra = {}
+        if self.model.fp8_state is not None:
+            extra["fp8"] = self.model.fp8_state.state_dict()
         save_checkpoint(self.model, _EngineOptimizerView(self.engine), it, self._ckpt_path(it), rank=self.info.rank,
-                        config=self.cfg.to_dict())
+                        config=self.cfg.to_dict(), **extra)
 
     def _resume(self, spec: str) -> None:
         path = latest_checkpoint(self.cfg.ckpt_dir) if spec == "latest" else Path(spec)
@@ -93,6 +100,8 @@ class Trainer:
         with torch.no_grad():
             self.model.load_state_dict(obj["model"])
         self.engine.load_state_dict(obj["optimizer"])
+        if self.model.fp8_state is not None and "fp8" in obj:
+            self.model.fp8_state.load_state_dict(obj["fp8"])
         self.start_iter = int(obj["iteration"])
         log.info(f"resumed from {path} at iteration {self.start_iter}")
 
