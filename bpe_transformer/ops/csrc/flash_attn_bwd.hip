@@ -81,6 +81,37 @@ __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const __bf16* __restric
     }
 }
 
+// P and dS of one 32-query half from its S / dP accumulators (key on the lane, 4 consecutive queries per
+// register group), two elements per packed instruction.  MASK: zero P where (unsigned)(q - klim) >= span,
+// with q = half start + row, passed as qoff = half start - klim.
+template <bool MASK>
+__device__ __forceinline__ void softmax_ds(f32x16& sp, f32x16& dp, const float* lc, const float* dc, int hh,
+                                           float scale_log2, int qoff, unsigned span) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int qi = 8 * i + 4 * hh;  // rows qi..qi+3
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
+        const f32x4 dl = *reinterpret_cast<const f32x4*>(dc + qi);
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+            const int r = 4 * i + j;
+            const f2 sc = {scale_log2, scale_log2};
+            const f2 x = f2{sp[r], sp[r + 1]} * sc - f2{lv[j], lv[j + 1]};
+            f2 p = {fast_exp2(x[0]), fast_exp2(x[1])};
+            if constexpr (MASK) {
+                p[0] = ((unsigned)(qoff + qi + j) < span) ? p[0] : 0.f;
+                p[1] = ((unsigned)(qoff + qi + j + 1) < span) ? p[1] : 0.f;
+            }
+            const f2 d = p * (f2{dp[r], dp[r + 1]} - f2{dl[j], dl[j + 1]});
+            sp[r] = p[0];
+            sp[r + 1] = p[1];
+            dp[r] = d[0];
+            dp[r + 1] = d[1];
+        }
+    }
+}
+
 template <int D, bool CAUSAL, bool ROPE>
 __global__ void __launch_bounds__(BwdCfg<D>::NW * 64, 1)
 fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv, long ld_q,
@@ -196,7 +227,9 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     const int trow = 4 * hh + ((l & 15) >> 2);          // tr-read row inside a 16-row k-step
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);  // tr-read column inside a 32-wide tile
 
-    for (int it = 0; it < total_it; ++it) {
+    // one query tile.  (Unrolling by two so the buffer index becomes an immediate offset was measured:
+    // the hoisted per-buffer addresses push the kernel past 256 VGPRs and it spills.)
+    auto body = [&](int it) {
         const int cur = it & 1;
         const int m0 = m_start + it * 64;
         if (it + 1 < total_it) load_tile(it + 1);
@@ -206,56 +239,35 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
         const float* dc = dltS + cur * 64;
         const bool active = !CAUSAL || (m0 + 63 >= kw0);
         if (active) {
-            bf16x8 kf[KS], vf[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const int off = swz<RB>(32 * w + l31, 2 * ks + hh);
-                kf[ks] = lds_row16(Kl, off);
-                vf[ks] = lds_row16(Vl, off);
-            }
-            f32x16 sp[2], dp[2];
-#pragma unroll
-            for (int qt = 0; qt < 2; ++qt) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) { sp[qt][r] = 0.f; dp[qt][r] = 0.f; }
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
-                    sp[qt] = mfma(lds_row16(Qc, off), kf[ks], sp[qt]);
-                    dp[qt] = mfma(lds_row16(Oc, off), vf[ks], dp[qt]);
-                }
-            }
-            // wave-uniform test (a per-lane one turns every element's mask into an exec-masked branch)
+            // the two 32-query halves one after the other: only one S / dP accumulator pair is live
             const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + 64 > S) || (kw0 + 32 > S);
-            // valid  <=>  key <= q < S  <=>  (unsigned)(q - key) < (unsigned)(S - key); a key past the end gets
-            // klim = S, an empty range
             const int klim = CAUSAL ? (key_ok ? key : S) : (key_ok ? 0 : S);
             const unsigned span = (unsigned)(S - klim);
 #pragma unroll
-            for (int qt = 0; qt < 2; ++qt)
+            for (int qt = 0; qt < 2; ++qt) {
+                f32x16 sp, dp;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int qi = qt * 32 + 8 * i + 4 * hh;  // rows qi..qi+3
-                    const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
-                    const f32x4 dlt = *reinterpret_cast<const f32x4*>(dc + qi);
+                for (int r = 0; r < 16; ++r) { sp[r] = 0.f; dp[r] = 0.f; }
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int r = 4 * i + j;
-                        float p = fast_exp2(sp[qt][r] * scale_log2 - lv[j]);
-                        if (need_mask) p = ((unsigned)(m0 + qi + j - klim) < span) ? p : 0.f;
-                        sp[qt][r] = p;
-                        dp[qt][r] = p * (dp[qt][r] - dlt[j]);
-                    }
+                for (int ks = 0; ks < KS; ++ks) {
+                    const int koff = swz<RB>(32 * w + l31, 2 * ks + hh);
+                    const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
+                    sp = mfma(lds_row16(Qc, off), lds_row16(Kl, koff), sp);
+                    dp = mfma(lds_row16(Oc, off), lds_row16(Vl, koff), dp);
                 }
-#pragma unroll
-            for (int qt = 0; qt < 2; ++qt)
+                // P = exp2(S * scale*log2e - LSE2), dS = P * (dP - delta); diagonal / ragged tiles (wave-uniform
+                // test, scalar branch) zero P where (unsigned)(q - klim) >= span
+                if (need_mask)
+                    softmax_ds<true>(sp, dp, lc + qt * 32, dc + qt * 32, hh, scale_log2, m0 + qt * 32 - klim, span);
+                else
+                    softmax_ds<false>(sp, dp, lc + qt * 32, dc + qt * 32, hh, scale_log2, 0, 0u);
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss) {
                     bf16x8 pb, db;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
-                        pb[j] = (__bf16)sp[qt][8 * ss + j];
-                        db[j] = (__bf16)dp[qt][8 * ss + j];
+                        pb[j] = (__bf16)sp[8 * ss + j];
+                        db[j] = (__bf16)dp[8 * ss + j];
                     }
                     const int qr = qt * 32 + 16 * ss;
 #pragma unroll
@@ -265,16 +277,16 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                         dv[dt] = mfma(lds_tr_pair(Oc, o0, o1), pb, dv[dt]);
                         dk[dt] = mfma(lds_tr_pair(Qc, o0, o1), db, dk[dt]);
                     }
-                }
-            // dS^T -> LDS [key row][q]: registers 4i..4i+3 are 4 consecutive queries
+                    // dS^T -> LDS [key row][q] from the same bf16 values: elements 4g..4g+3 of db are
+                    // registers 8ss+4g.. = 4 consecutive queries of group i = 2ss+g
+                    const u16x8 du = __builtin_bit_cast(u16x8, db);
 #pragma unroll
-            for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    u16x4 t = {f2bf(dp[qt][4 * i]), f2bf(dp[qt][4 * i + 1]), f2bf(dp[qt][4 * i + 2]),
-                               f2bf(dp[qt][4 * i + 3])};
-                    *reinterpret_cast<u16x4*>(dST + swz<128>(32 * w + l31, qt * 4 + i) + 8 * hh) = t;
+                    for (int g = 0; g < 2; ++g) {
+                        const u16x4 t = {du[4 * g], du[4 * g + 1], du[4 * g + 2], du[4 * g + 3]};
+                        *reinterpret_cast<u16x4*>(dST + swz<128>(32 * w + l31, qt * 4 + 2 * ss + g) + 8 * hh) = t;
+                    }
                 }
+            }
         } else {
 #pragma unroll
             for (int c = 0; c < 4; ++c)
@@ -337,7 +349,8 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
         }
         if (it + 1 < total_it) write_tile(it + 1, cur ^ 1);
         __syncthreads();
-    }
+    };
+    for (int it = 0; it < total_it; ++it) body(it);
 
     // ---- GQA: fp32 partials of this query head -> [b, s, h, {dK, dV}, D] for the reduce kernel
     if (G > 1) {
