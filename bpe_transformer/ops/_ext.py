@@ -15,7 +15,8 @@ from pathlib import Path
 
 import torch
 
-LIB_PATH = Path(__file__).resolve().parent / "_bpe_hip.so"
+_VARIANT = os.environ.get("BPE_HIP_VARIANT") or None  # A/B builds: _bpe_hip_<variant>.so (ops/build.py)
+LIB_PATH = Path(__file__).resolve().parent / ("_bpe_hip.so" if not _VARIANT else f"_bpe_hip_{_VARIANT}.so")
 _lock = threading.Lock()
 _loaded = False
 
@@ -36,7 +37,7 @@ def load() -> None:
         if _loaded:
             return
         if not LIB_PATH.exists():
-            if os.environ.get("BPE_AUTOBUILD", "0") == "1":
+            if os.environ.get("BPE_AUTOBUILD", "0") == "1" and not _VARIANT:
                 from .build import build
 
                 build()

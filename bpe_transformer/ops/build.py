@@ -57,21 +57,31 @@ def _run(cmd: list[str], verbose: bool) -> None:
         sys.stderr.write(r.stderr)
 
 
-def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
+def lib_path(variant: str | None = None) -> Path:
+    return LIB if not variant else HERE / f"_bpe_hip_{variant}.so"
+
+
+def build(verbose: bool = False, jobs: int | None = None, force: bool = False, variant: str | None = None,
+          defines: list[str] | None = None) -> Path:
+    """Build the library; ``variant`` + ``defines`` build an A/B copy (``_bpe_hip_<variant>.so``, own object
+    directory) compiled with extra ``-D`` flags, selected at run time with ``BPE_HIP_VARIANT=<variant>``."""
+    build_dir = BUILD if not variant else BUILD.parent / f"hip_{variant}"
+    lib = lib_path(variant)
+    build_dir.mkdir(parents=True, exist_ok=True)
     headers = sorted(CSRC.glob("*.h"))
     hip_srcs = sorted(CSRC.glob("*.hip"))
     inc, libdirs, abi = _torch_paths()
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", str(CSRC)]
+    common += [f"-D{d}" for d in (defines or [])]
     jobs_list = []
     objs = []
     for src in hip_srcs:
-        obj = BUILD / (src.stem + ".o")
+        obj = build_dir / (src.stem + ".o")
         objs.append(obj)
         if force or _needs_build(obj, src, headers):
             jobs_list.append([HIPCC, *common, "-c", str(src), "-o", str(obj)])
     bind_src = CSRC / "torch_bindings.cpp"
-    bind_obj = BUILD / "torch_bindings.o"
+    bind_obj = build_dir / "torch_bindings.o"
     objs.append(bind_obj)
     if force or _needs_build(bind_obj, bind_src, headers):
         cmd = [HIPCC, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
@@ -84,13 +94,13 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         n = jobs or min(8, os.cpu_count() or 4)
         with cf.ThreadPoolExecutor(n) as ex:
             list(ex.map(lambda c: _run(c, verbose), jobs_list))
-    if force or jobs_list or not LIB.exists():
-        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(LIB), *map(str, objs)]
+    if force or jobs_list or not lib.exists():
+        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(lib), *map(str, objs)]
         for d in libdirs:
             link += ["-L", d, f"-Wl,-rpath,{d}"]
         link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip"]
         _run(link, verbose)
-    return LIB
+    return lib
 
 
 def main() -> None:
@@ -98,8 +108,10 @@ def main() -> None:
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("-f", "--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--variant", default=None, help="build an A/B copy _bpe_hip_<variant>.so")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra preprocessor define")
     a = ap.parse_args()
-    print(build(verbose=a.verbose, jobs=a.jobs, force=a.force))
+    print(build(verbose=a.verbose, jobs=a.jobs, force=a.force, variant=a.variant, defines=a.defines))
 
 
 if __name__ == "__main__":

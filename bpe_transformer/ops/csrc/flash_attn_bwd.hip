@@ -16,12 +16,10 @@
 //                                        accumulators; A = dO^T / Q^T via
 //                                        ds_read_b64_tr_b16 of the same images)
 //   dS^T -> LDS (8-byte writes), then dQ = dS.K for the workgroup's keys:
-//   2 x (D/32) output tiles of 32x32 spread over the waves; when there are
-//   more waves than tiles the key range is split and the partial tiles are
-//   summed through LDS first.  The dQ tile is then added to an fp32 buffer with
-//   float atomics shaped as two 128-byte row segments per wave instruction
-//   (guide G12).  256-key workgroups halve the atomic bytes of a 128-key
-//   design; at ~1.3 TB/s chip-wide those bytes set this kernel's floor.
+//   16x16x32 MFMA blocks, 2 (D = 64) per wave over all the workgroup's keys
+//   (no key split, no partial-sum exchange), added to an fp32 buffer with
+//   float atomics (guide G12).  256-key workgroups halve the atomic bytes of a
+//   128-key design.
 // RoPE: Q tiles are rotated while staged, K once at the start; dK is
 // un-rotated in the epilogue and dQ in the convert kernel.  GQA: one
 // workgroup per query head; the G partial dK / dV of a kv head are summed in
@@ -41,14 +39,18 @@ template <int D> struct BwdCfg {
     static constexpr int RB = D * 2;
     static constexpr int QT = 64 * RB;                                  // bytes per 64-query tile
     static constexpr int DT = D / 32;
-    static constexpr int OUT_TILES = 2 * DT;                            // 32x32 dQ tiles per query tile
-    static constexpr int KSPLIT = NW > OUT_TILES ? NW / OUT_TILES : 1;  // key-range split of the dQ product
-    static constexpr int TPW = OUT_TILES > NW ? OUT_TILES / NW : 1;     // dQ tiles per wave
     static constexpr size_t LDS_Q = 2 * QT, LDS_DO = 2 * QT;
     static constexpr size_t LDS_K = (size_t)KB * RB;  // K (roped) and V of the workgroup's keys, each
     static constexpr size_t LDS_DST = (size_t)KB * 128;
-    static constexpr size_t LDS_X = KSPLIT > 1 ? (size_t)(KSPLIT - 1) * OUT_TILES * 16 * 64 * 4 : 0;
     static constexpr size_t LDS_STATS = 4 * 64 * 4;
+#ifdef BPE_FA_DQ32
+    static constexpr int OUT_TILES = 2 * DT;
+    static constexpr int KSPLIT = NW > OUT_TILES ? NW / OUT_TILES : 1;
+    static constexpr int TPW = OUT_TILES > NW ? OUT_TILES / NW : 1;
+    static constexpr size_t LDS_X = KSPLIT > 1 ? (size_t)(KSPLIT - 1) * OUT_TILES * 16 * 64 * 4 : 0;
+#else
+    static constexpr size_t LDS_X = 0;
+#endif
     static constexpr size_t LDS = LDS_Q + LDS_DO + 2 * LDS_K + LDS_DST + LDS_X + LDS_STATS;
 };
 
@@ -82,33 +84,29 @@ __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const __bf16* __restric
 }
 
 // P and dS of one 32-query half from its S / dP accumulators (key on the lane, 4 consecutive queries per
-// register group), two elements per packed instruction.  MASK: zero P where (unsigned)(q - klim) >= span,
-// with q = half start + row, passed as qoff = half start - klim.
+// register group), two elements per packed instruction.  The accumulators STARTED at the row constants
+// (guide: "row constants as the initial accumulator"): S' = S - LSE2 / (scale*log2e), dP' = dP - delta, so
+// P = exp2(scale*log2e * S') and dS = P * dP'.  MASK: zero P where (unsigned)(q - klim) >= span, with
+// q = half start + row, passed as qoff = half start - klim.
 template <bool MASK>
-__device__ __forceinline__ void softmax_ds(f32x16& sp, f32x16& dp, const float* lc, const float* dc, int hh,
-                                           float scale_log2, int qoff, unsigned span) {
+__device__ __forceinline__ void softmax_ds(f32x16& sp, f32x16& dp, int hh, float scale_log2, int qoff,
+                                           unsigned span) {
     typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 sc = {scale_log2, scale_log2};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int qi = 8 * i + 4 * hh;  // rows qi..qi+3
-        const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
-        const f32x4 dl = *reinterpret_cast<const f32x4*>(dc + qi);
-#pragma unroll
-        for (int j = 0; j < 4; j += 2) {
-            const int r = 4 * i + j;
-            const f2 sc = {scale_log2, scale_log2};
-            const f2 x = f2{sp[r], sp[r + 1]} * sc - f2{lv[j], lv[j + 1]};
-            f2 p = {fast_exp2(x[0]), fast_exp2(x[1])};
-            if constexpr (MASK) {
-                p[0] = ((unsigned)(qoff + qi + j) < span) ? p[0] : 0.f;
-                p[1] = ((unsigned)(qoff + qi + j + 1) < span) ? p[1] : 0.f;
-            }
-            const f2 d = p * (f2{dp[r], dp[r + 1]} - f2{dl[j], dl[j + 1]});
-            sp[r] = p[0];
-            sp[r + 1] = p[1];
-            dp[r] = d[0];
-            dp[r + 1] = d[1];
+    for (int r = 0; r < 16; r += 2) {
+        const f2 x = f2{sp[r], sp[r + 1]} * sc;
+        f2 p = {fast_exp2(x[0]), fast_exp2(x[1])};
+        if constexpr (MASK) {
+            const int q = qoff + acc_row(r, hh);
+            p[0] = ((unsigned)q < span) ? p[0] : 0.f;
+            p[1] = ((unsigned)(q + 1) < span) ? p[1] : 0.f;
         }
+        const f2 d = p * f2{dp[r], dp[r + 1]};
+        sp[r] = p[0];
+        sp[r + 1] = p[1];
+        dp[r] = d[0];
+        dp[r + 1] = d[1];
     }
 }
 
@@ -130,7 +128,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     char* Kl = dOs + C::LDS_DO;                       // [KB][D]  roped K of this workgroup's keys
     char* Vl = Kl + C::LDS_K;                         // [KB][D]  V of this workgroup's keys
     char* dST = Vl + C::LDS_K;                        // [KB keys][64 q] bf16
-    float* xch = reinterpret_cast<float*>(dST + C::LDS_DST);              // dQ partial exchange
+    [[maybe_unused]] float* xch = reinterpret_cast<float*>(dST + C::LDS_DST);  // (BPE_FA_DQ32 only)
     float* lseS = reinterpret_cast<float*>(dST + C::LDS_DST + C::LDS_X);  // [2][64]
     float* dltS = lseS + 128;                                              // [2][64]
 
@@ -215,8 +213,9 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
             *reinterpret_cast<u16x8*>(dOs + buf * QT + swz<RB>(row, c)) = oreg[i];
         }
         if (tid < 64) {
-            lseS[buf * 64 + tid] = lreg;
-            dltS[buf * 64 + tid] = dreg;
+            // the S / dP accumulators' starting values: -LSE2 / (scale*log2e) and -delta
+            lseS[buf * 64 + tid] = (lreg == INFINITY) ? -INFINITY : -lreg / scale_log2;
+            dltS[buf * 64 + tid] = -dreg;
         }
     };
 
@@ -247,7 +246,13 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
             for (int qt = 0; qt < 2; ++qt) {
                 f32x16 sp, dp;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) { sp[r] = 0.f; dp[r] = 0.f; }
+                for (int i = 0; i < 4; ++i) {
+                    const int qi = qt * 32 + 8 * i + 4 * hh;  // rows qi..qi+3 of registers 4i..4i+3
+                    const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
+                    const f32x4 dl = *reinterpret_cast<const f32x4*>(dc + qi);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) { sp[4 * i + j] = lv[j]; dp[4 * i + j] = dl[j]; }
+                }
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks) {
                     const int koff = swz<RB>(32 * w + l31, 2 * ks + hh);
@@ -258,9 +263,9 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                 // P = exp2(S * scale*log2e - LSE2), dS = P * (dP - delta); diagonal / ragged tiles (wave-uniform
                 // test, scalar branch) zero P where (unsigned)(q - klim) >= span
                 if (need_mask)
-                    softmax_ds<true>(sp, dp, lc + qt * 32, dc + qt * 32, hh, scale_log2, m0 + qt * 32 - klim, span);
+                    softmax_ds<true>(sp, dp, hh, scale_log2, m0 + qt * 32 - klim, span);
                 else
-                    softmax_ds<false>(sp, dp, lc + qt * 32, dc + qt * 32, hh, scale_log2, 0, 0u);
+                    softmax_ds<false>(sp, dp, hh, scale_log2, 0, 0u);
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss) {
                     bf16x8 pb, db;
@@ -293,6 +298,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                 *reinterpret_cast<u16x8*>(dST + swz<128>(32 * w + l31, 2 * c + hh)) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
         __syncthreads();
+#ifdef BPE_FA_DQ32  // A/B: 32x32 tiles with a key split and an LDS partial-sum exchange
         // ---- dQ = dS.K over this workgroup's keys
         {
             constexpr int KPART = C::KB / C::KSPLIT;  // keys per part
@@ -347,6 +353,41 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                 }
             }
         }
+#else
+        // ---- dQ = dS.K over this workgroup's keys with 16x16x32 MFMA: the 64 x D tile is 4 x D/16 blocks
+        //      of 16 x 16, TPW per wave over ALL keys (no key split, no partial-sum exchange); the TPW blocks
+        //      of a wave share their query block, so the dS^T fragments are read once per 32-key step.
+        //      dQacc rows are padded to a multiple of 64 per batch: rows q >= S of the last tile land in
+        //      padding (carrying zeros: P = 0 there), so the atomics need no per-element guard.
+        {
+            constexpr int DB = D / 16, TPW = 4 * DB / NW;
+            const int t0 = w * TPW, qb = t0 / DB;
+            f32x4 acc[TPW];
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int lr = 8 * (l >> 4) + ((l & 15) >> 2), lc4 = 4 * (l & 3);
+#pragma unroll
+            for (int ks = 0; ks < C::KB / 32; ++ks) {
+                const int kr = 32 * ks + lr;
+                const bf16x8 a = lds_tr_pair(dST, tr_off<128>(kr, qb * 16 + lc4), tr_off<128>(kr + 4, qb * 16 + lc4));
+#pragma unroll
+                for (int u = 0; u < TPW; ++u) {
+                    const int dc2 = ((t0 + u) % DB) * 16 + lc4;
+                    const bf16x8 bb = lds_tr_pair(Kl, tr_off<RB>(kr, dc2), tr_off<RB>(kr + 4, dc2));
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[u], 0, 0, 0);
+                }
+            }
+            if (!(flags & 1)) {
+                const long HD = (long)H * D;
+                const int Spad = (S + 63) & ~63;
+                float* dqp = dQacc + ((long)b * Spad + m0 + qb * 16 + 4 * (l >> 4)) * HD + (long)h * D + (l & 15);
+#pragma unroll
+                for (int u = 0; u < TPW; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) atomicAdd(dqp + r * HD + ((t0 + u) % DB) * 16, acc[u][r]);
+            }
+        }
+#endif
         if (it + 1 < total_it) write_tile(it + 1, cur ^ 1);
         __syncthreads();
     };
@@ -488,20 +529,22 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
     }
     const size_t spad = (size_t)((a.S + 63) & ~63);
     (void)hipMemsetAsync(a.dq_acc, 0, (size_t)a.B * spad * a.H * D * sizeof(float), s);
-    const int nkb = (a.S + Cfg::KB - 1) / Cfg::KB;
-    static bool lds_attr = false;  // > 64 KiB of dynamic LDS: opt in once (before any graph capture)
-    if (!lds_attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fa_bwd_kernel<D, C, R>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
-        lds_attr = true;
-    }
     static const int dbg = [] {
         const char* e = getenv("BPE_FA_DEBUG");  // bit 0: skip the dQ atomics (timing diagnostics only)
         return e ? atoi(e) : 0;
     }();
-    fa_bwd_kernel<D, C, R><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
-        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv, a.dkv_part,
-        a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, dbg);
+    {
+        const int nkb = (a.S + Cfg::KB - 1) / Cfg::KB;
+        static bool lds_attr = false;  // > 64 KiB of dynamic LDS: opt in once (before any graph capture)
+        if (!lds_attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fa_bwd_kernel<D, C, R>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+            lds_attr = true;
+        }
+        fa_bwd_kernel<D, C, R><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
+            a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv,
+            a.dkv_part, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, dbg);
+    }
     if (a.Hkv < a.H) {
         const long tkv = (long)a.B * a.S * a.Hkv * (D / 4);
         const int g2 = (int)std::min<long>((tkv + 255) / 256, 4096);
