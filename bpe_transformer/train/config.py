@@ -57,6 +57,7 @@ class TrainConfig:
     resume: str | None = None  # path or "latest"
     metrics_path: str | None = None  # JSONL
     profile: bool = False
+    phase_timing: bool = False  # log fwd / bwd / exposed-comm / optimizer ms (device events) at each log step
     nan_guard: bool = True
 
     def to_dict(self) -> dict:

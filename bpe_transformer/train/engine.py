@@ -33,6 +33,7 @@ class TrainEngine:
         weight_decay: float = 0.1,
         max_grad_norm: float | None = 1.0,
         bucket_mb: float = 64.0,
+        time_phases: bool = False,
     ):
         self.model = model
         self.dist = dist_info or DistInfo()
@@ -46,6 +47,30 @@ class TrainEngine:
             self.ddp.broadcast_parameters(0)
             self.opt.master.copy_(self.flat.data)  # keep fp32 master == broadcast weights
         self.last_grad_norm: Tensor | None = None
+        # phase timing (SURVEY §5 tracing): device events around forward / backward / exposed all-reduce wait /
+        # clip + optimizer, recorded every step and only read (one host sync) when phase_times() is called
+        self.time_phases = time_phases and torch.cuda.is_available() and self.flat.data.is_cuda
+        self._ev: dict[str, list] = {}
+
+    def _mark(self, name: str) -> None:
+        if self.time_phases:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self._ev.setdefault(name, []).append(e)
+
+    def phase_times(self) -> dict[str, float]:
+        """Mean milliseconds per step of each phase since the last call (synchronises the device)."""
+        if not self.time_phases or "start" not in self._ev:
+            return {}
+        torch.cuda.synchronize()
+        order = ["start", "fwd", "bwd", "comm", "opt"]
+        out: dict[str, float] = {}
+        n = len(self._ev["start"])
+        for a, b in zip(order, order[1:]):
+            if a in self._ev and b in self._ev and len(self._ev[b]) == n:
+                out[f"{b}_ms"] = sum(x.elapsed_time(y) for x, y in zip(self._ev[a], self._ev[b])) / n
+        self._ev.clear()
+        return out
 
     def train_step(self, batches: list[tuple[Tensor, Tensor]], lr: float | None = None) -> Tensor:
         """Run one optimizer step over ``batches`` (gradient accumulation when > 1).
@@ -53,6 +78,7 @@ class TrainEngine:
         Returns the mean loss as a 0-dim device tensor (no host sync).
         """
         self.model.train()
+        self._mark("start")
         self.flat.grad.zero_()
         n = len(batches)
         total = None
@@ -63,15 +89,20 @@ class TrainEngine:
             ctx = self.ddp.no_sync() if (self.ddp is not None and not last) else nullcontext()
             with ctx:
                 loss = self.model.loss(x, y)
+                if last:
+                    self._mark("fwd")
                 (loss / n if n > 1 else loss).backward()
             total = loss.detach() if total is None else total + loss.detach()
+        self._mark("bwd")
         if self.ddp is not None:
             self.ddp.finish()
+        self._mark("comm")
         coef = None
         if self.max_grad_norm is not None and self.max_grad_norm > 0:
             norm, coef = self.opt.clip_grad_norm(self.max_grad_norm)
             self.last_grad_norm = norm
         self.opt.step(lr, coef)
+        self._mark("opt")
         fp8 = getattr(self.model, "fp8_state", None)
         if fp8 is not None:
             if self.ddp is not None:

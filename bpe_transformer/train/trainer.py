@@ -64,7 +64,7 @@ class Trainer:
         o = cfg.optim
         self.engine = TrainEngine(self.model, self.info, lr=o.lr, betas=o.betas, eps=o.eps,
                                   weight_decay=o.weight_decay, max_grad_norm=o.max_grad_norm,
-                                  bucket_mb=cfg.bucket_mb)
+                                  bucket_mb=cfg.bucket_mb, time_phases=cfg.phase_timing)
         self.schedule = CosineSchedule(o.lr, o.min_lr, o.warmup_iters, o.cosine_cycle_iters or cfg.max_iters)
         ctx = cfg.model.context_length
         if cfg.data.train_path:
@@ -72,6 +72,7 @@ class Trainer:
         else:
             train = synthetic_tokens(cfg.model.vocab_size, cfg.data.synthetic_tokens, seed=cfg.seed)
         self.val = load_tokens(cfg.data.val_path, cfg.data.vocab_size_for_dtype) if cfg.data.val_path else None
+        self.train_data = train
         self.loader = BatchLoader(train, cfg.batch_size, ctx, dev, seed=cfg.seed + 1000 * self.info.rank)
         self.metrics = MetricsLogger(cfg.metrics_path, self.info.rank)
         self.start_iter = 0
@@ -85,7 +86,8 @@ class Trainer:
         return Path(self.cfg.ckpt_dir) / f"ckpt_{it:08d}.pt"
 
     def save(self, it: int) -> None:
-        extra = {}
+        extra = {"rng": {"torch": torch.get_rng_state(),
+                         "cuda": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else []}}
         if self.model.fp8_state is not None:
             extra["fp8"] = self.model.fp8_state.state_dict()
         save_checkpoint(self.model, _EngineOptimizerView(self.engine), it, self._ckpt_path(it), rank=self.info.rank,
@@ -102,7 +104,17 @@ class Trainer:
         self.engine.load_state_dict(obj["optimizer"])
         if self.model.fp8_state is not None and "fp8" in obj:
             self.model.fp8_state.load_state_dict(obj["fp8"])
+        rng = obj.get("rng")
+        if rng is not None:
+            torch.set_rng_state(rng["torch"].cpu())
+            if torch.cuda.is_available() and len(rng["cuda"]) == torch.cuda.device_count():
+                torch.cuda.set_rng_state_all([t.cpu() for t in rng["cuda"]])
         self.start_iter = int(obj["iteration"])
+        # the prefetching loader runs ahead of the step counter, so its generator state is not checkpointed;
+        # a resumed run draws a fresh, deterministic stream keyed by (seed, rank, resume iteration)
+        self.loader.close()
+        self.loader = BatchLoader(self.train_data, self.cfg.batch_size, self.cfg.model.context_length, self.info.device,
+                                  seed=self.cfg.seed + 1000 * self.info.rank + 7919 * self.start_iter)
         log.info(f"resumed from {path} at iteration {self.start_iter}")
 
     # ------------------------------------------------------------------ eval
@@ -156,7 +168,7 @@ class Trainer:
                     self.metrics.log(step=step, loss=loss_v, lr=lr, grad_norm=gn_v, ms_per_step=1000 * dt,
                                      tokens_per_s=tps,
                                      mfu=tps * flops_tok / (MI355X_BF16_DENSE_FLOPS * self.info.world_size),
-                                     mem_gb=device_memory_gb())
+                                     mem_gb=device_memory_gb(), **self.engine.phase_times())
                     if cfg.nan_guard and not math.isfinite(loss_v):
                         bad += 1
                         log.warning(f"non-finite loss at step {step} ({bad} consecutive)")

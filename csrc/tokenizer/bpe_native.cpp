@@ -20,9 +20,11 @@
 //   * encoding (reference: bpe_tokenizer.py:139-290, O(n^2) per pre-token):
 //     rank-ordered merges with a linked list + min-heap (O(n log n)), a
 //     pre-token cache, and a threaded batch/file encoder.
+#ifndef BPE_NATIVE_NO_PYTHON  // the core below is plain C++; tools/native_selftest builds it without Python
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#endif
 
 #include <algorithm>
 #include <atomic>
@@ -42,7 +44,9 @@
 
 #include "unicode_tables.h"
 
+#ifndef BPE_NATIVE_NO_PYTHON
 namespace py = pybind11;
+#endif
 
 namespace bpe_tok {
 
@@ -635,6 +639,7 @@ struct Encoder {
 }  // namespace bpe_tok
 
 // ------------------------------------------------------------------ bindings
+#ifndef BPE_NATIVE_NO_PYTHON
 using namespace bpe_tok;
 
 static std::string to_str(const py::bytes& b) { return std::string(b); }
@@ -789,3 +794,4 @@ PYBIND11_MODULE(_bpe_native, m) {
         .def("cache_size", [](const Encoder& e) { return e.cache.size(); })
         .def("clear_cache", [](Encoder& e) { e.cache.clear(); });
 }
+#endif  // BPE_NATIVE_NO_PYTHON

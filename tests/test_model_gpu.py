@@ -119,3 +119,28 @@ def test_fp8_engine_reduces_loss(gpu_device):
         last = eng.train_step([(x, y)]).item()
     assert last < first - 1.0, (first, last)
     assert model.fp8_state.pos == 31
+
+
+def test_forward_is_bitwise_deterministic(gpu_device):
+    """Every forward kernel (attention, norms, CE, GEMM routing) is run-to-run deterministic; only the attention
+    dQ accumulation (fp32 atomics) makes gradients non-bitwise-reproducible."""
+    _, gpu = _pair(gpu_device)
+    ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    with torch.no_grad():
+        a = gpu.loss(ids, tgt)
+        b = gpu.loss(ids, tgt)
+    assert torch.equal(a, b)
+
+
+def test_engine_phase_timing(gpu_device):
+    from bpe_transformer.train.engine import TrainEngine
+
+    torch.manual_seed(0)
+    model = TransformerLM(1000, 128, 256, 2, 4, 512, device=gpu_device, dtype=torch.bfloat16)
+    eng = TrainEngine(model, time_phases=True)
+    x = torch.randint(0, 1000, (4, 128), device=gpu_device)
+    for _ in range(3):
+        eng.train_step([(x, torch.roll(x, -1, 1))])
+    ph = eng.phase_times()
+    assert set(ph) == {"fwd_ms", "bwd_ms", "comm_ms", "opt_ms"} and all(v >= 0 for v in ph.values())

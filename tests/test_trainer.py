@@ -88,3 +88,39 @@ def test_config_overrides_and_cli(tmp_path, capsys):
     rc = cli_main(["--preset", "ts-tests", "device=cpu", "max_iters=2", "batch_size=2", "log_every=1",
                    "model.vocab_size=128", f"ckpt_dir={tmp_path}", "data.synthetic_tokens=5000"])
     assert rc == 0
+
+
+def test_training_is_deterministic_on_cpu():
+    """two runs from the same seed give bitwise-identical losses and weights (fp32, CPU)."""
+    import torch
+
+    from bpe_transformer.models import TransformerLM
+    from bpe_transformer.train.engine import TrainEngine
+
+    def run():
+        torch.manual_seed(0)
+        m = TransformerLM(300, 32, 32, 2, 2, 64)
+        eng = TrainEngine(m, lr=1e-2, weight_decay=0.1, max_grad_norm=1.0)
+        g = torch.Generator().manual_seed(5)
+        losses = []
+        for _ in range(4):
+            x = torch.randint(0, 300, (2, 32), generator=g)
+            losses.append(eng.train_step([(x, torch.roll(x, -1, 1))]).item())
+        return losses, eng.flat.data.clone()
+
+    (l1, w1), (l2, w2) = run(), run()
+    assert l1 == l2
+    assert torch.equal(w1, w2)
+
+
+def test_phase_timing_is_a_noop_on_cpu():
+    import torch
+
+    from bpe_transformer.models import TransformerLM
+    from bpe_transformer.train.engine import TrainEngine
+
+    m = TransformerLM(100, 16, 32, 1, 2, 64)
+    eng = TrainEngine(m, time_phases=True)
+    x = torch.randint(0, 100, (2, 16))
+    eng.train_step([(x, x)])
+    assert eng.phase_times() == {}
