@@ -69,6 +69,8 @@ def main() -> int:
                          "shipped table for this model/batch if present, 'off' = library heuristics")
     ap.add_argument("--precision", choices=["bf16", "fp8"], default="bf16",
                     help="fp8 = block projections' forward GEMMs in e4m3fn with delayed scaling (bf16 backward)")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu = the plumbing config path (fp32, no HIP kernels), e.g. --model tinystories-17m --seq 256")
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args()
 
@@ -77,14 +79,17 @@ def main() -> int:
     from bpe_transformer.parallel import all_reduce_max, barrier, cleanup, init_distributed
     from bpe_transformer.train.engine import TrainEngine
 
-    info = init_distributed("cuda")
+    info = init_distributed(args.device)
+    on_gpu = info.device.type == "cuda"
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     tuning = load_gemm_tuning(args.gemm_tuning, args.model, args.batch, args.seq)
     if args.gpus != info.world_size:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
     dev = info.device
     torch.manual_seed(1234)  # identical init on every rank (rank-0 broadcast also enforces it)
     cfg = get_preset(args.model, context_length=args.seq)
-    model = TransformerLM.from_config(cfg, device=dev, dtype=torch.bfloat16)
+    dtype = torch.bfloat16 if on_gpu else torch.float32
+    model = TransformerLM.from_config(cfg, device=dev, dtype=dtype)
     if args.precision == "fp8":
         model.enable_fp8()
     engine = TrainEngine(model, info, lr=3e-4, weight_decay=0.1, max_grad_norm=1.0, bucket_mb=args.bucket_mb)
@@ -101,16 +106,16 @@ def main() -> int:
 
     for i in range(args.warmup):
         engine.train_step(batch(i))
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     loss = None
     for i in range(args.steps):
         loss = engine.train_step(batch(args.warmup + i))
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     dt = all_reduce_max(dt, dev)
     loss_v = float(loss.item()) if loss is not None else float("nan")
@@ -130,7 +135,7 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if args.precision == "bf16" else "fp8(e4m3 fwd GEMMs)+bf16",
+        "dtype": ("bf16" if args.precision == "bf16" else "fp8(e4m3 fwd GEMMs)+bf16") if on_gpu else "fp32",
         "data": "synthetic (uniform random tokens, random-init weights)",
         "config": {
             "model": f"{args.model} ({cfg.num_layers}L/{cfg.d_model}d/{cfg.num_heads}H, RoPE+SwiGLU+RMSNorm, "

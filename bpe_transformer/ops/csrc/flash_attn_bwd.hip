@@ -34,24 +34,22 @@ namespace bpe {
 namespace fa {
 
 template <int D> struct BwdCfg {
-    static constexpr int NW = (D == 64) ? 8 : 4;                        // waves per workgroup
+#ifdef BPE_FA_BWD_2WG
+    // two independent 4-wave workgroups per CU (their phases drift apart, so one's softmax VALU overlaps the
+    // other's MFMAs), single-buffered Q / dO tiles (written after the dS barrier, when no wave reads them)
+    static constexpr int NW = 4, QBUF = (D == 64) ? 1 : 2, WGS = (D == 64) ? 2 : 1;
+#else
+    static constexpr int NW = (D == 64) ? 8 : 4, QBUF = 2, WGS = 1;  // waves per workgroup
+#endif
     static constexpr int KB = 32 * NW;                                  // keys per workgroup
     static constexpr int RB = D * 2;
     static constexpr int QT = 64 * RB;                                  // bytes per 64-query tile
     static constexpr int DT = D / 32;
-    static constexpr size_t LDS_Q = 2 * QT, LDS_DO = 2 * QT;
+    static constexpr size_t LDS_Q = QBUF * QT, LDS_DO = QBUF * QT;
     static constexpr size_t LDS_K = (size_t)KB * RB;  // K (roped) and V of the workgroup's keys, each
     static constexpr size_t LDS_DST = (size_t)KB * 128;
     static constexpr size_t LDS_STATS = 4 * 64 * 4;
-#ifdef BPE_FA_DQ32
-    static constexpr int OUT_TILES = 2 * DT;
-    static constexpr int KSPLIT = NW > OUT_TILES ? NW / OUT_TILES : 1;
-    static constexpr int TPW = OUT_TILES > NW ? OUT_TILES / NW : 1;
-    static constexpr size_t LDS_X = KSPLIT > 1 ? (size_t)(KSPLIT - 1) * OUT_TILES * 16 * 64 * 4 : 0;
-#else
-    static constexpr size_t LDS_X = 0;
-#endif
-    static constexpr size_t LDS = LDS_Q + LDS_DO + 2 * LDS_K + LDS_DST + LDS_X + LDS_STATS;
+    static constexpr size_t LDS = LDS_Q + LDS_DO + 2 * LDS_K + LDS_DST + LDS_STATS;
 };
 
 // delta = rowsum(dO * O) per (b, h, s)
@@ -111,7 +109,7 @@ __device__ __forceinline__ void softmax_ds(f32x16& sp, f32x16& dp, int hh, float
 }
 
 template <int D, bool CAUSAL, bool ROPE>
-__global__ void __launch_bounds__(BwdCfg<D>::NW * 64, 1)
+__global__ void __launch_bounds__(BwdCfg<D>::NW * 64, BwdCfg<D>::WGS)
 fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv, long ld_q,
               long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
               const float* __restrict__ DELTA, float* __restrict__ dQacc, __bf16* __restrict__ dK,
@@ -128,8 +126,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     char* Kl = dOs + C::LDS_DO;                       // [KB][D]  roped K of this workgroup's keys
     char* Vl = Kl + C::LDS_K;                         // [KB][D]  V of this workgroup's keys
     char* dST = Vl + C::LDS_K;                        // [KB keys][64 q] bf16
-    [[maybe_unused]] float* xch = reinterpret_cast<float*>(dST + C::LDS_DST);  // (BPE_FA_DQ32 only)
-    float* lseS = reinterpret_cast<float*>(dST + C::LDS_DST + C::LDS_X);  // [2][64]
+    float* lseS = reinterpret_cast<float*>(dST + C::LDS_DST);  // [2][64]
     float* dltS = lseS + 128;                                              // [2][64]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
@@ -229,7 +226,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     // one query tile.  (Unrolling by two so the buffer index becomes an immediate offset was measured:
     // the hoisted per-buffer addresses push the kernel past 256 VGPRs and it spills.)
     auto body = [&](int it) {
-        const int cur = it & 1;
+        const int cur = C::QBUF == 2 ? (it & 1) : 0;
         const int m0 = m_start + it * 64;
         if (it + 1 < total_it) load_tile(it + 1);
         char* Qc = Qs + cur * QT;
@@ -298,62 +295,6 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                 *reinterpret_cast<u16x8*>(dST + swz<128>(32 * w + l31, 2 * c + hh)) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
         __syncthreads();
-#ifdef BPE_FA_DQ32  // A/B: 32x32 tiles with a key split and an LDS partial-sum exchange
-        // ---- dQ = dS.K over this workgroup's keys
-        {
-            constexpr int KPART = C::KB / C::KSPLIT;  // keys per part
-            const int part = w / C::OUT_TILES;        // 0 when KSPLIT == 1
-            const int krow0 = part * KPART;
-            f32x16 acc[C::TPW];
-#pragma unroll
-            for (int tt = 0; tt < C::TPW; ++tt) {
-                const int tile = (C::TPW == 1) ? (w % C::OUT_TILES) : (w * C::TPW + tt);
-                const int qt2 = tile / DT, dt2 = tile % DT;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[tt][r] = 0.f;
-#pragma unroll
-                for (int ks = 0; ks < KPART / 16; ++ks) {
-                    const int kr = krow0 + 16 * ks + 8 * hh + ((l & 15) >> 2);
-                    const int qc = qt2 * 32 + tcol;
-                    const int dc2 = dt2 * 32 + tcol;
-                    const bf16x8 a = lds_tr_pair(dST, tr_off<128>(kr, qc), tr_off<128>(kr + 4, qc));
-                    const bf16x8 bb = lds_tr_pair(Kl, tr_off<RB>(kr, dc2), tr_off<RB>(kr + 4, dc2));
-                    acc[tt] = mfma(a, bb, acc[tt]);
-                }
-            }
-            if constexpr (C::KSPLIT > 1) {
-                const int tile = w % C::OUT_TILES;
-                if (part > 0) {
-                    float* dst = xch + ((size_t)(part - 1) * C::OUT_TILES + tile) * 16 * 64;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) dst[r * 64 + l] = acc[0][r];
-                }
-                __syncthreads();
-                if (part == 0) {
-#pragma unroll
-                    for (int pp = 1; pp < C::KSPLIT; ++pp) {
-                        const float* src = xch + ((size_t)(pp - 1) * C::OUT_TILES + tile) * 16 * 64;
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) acc[0][r] += src[r * 64 + l];
-                    }
-                }
-            }
-            // dQacc rows are padded to a multiple of 64 per batch (Spad): rows q >= S of the last tile land
-            // in padding (and carry zeros: P = 0 there), so the atomics need no per-element guard
-            if (part == 0 && !(flags & 1)) {
-                const long HD = (long)H * D;
-                const int Spad = (S + 63) & ~63;
-#pragma unroll
-                for (int tt = 0; tt < C::TPW; ++tt) {
-                    const int tile = (C::TPW == 1) ? (w % C::OUT_TILES) : (w * C::TPW + tt);
-                    const int qt2 = tile / DT, dt2 = tile % DT;
-                    float* dqp = dQacc + ((long)b * Spad + m0 + qt2 * 32 + 4 * hh) * HD + (long)h * D + dt2 * 32 + l31;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) atomicAdd(dqp + ((r & 3) + 8 * (r >> 2)) * HD, acc[tt][r]);
-                }
-            }
-        }
-#else
         // ---- dQ = dS.K over this workgroup's keys with 16x16x32 MFMA: the 64 x D tile is 4 x D/16 blocks
         //      of 16 x 16, TPW per wave over ALL keys (no key split, no partial-sum exchange); the TPW blocks
         //      of a wave share their query block, so the dS^T fragments are read once per 32-key step.
@@ -387,8 +328,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                     for (int r = 0; r < 4; ++r) atomicAdd(dqp + r * HD + ((t0 + u) % DB) * 16, acc[u][r]);
             }
         }
-#endif
-        if (it + 1 < total_it) write_tile(it + 1, cur ^ 1);
+        if (it + 1 < total_it) write_tile(it + 1, C::QBUF == 2 ? cur ^ 1 : 0);
         __syncthreads();
     };
     for (int it = 0; it < total_it; ++it) body(it);
