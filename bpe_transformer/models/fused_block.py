@@ -69,29 +69,42 @@ class FusedBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, ln1, wq, wk, wv, wo, ln2, w1, w3, w2, cos, sin, meta):
         B, S, H, Hkv, D, eps, use_rope = meta[:7]
-        fp8 = meta[7] if len(meta) > 7 else None  # (Fp8State, first slot) or None
+        # fp8: (e4m3 Fp8State, first slot, e5m2 gradient Fp8State or None, first gradient slot) or None
+        fp8 = meta[7] if len(meta) > 7 else None
         scale = 1.0 / math.sqrt(D)
         w_qkv = _cat_weights([wq, wk, wv])
         w_13 = _cat_weights([w1, w3])
         h1, r1 = hip().rmsnorm_fwd(x2, ln1, eps)
+        w8s = None
         if fp8 is not None:
-            st, s0 = fp8  # slots s0..s0+3: activations, s0+4..s0+7: weights
-            qkv = st.matmul(h1, w_qkv, s0, s0 + 4)
+            st, s0 = fp8[0], fp8[1]  # slots s0..s0+3: activations, s0+4..s0+7: weights
+            keep = fp8[2] is not None  # fp8 input-gradient GEMMs reuse the quantised weights
+            w8s = []
+
+            def mm(x, w, i):
+                r = st.matmul(x, w, s0 + i, s0 + 4 + i, keep_w8=keep)
+                if keep:
+                    w8s.append(r[1])
+                    return r[0]
+                return r
+
+            qkv = mm(h1, w_qkv, 0)
         else:
             qkv = torch.matmul(h1, w_qkv.t())
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale)
         if fp8 is not None:
-            xm = x2 + st.matmul(o, wo.detach(), s0 + 1, s0 + 5)
+            xm = x2 + mm(o, wo.detach(), 1)
         else:
             xm = torch.addmm(x2, o, wo.t())
         h2, r2 = hip().rmsnorm_fwd(xm, ln2, eps)
-        gu = st.matmul(h2, w_13, s0 + 2, s0 + 6) if fp8 is not None else torch.matmul(h2, w_13.t())
+        gu = mm(h2, w_13, 2) if fp8 is not None else torch.matmul(h2, w_13.t())
         a = hip().swiglu_fwd(gu)
         if fp8 is not None:
-            y = xm + st.matmul(a, w2.detach(), s0 + 3, s0 + 7)
+            y = xm + mm(a, w2.detach(), 3)
         else:
             y = torch.addmm(xm, a, w2.t())
+        ctx.w8s = w8s if w8s else None
         ctx.save_for_backward(x2, r1, h1, qkv, o, lse, xm, r2, h2, gu, a, cos, sin)
         ctx.params = (ln1, wq, wk, wv, wo, ln2, w1, w3, w2)
         ctx.meta = meta
@@ -130,20 +143,31 @@ class FusedBlockFn(torch.autograd.Function):
                     grads[id(p)] = dw[off : off + n]
                     off += n
 
+        fp8 = ctx.meta[7] if len(ctx.meta) > 7 else None
+        w8s = getattr(ctx, "w8s", None)
+
+        def dx(g_out: Tensor, ws: list[Tensor], i: int) -> Tensor:
+            """Input gradient g_out @ W of projection i (0 qkv, 1 o, 2 w13, 3 w2): fp8 e5m2 x e4m3 when enabled."""
+            if w8s is not None:
+                from ..ops.fp8 import dgrad
+
+                return dgrad(fp8[2], g_out, fp8[3] + i, w8s[i], fp8[0], fp8[1] + 4 + i)
+            return torch.matmul(g_out, ws[0].detach() if len(ws) == 1 else _cat_weights(ws))
+
         # ---- FFN
         acc_weight([w2], dy, a)
-        da = torch.matmul(dy, w2.detach())
+        da = dx(dy, [w2], 3)
         dgu = hip().swiglu_bwd(da, gu)
         acc_weight([w1, w3], dgu, h2)
-        dh2 = torch.matmul(dgu, _cat_weights([w1, w3]))
+        dh2 = dx(dgu, [w1, w3], 2)
         dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dy)
         # ---- attention
         acc_weight([wo], dxm, o)
-        do = torch.matmul(dxm, wo.detach())
+        do = dx(dxm, [wo], 1)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         dqkv = hip().fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, use_rope, scale)
         acc_weight([wq, wk, wv], dqkv, h1)
-        dh1 = torch.matmul(dqkv, _cat_weights([wq, wk, wv]))
+        dh1 = dx(dqkv, [wq, wk, wv], 0)
         dx, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm)
         if main:
             ln2.main_grad.add_(dln2)

@@ -66,21 +66,28 @@ class TransformerLM(nn.Module):
         )
 
     fp8_state = None
+    fp8_grad_state = None
 
-    def enable_fp8(self, history: int = 16, margin: float = 1.0):
-        """Run the block projections' forward GEMMs in fp8 (e4m3fn, delayed scaling).
+    def enable_fp8(self, history: int = 16, margin: float = 1.0, dgrad: bool = True):
+        """Run the block projections in fp8 with delayed scaling: forward GEMMs e4m3 x e4m3, and with ``dgrad``
+        the input-gradient GEMMs e5m2 (gradient) x e4m3 (weight) as well; weight gradients stay bf16.
 
-        Only the fused GPU block path quantises (``models/fused_block.py``); every
-        block owns 8 scale slots (4 activations + 4 weights).  The training engine
-        calls ``fp8_state.update()`` once per optimizer step.
+        Only the fused GPU block path quantises (``models/fused_block.py``); every block owns 8 e4m3 scale
+        slots (4 activations + 4 weights) and 4 e5m2 slots (output gradients).  The training engine calls
+        ``update()`` on both states once per optimizer step.
         """
         from ..ops.fp8 import Fp8State
 
         dev = self.lm_head.weight.device
-        self.fp8_state = Fp8State(8 * len(self.layers), dev, history=history, margin=margin)
+        L = len(self.layers)
+        self.fp8_state = Fp8State(8 * L, dev, history=history, margin=margin)
+        self.fp8_grad_state = Fp8State(4 * L, dev, history=history, margin=margin, fmt="e5m2") if dgrad else None
         for i, layer in enumerate(self.layers):
-            layer.fp8 = (self.fp8_state, 8 * i)
+            layer.fp8 = (self.fp8_state, 8 * i, self.fp8_grad_state, 4 * i)
         return self.fp8_state
+
+    def fp8_states(self) -> list:
+        return [s for s in (self.fp8_state, self.fp8_grad_state) if s is not None]
 
     def hidden_states(self, in_indices: Tensor) -> Tensor:
         assert in_indices.shape[-1] <= self.context_length, "sequence longer than context_length"

@@ -4,7 +4,7 @@
 // path") runs the forward projections as fp8 x fp8 -> bf16 GEMMs on the
 // MFMA fp8 units through hipBLASLt, with per-tensor scales:
 //
-//   x8 = sat(x * s)            s = 448 / (max over the amax history)
+//   x8 = sat(x * s)            s = FMAX / (max over the amax history), FMAX = 448 (e4m3) / 57344 (e5m2)
 //   y  = (x8 / s_x) . (w8 / s_w)^T
 //
 // Everything that touches the scales stays on the device -- no host sync:
@@ -20,19 +20,29 @@
 
 namespace bpe {
 
-constexpr float FP8_E4M3_MAX = 448.f;
+constexpr float FP8_E4M3_MAX = 448.f;     // OCP e4m3fn: activations / weights
+constexpr float FP8_E5M2_MAX = 57344.f;   // OCP e5m2: gradients (wider range, 2 mantissa bits)
 
+// FMT 0 = e4m3fn (v_cvt_pk_fp8_f32), 1 = e5m2 (v_cvt_pk_bf8_f32); saturating: clamp before the convert
+template <int FMT>
 __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
-    a = fminf(fmaxf(a, -FP8_E4M3_MAX), FP8_E4M3_MAX);
-    b = fminf(fmaxf(b, -FP8_E4M3_MAX), FP8_E4M3_MAX);
-    c = fminf(fmaxf(c, -FP8_E4M3_MAX), FP8_E4M3_MAX);
-    d = fminf(fmaxf(d, -FP8_E4M3_MAX), FP8_E4M3_MAX);
-    int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);   // bytes 0,1
-    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);         // bytes 2,3
+    constexpr float M = FMT == 0 ? FP8_E4M3_MAX : FP8_E5M2_MAX;
+    a = fminf(fmaxf(a, -M), M);
+    b = fminf(fmaxf(b, -M), M);
+    c = fminf(fmaxf(c, -M), M);
+    d = fminf(fmaxf(d, -M), M);
+    int w;
+    if constexpr (FMT == 0) {
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);  // bytes 0,1
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);   // bytes 2,3
+    } else {
+        w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+        w = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
+    }
     return (unsigned)w;
 }
 
-template <typename T>
+template <typename T, int FMT>
 __global__ void __launch_bounds__(256) cast_fp8_kernel(const T* __restrict__ x, size_t n, const float* __restrict__ scale,
                                                        uint8_t* __restrict__ out, unsigned* __restrict__ amax_bits) {
     constexpr int V = Vec<T>::N;  // 8 bf16 / 4 fp32 per 16-byte load
@@ -45,11 +55,12 @@ __global__ void __launch_bounds__(256) cast_fp8_kernel(const T* __restrict__ x, 
 #pragma unroll
         for (int j = 0; j < V; ++j) am = fmaxf(am, fabsf(a.v[j]));
         if constexpr (V == 8) {
-            uint2 o = {pack4_fp8(a.v[0] * s, a.v[1] * s, a.v[2] * s, a.v[3] * s),
-                       pack4_fp8(a.v[4] * s, a.v[5] * s, a.v[6] * s, a.v[7] * s)};
+            uint2 o = {pack4_fp8<FMT>(a.v[0] * s, a.v[1] * s, a.v[2] * s, a.v[3] * s),
+                       pack4_fp8<FMT>(a.v[4] * s, a.v[5] * s, a.v[6] * s, a.v[7] * s)};
             *reinterpret_cast<uint2*>(out + i * V) = o;
         } else {
-            *reinterpret_cast<unsigned*>(out + i * V) = pack4_fp8(a.v[0] * s, a.v[1] * s, a.v[2] * s, a.v[3] * s);
+            *reinterpret_cast<unsigned*>(out + i * V) =
+                pack4_fp8<FMT>(a.v[0] * s, a.v[1] * s, a.v[2] * s, a.v[3] * s);
         }
     }
     // scalar tail
@@ -57,7 +68,7 @@ __global__ void __launch_bounds__(256) cast_fp8_kernel(const T* __restrict__ x, 
     if (blockIdx.x == 0 && t < n) {
         const float v = ld1<T>(x + t);
         am = fmaxf(am, fabsf(v));
-        out[t] = (uint8_t)(pack4_fp8(v * s, 0.f, 0.f, 0.f) & 0xFF);
+        out[t] = (uint8_t)(pack4_fp8<FMT>(v * s, 0.f, 0.f, 0.f) & 0xFF);
     }
     // one atomic per block: thousands of same-address atomics serialise at the L2 (measured 170 us per
     // 67 MB cast with per-wave atomics vs ~25 us of streaming)
@@ -69,7 +80,7 @@ __global__ void __launch_bounds__(256) cast_fp8_kernel(const T* __restrict__ x, 
 // amax_cur [n] (float bits, zeroed here after use), hist [n][H], scale/inv [n]
 __global__ void __launch_bounds__(256) update_scales_kernel(unsigned* __restrict__ amax_cur, float* __restrict__ hist,
                                                             float* __restrict__ scale, float* __restrict__ inv_scale,
-                                                            int n, int H, int pos, float margin) {
+                                                            int n, int H, int pos, float margin, float fmax) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float a = __uint_as_float(amax_cur[i]);
@@ -77,7 +88,7 @@ __global__ void __launch_bounds__(256) update_scales_kernel(unsigned* __restrict
     hist[(size_t)i * H + pos] = a;
     float m = 0.f;
     for (int k = 0; k < H; ++k) m = fmaxf(m, hist[(size_t)i * H + k]);
-    float s = (m > 0.f && isfinite(m)) ? FP8_E4M3_MAX / (m * margin) : 1.f;
+    float s = (m > 0.f && isfinite(m)) ? fmax / (m * margin) : 1.f;
     // keep scales powers of two: exact dequantisation, no rounding drift between steps
     s = exp2f(floorf(log2f(s)));
     scale[i] = s;
@@ -88,18 +99,19 @@ __global__ void __launch_bounds__(256) update_scales_kernel(unsigned* __restrict
 
 using namespace bpe;
 
-void launch_cast_fp8(int dtype, const void* x, size_t n, const float* scale, void* out, unsigned* amax_bits,
-                     hipStream_t s) {
+void launch_cast_fp8(int dtype, int fmt, const void* x, size_t n, const float* scale, void* out,
+                     unsigned* amax_bits, hipStream_t s) {
     if (n == 0) return;
     const int V = dtype == DT_BF16 ? 8 : 4;
     const int grid = stream_grid(n / V + 1, 256, 1024);
-    if (dtype == DT_BF16)
-        cast_fp8_kernel<__bf16><<<grid, 256, 0, s>>>((const __bf16*)x, n, scale, (uint8_t*)out, amax_bits);
-    else
-        cast_fp8_kernel<float><<<grid, 256, 0, s>>>((const float*)x, n, scale, (uint8_t*)out, amax_bits);
+#define CAST(T, F) cast_fp8_kernel<T, F><<<grid, 256, 0, s>>>((const T*)x, n, scale, (uint8_t*)out, amax_bits)
+    if (dtype == DT_BF16) { if (fmt == 0) CAST(__bf16, 0); else CAST(__bf16, 1); }
+    else { if (fmt == 0) CAST(float, 0); else CAST(float, 1); }
+#undef CAST
 }
 
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,
-                          float margin, hipStream_t s) {
-    update_scales_kernel<<<(n + 255) / 256, 256, 0, s>>>(amax_cur, hist, scale, inv_scale, n, H, pos, margin);
+                          float margin, int fmt, hipStream_t s) {
+    update_scales_kernel<<<(n + 255) / 256, 256, 0, s>>>(amax_cur, hist, scale, inv_scale, n, H, pos, margin,
+                                                         fmt == 0 ? FP8_E4M3_MAX : FP8_E5M2_MAX);
 }

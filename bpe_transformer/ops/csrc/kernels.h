@@ -45,10 +45,10 @@ void launch_softmax_fwd(int dtype, const void* x, void* y, int M, int N, hipStre
 void launch_softmax_bwd(int dtype, const void* dy, const void* y, void* dx, int M, int N, hipStream_t s);
 
 // fp8.hip
-void launch_cast_fp8(int dtype, const void* x, size_t n, const float* scale, void* out, unsigned* amax_bits,
-                     hipStream_t s);
+void launch_cast_fp8(int dtype, int fmt, const void* x, size_t n, const float* scale, void* out,
+                     unsigned* amax_bits, hipStream_t s);  // fmt 0 = e4m3fn, 1 = e5m2
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,
-                          float margin, hipStream_t s);
+                          float margin, int fmt, hipStream_t s);
 
 // gemm.hip
 size_t gemm_lds_bytes();

@@ -286,19 +286,22 @@ void cast_fp8(const at::Tensor& x, const at::Tensor& scale, at::Tensor out, at::
     TORCH_CHECK(amax_bits.scalar_type() == at::kInt && amax_bits.numel() == 1, "cast_fp8: amax slot must be int32");
     check_aligned(x, "x");
     DevGuard g(x.device());
-    launch_cast_fp8(dt_code(x), x.data_ptr(), x.numel(), scale.data_ptr<float>(), out.data_ptr(),
+    const int fmt = out.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
+    TORCH_CHECK(fmt == 1 || out.scalar_type() == at::kFloat8_e4m3fn || out.scalar_type() == at::kByte,
+                "cast_fp8: out must be float8_e4m3fn or float8_e5m2");
+    launch_cast_fp8(dt_code(x), fmt, x.data_ptr(), x.numel(), scale.data_ptr<float>(), out.data_ptr(),
                     reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
 }
 
 void update_scales(at::Tensor amax_bits, at::Tensor hist, at::Tensor scale, at::Tensor inv_scale, int64_t pos,
-                   double margin) {
+                   double margin, int64_t fmt) {
     check_cuda(hist, "hist");
     const int n = (int)hist.size(0), H = (int)hist.size(1);
     TORCH_CHECK(amax_bits.numel() == n && scale.numel() == n && inv_scale.numel() == n, "update_scales: sizes");
     DevGuard g(hist.device());
     launch_update_scales(reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), hist.data_ptr<float>(),
                          scale.data_ptr<float>(), inv_scale.data_ptr<float>(), n, H, (int)(pos % H), (float)margin,
-                         cur_stream());
+                         (int)fmt, cur_stream());
 }
 
 // ---------------------------------------------------------------- RoPE
@@ -409,7 +412,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
     m.def("update_scales(Tensor(a!) amax_bits, Tensor(b!) hist, Tensor(c!) scale, Tensor(d!) inv_scale, int pos, "
-          "float margin) -> ()");
+          "float margin, int fmt=0) -> ()");
     m.def("softmax_fwd(Tensor x) -> Tensor");
     m.def("softmax_bwd(Tensor dy, Tensor y) -> Tensor");
     m.def("rope(Tensor x, Tensor pos, Tensor cos, Tensor sin, bool inverse) -> Tensor");

@@ -8,8 +8,11 @@ Recipe (BASELINE.json "Llama-style 1.1B fp8 MFMA path"):
     derived from an amax history (delayed scaling, powers of two); the cast
     pass also records this step's amax, and one launch per step refreshes all
     scales -- the host never reads a scale;
-  * backward GEMMs stay bf16 on the saved bf16 activations (fp8 forward,
-    bf16 gradients), master weights and optimizer state stay fp32.
+  * input-gradient GEMMs (dX = dY . W) optionally run in fp8 too: dY is
+    quantised to e5m2 (wider range, the usual gradient format) with its own
+    delayed scales, W reuses the forward's e4m3 copy (transposed once);
+    weight-gradient GEMMs stay bf16 on the saved bf16 activations; master
+    weights and optimizer state stay fp32.
 """
 
 from __future__ import annotations
@@ -20,12 +23,16 @@ from torch import Tensor
 from ._ext import ops
 
 FP8 = torch.float8_e4m3fn
+BF8 = torch.float8_e5m2
+_FMT = {"e4m3": (FP8, 0), "e5m2": (BF8, 1)}
 
 
 class Fp8State:
-    """Scaling state for ``n_slots`` quantised tensors (device-resident)."""
+    """Scaling state for ``n_slots`` quantised tensors of one format (device-resident)."""
 
-    def __init__(self, n_slots: int, device, history: int = 16, margin: float = 1.0):
+    def __init__(self, n_slots: int, device, history: int = 16, margin: float = 1.0, fmt: str = "e4m3"):
+        self.dtype, self.fmt_code = _FMT[fmt]
+        self.fmt = fmt
         self.n = n_slots
         self.amax = torch.zeros(n_slots, dtype=torch.int32, device=device)
         self.hist = torch.zeros(n_slots, history, dtype=torch.float32, device=device)
@@ -35,13 +42,13 @@ class Fp8State:
         self.pos = 0
 
     def cast(self, x: Tensor, slot: int) -> Tensor:
-        out = torch.empty(x.shape, dtype=FP8, device=x.device)
+        out = torch.empty(x.shape, dtype=self.dtype, device=x.device)
         ops().cast_fp8(x.contiguous(), self.scale[slot : slot + 1], out, self.amax[slot : slot + 1])
         return out
 
     def update(self) -> None:
         """Fold this step's amaxes into the history and recompute every scale (one launch)."""
-        ops().update_scales(self.amax, self.hist, self.scale, self.inv_scale, self.pos, self.margin)
+        ops().update_scales(self.amax, self.hist, self.scale, self.inv_scale, self.pos, self.margin, self.fmt_code)
         self.pos += 1
 
     def state_dict(self) -> dict:
@@ -59,14 +66,28 @@ class Fp8State:
         self.pos = int(sd["pos"])
         self.margin = float(sd["margin"])
 
-    def matmul(self, x: Tensor, w: Tensor, x_slot: int, w_slot: int) -> Tensor:
-        """``x @ w.T`` in fp8 with bf16 output; x: [M, K] bf16, w: [N, K] bf16."""
+    def matmul(self, x: Tensor, w: Tensor, x_slot: int, w_slot: int, keep_w8: bool = False):
+        """``x @ w.T`` in fp8 with bf16 output; x: [M, K] bf16, w: [N, K] bf16.  ``keep_w8`` also returns the
+        quantised weight (reused by the input-gradient GEMM)."""
         x8 = self.cast(x, x_slot)
         w8 = self.cast(w, w_slot)
-        return torch._scaled_mm(x8, w8.t(), scale_a=self.inv_scale[x_slot], scale_b=self.inv_scale[w_slot],
-                                out_dtype=torch.bfloat16)
+        y = torch._scaled_mm(x8, w8.t(), scale_a=self.inv_scale[x_slot], scale_b=self.inv_scale[w_slot],
+                             out_dtype=torch.bfloat16)
+        return (y, w8) if keep_w8 else y
 
 
-def quantize_reference(x: Tensor, scale: float) -> Tensor:
-    """Oracle: saturating cast to e4m3fn and back (for tests)."""
-    return (x.float() * scale).clamp(-448.0, 448.0).to(FP8).float() / scale
+def dgrad(g_state: Fp8State, g: Tensor, g_slot: int, w8: Tensor, w_state: Fp8State, w_slot: int) -> Tensor:
+    """``g @ W`` with g: [M, N] bf16 quantised to e5m2 (slot ``g_slot`` of ``g_state``) and W the forward's e4m3
+    copy w8: [N, K] (its scale in slot ``w_slot`` of ``w_state``).  The library wants the second operand
+    column-major, i.e. W^T contiguous."""
+    g8 = g_state.cast(g.contiguous(), g_slot)
+    w8t = w8.t().contiguous()
+    return torch._scaled_mm(g8, w8t.t(), scale_a=g_state.inv_scale[g_slot], scale_b=w_state.inv_scale[w_slot],
+                            out_dtype=torch.bfloat16)
+
+
+def quantize_reference(x: Tensor, scale: float, fmt: str = "e4m3") -> Tensor:
+    """Oracle: saturating cast to e4m3fn / e5m2 and back (for tests)."""
+    dt, _ = _FMT[fmt]
+    m = 448.0 if fmt == "e4m3" else 57344.0
+    return (x.float() * scale).clamp(-m, m).to(dt).float() / scale

@@ -103,8 +103,8 @@ class TrainEngine:
             self.last_grad_norm = norm
         self.opt.step(lr, coef)
         self._mark("opt")
-        fp8 = getattr(self.model, "fp8_state", None)
-        if fp8 is not None:
+        states = self.model.fp8_states() if hasattr(self.model, "fp8_states") else []
+        for fp8 in states:
             if self.ddp is not None:
                 # identical scales on every rank: amax bit patterns order like the (non-negative) floats
                 torch.distributed.all_reduce(fp8.amax, op=torch.distributed.ReduceOp.MAX)

@@ -89,7 +89,7 @@ class Trainer:
         extra = {"rng": {"torch": torch.get_rng_state(),
                          "cuda": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else []}}
         if self.model.fp8_state is not None:
-            extra["fp8"] = self.model.fp8_state.state_dict()
+            extra["fp8"] = [st.state_dict() for st in self.model.fp8_states()]
         save_checkpoint(self.model, _EngineOptimizerView(self.engine), it, self._ckpt_path(it), rank=self.info.rank,
                         config=self.cfg.to_dict(), **extra)
 
@@ -103,7 +103,8 @@ class Trainer:
             self.model.load_state_dict(obj["model"])
         self.engine.load_state_dict(obj["optimizer"])
         if self.model.fp8_state is not None and "fp8" in obj:
-            self.model.fp8_state.load_state_dict(obj["fp8"])
+            for st, sd in zip(self.model.fp8_states(), obj["fp8"]):
+                st.load_state_dict(sd)
         rng = obj.get("rng")
         if rng is not None:
             torch.set_rng_state(rng["torch"].cpu())

@@ -332,18 +332,20 @@ def test_flash_attention_large_scores(gpu_device):
     assert rel(o.detach().cpu(), orf) < 2e-2
 
 
+@pytest.mark.parametrize("fmt", ["e4m3", "e5m2"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n", [4096, 1000003, 37])
-def test_cast_fp8_and_amax(gpu_device, dtype, n):
-    """Saturating e4m3fn cast (incl. values beyond +-448 after scaling) + amax recording."""
+def test_cast_fp8_and_amax(gpu_device, dtype, n, fmt):
+    """Saturating e4m3fn / e5m2 cast (incl. values beyond the range after scaling) + amax recording."""
     torch.manual_seed(0)
+    fdt, fmax, big = ((torch.float8_e4m3fn, 448.0, 300.0) if fmt == "e4m3" else (torch.float8_e5m2, 57344.0, 30000.0))
     x = (torch.randn(n, device=gpu_device) * 3).to(dtype)
-    x[n // 2] = 300.0  # saturates at scale 4
+    x[n // 2] = big  # saturates at scale 4
     scale = torch.tensor([4.0], device=gpu_device)
-    out = torch.empty(n, dtype=torch.float8_e4m3fn, device=gpu_device)
+    out = torch.empty(n, dtype=fdt, device=gpu_device)
     amax = torch.zeros(1, dtype=torch.int32, device=gpu_device)
     torch.ops.bpe_hip.cast_fp8(x.contiguous(), scale, out, amax)
-    ref = (x.float() * 4.0).clamp(-448, 448).to(torch.float8_e4m3fn)
+    ref = (x.float() * 4.0).clamp(-fmax, fmax).to(fdt)
     assert torch.equal(out.view(torch.uint8), ref.view(torch.uint8))
     assert amax.view(torch.float32).item() == x.float().abs().max().item()
 
@@ -355,8 +357,12 @@ def test_update_scales(gpu_device):
     hist[2, 1] = 3000.0  # older, larger amax dominates the window
     scale = torch.ones(n, device=gpu_device)
     inv = torch.ones(n, device=gpu_device)
-    torch.ops.bpe_hip.update_scales(amax, hist, scale, inv, 0, 1.0)
+    torch.ops.bpe_hip.update_scales(amax, hist, scale, inv, 0, 1.0, 0)
     assert scale.tolist() == [128.0, 1.0, 0.125]  # 2^floor(log2(448 / amax))
     assert torch.allclose(inv * scale, torch.ones(n, device=gpu_device))
     assert amax.tolist() == [0, 0, 0]
     assert hist[:, 0].tolist() == [2.0, 0.0, 1000.0]
+    # e5m2 (gradients): 2^floor(log2(57344 / amax))
+    amax.copy_(torch.tensor([2.0, 0.0, 1000.0], device=gpu_device).view(torch.int32))
+    torch.ops.bpe_hip.update_scales(amax, hist, scale, inv, 1, 1.0, 1)
+    assert scale.tolist() == [16384.0, 1.0, 32.0]  # row 2: pos 1 overwrote the old 3000 -> max 1000

@@ -84,17 +84,22 @@ def test_generate(gpu_device):
     assert out.shape == (11,)
 
 
-def test_fp8_forward_close_to_bf16(gpu_device):
-    """fp8 (e4m3, delayed scaling) block projections: loss and grads stay close to the bf16 path."""
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_fp8_close_to_bf16(gpu_device, dgrad):
+    """fp8 projections (e4m3 forward; with dgrad also e5m2 x e4m3 input gradients), delayed scaling: loss and
+    grads stay close to the bf16 path after one calibration step."""
     _, a = _pair(gpu_device)
     b = copy.deepcopy(a)
-    st = b.enable_fp8()
+    st = b.enable_fp8(dgrad=dgrad)
     ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
     tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
-    with torch.no_grad():  # calibration pass: record amaxes, derive scales
-        b.loss(ids, tgt)
-    st.update()
+    b.loss(ids, tgt).backward()  # calibration step: record activation / weight / gradient amaxes
+    for s_ in b.fp8_states():
+        s_.update()
+    b.zero_grad()
     assert bool((st.scale > 1).all()), st.scale  # small activations/weights -> scales above 1
+    if dgrad:
+        assert bool((b.fp8_grad_state.scale > 1).all())  # gradients are far below the e5m2 range
     la = a.loss(ids, tgt)
     la.backward()
     lb = b.loss(ids, tgt)
@@ -102,7 +107,7 @@ def test_fp8_forward_close_to_bf16(gpu_device):
     assert abs(la.item() - lb.item()) < 2e-2, (la.item(), lb.item())
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         e = (pb.grad.float() - pa.grad.float()).norm() / pa.grad.float().norm().clamp_min(1e-12)
-        assert e < 0.15, (n, float(e))
+        assert e < (0.2 if dgrad else 0.15), (n, float(e))
 
 
 def test_fp8_engine_reduces_loss(gpu_device):
