@@ -67,14 +67,20 @@ def _notify(p: Tensor) -> None:
 
 class FusedBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, ln1, wq, wk, wv, wo, ln2, w1, w3, w2, cos, sin, meta):
+    def forward(ctx, xr, xd, ln1, wq, wk, wv, wo, ln2, w1, w3, w2, cos, sin, meta):
         B, S, H, Hkv, D, eps, use_rope = meta[:7]
         # fp8: (e4m3 Fp8State, first slot, e5m2 gradient Fp8State or None, first gradient slot) or None
         fp8 = meta[7] if len(meta) > 7 else None
         scale = 1.0 / math.sqrt(D)
         w_qkv = _cat_weights([wq, wk, wv])
         w_13 = _cat_weights([w1, w3])
-        h1, r1 = hip().rmsnorm_fwd(x2, ln1, eps)
+        # block input x2 = xr + xd: the previous block's residual and its un-added FFN output (residual adds
+        # are fused into the following RMSNorm instead of a copy-then-accumulate GEMM)
+        if xd is None:
+            x2 = xr
+            h1, r1 = hip().rmsnorm_fwd(x2, ln1, eps)
+        else:
+            x2, h1, r1 = hip().add_rmsnorm_fwd(xr, xd, ln1, eps)
         w8s = None
         if fp8 is not None:
             st, s0 = fp8[0], fp8[1]  # slots s0..s0+3: activations, s0+4..s0+7: weights
@@ -93,30 +99,26 @@ class FusedBlockFn(torch.autograd.Function):
             qkv = torch.matmul(h1, w_qkv.t())
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale)
-        if fp8 is not None:
-            xm = x2 + mm(o, wo.detach(), 1)
-        else:
-            xm = torch.addmm(x2, o, wo.t())
-        h2, r2 = hip().rmsnorm_fwd(xm, ln2, eps)
+        g1 = mm(o, wo.detach(), 1) if fp8 is not None else torch.matmul(o, wo.t())
+        xm, h2, r2 = hip().add_rmsnorm_fwd(x2, g1, ln2, eps)
         gu = mm(h2, w_13, 2) if fp8 is not None else torch.matmul(h2, w_13.t())
         a = hip().swiglu_fwd(gu)
-        if fp8 is not None:
-            y = xm + mm(a, w2.detach(), 3)
-        else:
-            y = torch.addmm(xm, a, w2.t())
+        g2 = mm(a, w2.detach(), 3) if fp8 is not None else torch.matmul(a, w2.t())
         ctx.w8s = w8s if w8s else None
+        ctx.has_xd = xd is not None
         ctx.save_for_backward(x2, r1, h1, qkv, o, lse, xm, r2, h2, gu, a, cos, sin)
         ctx.params = (ln1, wq, wk, wv, wo, ln2, w1, w3, w2)
         ctx.meta = meta
-        return y
+        return xm, g2  # block output = xm + g2, added by the consumer
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dxm_out, dg2):
         x2, r1, h1, qkv, o, lse, xm, r2, h2, gu, a, cos, sin = ctx.saved_tensors
         ln1, wq, wk, wv, wo, ln2, w1, w3, w2 = ctx.params
         B, S, H, Hkv, D, eps, use_rope = ctx.meta[:7]
         scale = 1.0 / math.sqrt(D)
-        dy = dy.contiguous()
+        dy = dg2.contiguous()  # gradient of the FFN output g2
+        dxm_out = dxm_out.contiguous()  # gradient reaching xm through the residual stream
         params = ctx.params
         main = all(hasattr(p, "main_grad") for p in params)
         grads: dict[int, Tensor] = {}
@@ -160,7 +162,7 @@ class FusedBlockFn(torch.autograd.Function):
         dgu = hip().swiglu_bwd(da, gu)
         acc_weight([w1, w3], dgu, h2)
         dh2 = dx(dgu, [w1, w3], 2)
-        dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dy)
+        dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dxm_out)
         # ---- attention
         acc_weight([wo], dxm, o)
         do = dx(dxm, [wo], 1)
@@ -168,39 +170,71 @@ class FusedBlockFn(torch.autograd.Function):
         dqkv = hip().fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, use_rope, scale)
         acc_weight([wq, wk, wv], dqkv, h1)
         dh1 = dx(dqkv, [wq, wk, wv], 0)
-        dx, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm)
+        dx2, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm)
+        dxd = dx2 if ctx.has_xd else None
         if main:
             ln2.main_grad.add_(dln2)
             ln1.main_grad.add_(dln1)
             _notify(ln2)
             _notify(ln1)
-            return (dx,) + (None,) * 12
+            return (dx2, dxd) + (None,) * 12
         grads[id(ln1)] = dln1
         grads[id(ln2)] = dln2
-        return (dx, grads[id(ln1)], grads[id(wq)], grads[id(wk)], grads[id(wv)], grads[id(wo)], grads[id(ln2)],
+        return (dx2, dxd, grads[id(ln1)], grads[id(wq)], grads[id(wk)], grads[id(wv)], grads[id(wo)], grads[id(ln2)],
                 grads[id(w1)], grads[id(w3)], grads[id(w2)], None, None, None)
+
+
+class AddRMSNormFn(torch.autograd.Function):
+    """RMSNorm(xr + xd) with the residual add fused (the model's final norm after the last fused block)."""
+
+    @staticmethod
+    def forward(ctx, xr, xd, w, eps):
+        s_, y, r = hip().add_rmsnorm_fwd(xr, xd, w, eps)
+        ctx.save_for_backward(s_, w, r)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        s_, w, r = ctx.saved_tensors
+        dx, dw = hip().rmsnorm_bwd(dy.contiguous(), s_, w.detach(), r, None)
+        return dx, dx, dw.to(w.dtype), None
 
 
 _EMPTY: dict = {}
 
 
-def fused_block_forward(block, x: Tensor) -> Tensor:
-    """Run ``block`` (a TransformerBlock) through :class:`FusedBlockFn`; x: [B, S, d] bf16 on the GPU."""
-    B, S, d = x.shape
+def fused_block_pair(block, xr: Tensor, xd: Tensor | None, B: int, S: int) -> tuple[Tensor, Tensor]:
+    """Run ``block`` on input ``xr + xd`` ([B*S, d] each; xd may be None); returns (residual, delta) whose sum
+    is the block output -- the next block (or the final norm) adds them inside its RMSNorm."""
     attn, ffn = block.attn, block.ffn
     if attn.rope is not None:
         cos, sin, use_rope = attn.rope.cos, attn.rope.sin, True
     else:
-        key = x.device
+        key = xr.device
         if key not in _EMPTY:
-            _EMPTY[key] = torch.empty(0, 0, device=x.device, dtype=torch.float32)
+            _EMPTY[key] = torch.empty(0, 0, device=key, dtype=torch.float32)
         cos = sin = _EMPTY[key]
         use_rope = False
     meta = (B, S, attn.num_heads, attn.num_kv_heads, attn.d_k, block.ln1.eps, use_rope)
     fp8 = getattr(block, "fp8", None)
     if fp8 is not None:
         meta = meta + (fp8,)
-    y = FusedBlockFn.apply(x.reshape(B * S, d).contiguous(), block.ln1.weight, attn.q_proj.weight,
-                           attn.k_proj.weight, attn.v_proj.weight, attn.output_proj.weight, block.ln2.weight,
-                           ffn.w1.weight, ffn.w3.weight, ffn.w2.weight, cos, sin, meta)
-    return y.view(B, S, d)
+    return FusedBlockFn.apply(xr, xd, block.ln1.weight, attn.q_proj.weight, attn.k_proj.weight,
+                              attn.v_proj.weight, attn.output_proj.weight, block.ln2.weight, ffn.w1.weight,
+                              ffn.w3.weight, ffn.w2.weight, cos, sin, meta)
+
+
+def fused_block_forward(block, x: Tensor) -> Tensor:
+    """Run one ``block`` (a TransformerBlock) through :class:`FusedBlockFn`; x: [B, S, d] bf16 on the GPU."""
+    B, S, d = x.shape
+    xm, g2 = fused_block_pair(block, x.reshape(B * S, d).contiguous(), None, B, S)
+    return (xm + g2).view(B, S, d)
+
+
+def fused_stack_forward(layers, ln_final, x: Tensor) -> Tensor:
+    """All blocks + the final RMSNorm with every residual add fused into the following norm."""
+    B, S, d = x.shape
+    xr, xd = x.reshape(B * S, d).contiguous(), None
+    for layer in layers:
+        xr, xd = fused_block_pair(layer, xr, xd, B, S)
+    return AddRMSNormFn.apply(xr, xd, ln_final.weight, ln_final.eps).view(B, S, d)

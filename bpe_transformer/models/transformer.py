@@ -10,12 +10,18 @@ their gradient.
 
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import Tensor, nn
 
 from .. import ops
 from .config import ModelConfig
 from .layers import Embedding, Linear, RMSNorm, TransformerBlock
+
+# GPU path: residual adds fused into the following RMSNorm across block boundaries (0 = per-block fallback,
+# for A/B measurements)
+_FUSED_STACK = os.environ.get("BPE_FUSED_STACK", "1") == "1"
 
 
 class TransformerLM(nn.Module):
@@ -92,6 +98,11 @@ class TransformerLM(nn.Module):
     def hidden_states(self, in_indices: Tensor) -> Tensor:
         assert in_indices.shape[-1] <= self.context_length, "sequence longer than context_length"
         x = self.token_embeddings(in_indices)
+        if (_FUSED_STACK and len(self.layers) and x.dim() == 3
+                and all(layer._fused_ok(x) for layer in self.layers)):
+            from .fused_block import fused_stack_forward
+
+            return fused_stack_forward(self.layers, self.ln_final, x)
         for layer in self.layers:
             x = layer(x)
         return self.ln_final(x)

@@ -34,13 +34,10 @@ namespace bpe {
 namespace fa {
 
 template <int D> struct BwdCfg {
-#ifdef BPE_FA_BWD_2WG
-    // two independent 4-wave workgroups per CU (their phases drift apart, so one's softmax VALU overlaps the
-    // other's MFMAs), single-buffered Q / dO tiles (written after the dS barrier, when no wave reads them)
-    static constexpr int NW = 4, QBUF = (D == 64) ? 1 : 2, WGS = (D == 64) ? 2 : 1;
-#else
-    static constexpr int NW = (D == 64) ? 8 : 4, QBUF = 2, WGS = 1;  // waves per workgroup
-#endif
+    // waves per workgroup, Q / dO buffers, workgroups per CU.  (Measured alternative: two independent
+    // 4-wave / 128-key workgroups per CU with single-buffered Q / dO -- 20-30 % slower: twice the dQ atomics
+    // and no gain from the de-phased waves.)
+    static constexpr int NW = (D == 64) ? 8 : 4, QBUF = 2, WGS = 1;
     static constexpr int KB = 32 * NW;                                  // keys per workgroup
     static constexpr int RB = D * 2;
     static constexpr int QT = 64 * RB;                                  // bytes per 64-query tile

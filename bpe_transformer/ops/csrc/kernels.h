@@ -11,6 +11,8 @@ enum { DT_F32 = 0, DT_BF16 = 1 };
 // rmsnorm.hip
 void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float* rstd, int M, int N, float eps,
                         hipStream_t s);
+void launch_add_rmsnorm_fwd(int dtype, const void* x, const void* d, const void* w, void* sum, void* y, float* rstd,
+                            int M, int N, float eps, hipStream_t s);
 int rmsnorm_bwd_grid(int M);
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
                         float* partial, void* dw, const void* dres, int M, int N, hipStream_t s);

@@ -45,6 +45,47 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const T* __restrict__ 
     }
 }
 
+// Residual add fused into the norm: s = x + d (rounded to T: the residual stream is stored in T), y = RMSNorm(s).
+// Replaces "addmm(x, o, W^T)" (a full copy of x into the GEMM output, then a beta = 1 GEMM) + rmsnorm with a
+// plain GEMM and one pass here.  The second sweep re-reads s from L2 (just written by the same wave).
+template <typename T>
+__global__ void __launch_bounds__(256) add_rmsnorm_fwd_kernel(const T* __restrict__ x, const T* __restrict__ d,
+                                                              const T* __restrict__ w, T* __restrict__ sum,
+                                                              T* __restrict__ y, float* __restrict__ rstd_out, int M,
+                                                              int N, float eps) {
+    constexpr int V = Vec<T>::N;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const size_t off = (size_t)row * N;
+    const int nvec = N / V;
+    float ss = 0.f;
+    for (int i = lane; i < nvec; i += 64) {
+        Vec<T> a, b;
+        a.load(x + off + i * V);
+        b.load(d + off + i * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            float v = a.v[j] + b.v[j];
+            if constexpr (sizeof(T) == 2) v = bf2f(f2bf(v));  // statistics of the stored (rounded) sum
+            a.v[j] = v;
+            ss += v * v;
+        }
+        a.store(sum + off + i * V);
+    }
+    ss = wave_sum(ss);
+    const float r = rsqrtf(ss / (float)N + eps);
+    if (lane == 0 && rstd_out) rstd_out[row] = r;
+    for (int i = lane; i < nvec; i += 64) {
+        Vec<T> a, g;
+        a.load(sum + off + i * V);
+        g.load(w + i * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) a.v[j] = a.v[j] * r * g.v[j];
+        a.store(y + off + i * V);
+    }
+}
+
 // C = number of 16-byte column chunks each lane owns (ceil(N / V / 64)).
 template <typename T, int C>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
@@ -184,6 +225,17 @@ static void rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* r
     }
     RMS_CASE(1) RMS_CASE(2) RMS_CASE(4) RMS_CASE(8)
 #undef RMS_CASE
+}
+
+void launch_add_rmsnorm_fwd(int dtype, const void* x, const void* d, const void* w, void* sum, void* y, float* rstd,
+                            int M, int N, float eps, hipStream_t s) {
+    const int grid = (M + 3) / 4;
+    if (dtype == DT_BF16)
+        add_rmsnorm_fwd_kernel<__bf16><<<grid, 256, 0, s>>>((const __bf16*)x, (const __bf16*)d, (const __bf16*)w,
+                                                            (__bf16*)sum, (__bf16*)y, rstd, M, N, eps);
+    else
+        add_rmsnorm_fwd_kernel<float><<<grid, 256, 0, s>>>((const float*)x, (const float*)d, (const float*)w,
+                                                           (float*)sum, (float*)y, rstd, M, N, eps);
 }
 
 int rmsnorm_bwd_grid(int M) {

@@ -39,6 +39,28 @@ void check_aligned(const at::Tensor& t, const char* name) {
 }
 
 // ---------------------------------------------------------------- RMSNorm
+// s = x + d (stored), y = RMSNorm(s) -> (s, y, rstd)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> add_rmsnorm_fwd(const at::Tensor& x, const at::Tensor& d,
+                                                               const at::Tensor& w, double eps) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.is_contiguous() && d.is_contiguous() && w.is_contiguous(), "add_rmsnorm: contiguous inputs required");
+    TORCH_CHECK(x.scalar_type() == w.scalar_type() && d.scalar_type() == x.scalar_type(), "add_rmsnorm: dtypes differ");
+    TORCH_CHECK(d.sizes() == x.sizes(), "add_rmsnorm: x and d shapes differ");
+    const int N = (int)x.size(-1);
+    TORCH_CHECK(w.numel() == N, "add_rmsnorm: weight size mismatch");
+    TORCH_CHECK(N % vec_elems(x) == 0, "add_rmsnorm: last dim must be a multiple of 8 (bf16) / 4 (fp32)");
+    check_aligned(x, "x");
+    check_aligned(d, "d");
+    const int M = (int)(x.numel() / N);
+    DevGuard g(x.device());
+    auto sum = at::empty_like(x);
+    auto y = at::empty_like(x);
+    auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+    launch_add_rmsnorm_fwd(dt_code(x), x.data_ptr(), d.data_ptr(), w.data_ptr(), sum.data_ptr(), y.data_ptr(),
+                           rstd.data_ptr<float>(), M, N, (float)eps, cur_stream());
+    return {sum, y, rstd};
+}
+
 std::tuple<at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps) {
     check_cuda(x, "x");
     TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "rmsnorm: contiguous inputs required");
@@ -397,6 +419,7 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
 
 TORCH_LIBRARY(bpe_hip, m) {
     m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
+    m.def("add_rmsnorm_fwd(Tensor x, Tensor d, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
     m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
     m.def("swiglu_fwd(Tensor gu) -> Tensor");
     m.def("swiglu_bwd(Tensor dout, Tensor gu) -> Tensor");
@@ -424,6 +447,7 @@ TORCH_LIBRARY(bpe_hip, m) {
 
 TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+    m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
     m.impl("rmsnorm_bwd", &rmsnorm_bwd);
     m.impl("swiglu_fwd", &swiglu_fwd);
     m.impl("swiglu_bwd", &swiglu_bwd);

@@ -28,15 +28,26 @@ class _LMHeadCEFn(torch.autograd.Function):
         loss_rows, _ = ops().ce_fwd_bwd(logits, targets, ignore_index, True)
         nvalid = (targets != ignore_index).sum().clamp_min(1).to(torch.float32)
         ctx.save_for_backward(h, w, logits)
+        ctx.w_param = w
         return loss_rows.sum() / nvalid
 
     @staticmethod
     def backward(ctx, g: Tensor):
         h, w, dlogits = ctx.saved_tensors
-        dh = torch.matmul(dlogits, w)
-        dw = torch.matmul(dlogits.t(), h)
-        gg = g.to(dh.dtype)
-        return dh * gg, dw * gg, None, None
+        gg = g.to(h.dtype)
+        dh = torch.matmul(dlogits, w) * gg  # the upstream scale goes on the small operands, never on the logits
+        hs = h * gg
+        mg = getattr(ctx.w_param, "main_grad", None)
+        if mg is not None:
+            # weight gradient accumulated in place into the flat gradient buffer (no temporary, no grad add)
+            from .gemm import accumulate_weight_grad
+
+            accumulate_weight_grad(mg, dlogits, hs)
+            cb = getattr(ctx.w_param, "_bpe_grad_ready", None)
+            if cb is not None:
+                cb(ctx.w_param)
+            return dh, None, None, None
+        return dh, torch.matmul(dlogits.t(), hs), None, None
 
 
 class _CrossEntropyFn(torch.autograd.Function):
