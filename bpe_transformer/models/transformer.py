@@ -22,6 +22,9 @@ from .layers import Embedding, Linear, RMSNorm, TransformerBlock
 # GPU path: residual adds fused into the following RMSNorm across block boundaries (0 = per-block fallback,
 # for A/B measurements)
 _FUSED_STACK = os.environ.get("BPE_FUSED_STACK", "1") == "1"
+# LM-head rows padded (with zero rows, inside the flat parameter buffer) to a multiple of this, so the vocab
+# dimension of the head GEMMs and the logits row stride are aligned (0 = off)
+_VOCAB_PAD = int(os.environ.get("BPE_VOCAB_PAD", "256"))
 
 
 class TransformerLM(nn.Module):
@@ -62,6 +65,8 @@ class TransformerLM(nn.Module):
         )
         self.ln_final = RMSNorm(d_model, eps, device=device, dtype=dtype) if not remove_rmsnorm else nn.Identity()
         self.lm_head = Linear(d_model, vocab_size, device=device, dtype=dtype)
+        if _VOCAB_PAD > 0 and vocab_size % _VOCAB_PAD:
+            self.lm_head.pad_rows = -(-vocab_size // _VOCAB_PAD) * _VOCAB_PAD
 
     @classmethod
     def from_config(cls, cfg: ModelConfig, device=None, dtype=None) -> "TransformerLM":

@@ -24,11 +24,19 @@ IGNORE_INDEX = -100
 class _LMHeadCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h: Tensor, w: Tensor, targets: Tensor, ignore_index: int):
-        logits = torch.matmul(h, w.t())  # hipBLASLt
-        loss_rows, _ = ops().ce_fwd_bwd(logits, targets, ignore_index, True)
+        V = w.shape[0]
+        # zero-row padded weight (flat buffer, optim/flat.py): aligned GEMM shapes and logits row stride; the
+        # pad columns of the logits are exactly 0 and the CE kernel never touches them, so their "gradient"
+        # stays 0 and contributes nothing to dh or dW
+        wp = getattr(w, "_bpe_padded", None)
+        if wp is None or wp.data_ptr() != w.data_ptr():
+            wp = w
+        logits = torch.matmul(h, wp.t())  # hipBLASLt
+        loss_rows, _ = ops().ce_fwd_bwd(logits[:, :V], targets, ignore_index, True)
         nvalid = (targets != ignore_index).sum().clamp_min(1).to(torch.float32)
-        ctx.save_for_backward(h, w, logits)
+        ctx.save_for_backward(h, wp, logits)
         ctx.w_param = w
+        ctx.padded = wp is not w
         return loss_rows.sum() / nvalid
 
     @staticmethod
@@ -37,7 +45,9 @@ class _LMHeadCEFn(torch.autograd.Function):
         gg = g.to(h.dtype)
         dh = torch.matmul(dlogits, w) * gg  # the upstream scale goes on the small operands, never on the logits
         hs = h * gg
-        mg = getattr(ctx.w_param, "main_grad", None)
+        mg = getattr(ctx.w_param, "_bpe_padded_grad" if ctx.padded else "main_grad", None)
+        if ctx.padded and mg is None:
+            return dh, torch.matmul(dlogits.t(), hs)[: ctx.w_param.shape[0]], None, None
         if mg is not None:
             # weight gradient accumulated in place into the flat gradient buffer (no temporary, no grad add)
             from .gemm import accumulate_weight_grad

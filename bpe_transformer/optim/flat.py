@@ -14,6 +14,15 @@ in ONE contiguous buffer laid out identically.  That buys:
 
 Parameters are packed in registration order, each starting at a 64-element
 aligned offset (16-byte vector alignment for every kernel; padding stays 0).
+
+A 2-D parameter may ask for zero ROW padding (``param._bpe_pad_rows = R``, or
+``module.pad_rows = R`` on its module for :meth:`FlatParameters.from_module`):
+its slot then reserves ``R x cols`` elements and the parameter is the first
+``rows`` of them.  ``param._bpe_padded`` / ``param._bpe_padded_grad`` are the
+``[R, cols]`` views.  The LM head uses this so the vocab dimension of its
+GEMMs is a multiple of 256 (vocab 50257 is odd: an odd logits row stride
+rules out the libraries' vector accesses).  The pad rows receive zero
+gradients, so AdamW keeps them exactly zero.
 """
 
 from __future__ import annotations
@@ -46,22 +55,34 @@ class FlatParameters:
         self.device = devices.pop()
         self.slots: list[Slot] = []
         off = 0
+        reserve: list[int] = []
         for name, p in named_params:
             n = p.numel()
+            pad_rows = getattr(p, "_bpe_pad_rows", None)
+            r = pad_rows * p.shape[1] if (pad_rows and p.dim() == 2 and pad_rows >= p.shape[0]) else n
             self.slots.append(Slot(name, p, off, n))
-            off += (n + ALIGN - 1) // ALIGN * ALIGN
+            reserve.append(r)
+            off += (r + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
         self.data = torch.zeros(off, dtype=self.dtype, device=self.device)
         self.grad = torch.zeros(off, dtype=grad_dtype or self.dtype, device=self.device)
         with torch.no_grad():
-            for s in self.slots:
+            for s, r in zip(self.slots, reserve):
                 view = self.data[s.offset : s.offset + s.numel].view_as(s.param)
                 view.copy_(s.param.data)
                 s.param.data = view
                 s.param.grad = self.grad[s.offset : s.offset + s.numel].view_as(s.param)
+                if r != s.numel:
+                    cols = s.param.shape[1]
+                    s.param._bpe_padded = self.data[s.offset : s.offset + r].view(r // cols, cols)
+                    s.param._bpe_padded_grad = self.grad[s.offset : s.offset + r].view(r // cols, cols)
 
     @classmethod
     def from_module(cls, module: nn.Module, grad_dtype: torch.dtype | None = None) -> "FlatParameters":
+        for m in module.modules():  # row padding requested on the module (survives deepcopy / .to())
+            rows = getattr(m, "pad_rows", None)
+            if rows and isinstance(getattr(m, "weight", None), nn.Parameter):
+                m.weight._bpe_pad_rows = rows
         return cls([(n, p) for n, p in module.named_parameters() if p.requires_grad], grad_dtype)
 
     def zero_grad(self) -> None:

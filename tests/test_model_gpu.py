@@ -149,3 +149,27 @@ def test_engine_phase_timing(gpu_device):
         eng.train_step([(x, torch.roll(x, -1, 1))])
     ph = eng.phase_times()
     assert set(ph) == {"fwd_ms", "bwd_ms", "comm_ms", "opt_ms"} and all(v >= 0 for v in ph.values())
+
+
+def test_padded_lm_head_matches_unpadded(gpu_device):
+    """The zero-row padded LM head (vocab 1000 -> 1024 rows in the flat buffer) gives the same loss and
+    gradients as the unpadded head, and AdamW keeps the pad rows exactly zero."""
+    from bpe_transformer.train.engine import TrainEngine
+
+    _, a = _pair(gpu_device)
+    b = copy.deepcopy(a)
+    b.lm_head.pad_rows = None
+    ea = TrainEngine(a, lr=1e-3, weight_decay=0.1, max_grad_norm=None)
+    eb = TrainEngine(b, lr=1e-3, weight_decay=0.1, max_grad_norm=None)
+    wp = a.lm_head.weight._bpe_padded
+    assert wp.shape == (1024, 256) and not hasattr(b.lm_head.weight, "_bpe_padded")
+    ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    for _ in range(3):
+        la = ea.train_step([(ids, tgt)])
+        lb = eb.train_step([(ids, tgt)])
+        assert abs(la.item() - lb.item()) < 1e-3, (la.item(), lb.item())
+    ga, gb = a.lm_head.weight._bpe_padded_grad, b.lm_head.weight.grad
+    assert torch.count_nonzero(ga[1000:]) == 0 and torch.count_nonzero(wp[1000:]) == 0
+    e = (ga[:1000].float() - gb.float()).norm() / gb.float().norm()
+    assert e < 1e-2, float(e)
