@@ -28,7 +28,29 @@ def bench(fn, iters=10):
     return s.elapsed_time(e) / iters
 
 
+def sweep():
+    """ms per split count for each GPT-2 dW shape (incl. the padded LM head), 256-tile kernel."""
+    T = 65536
+    for n, k in SHAPES["gpt2"][1] + [(50432, 768)]:
+        dy = torch.randn(T, n, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(T, k, device="cuda", dtype=torch.bfloat16)
+        g = torch.zeros(n, k, device="cuda", dtype=torch.bfloat16)
+        res = {}
+        for sp in sorted({1, 2, 3, 4, 5, 6, 8, 9, 10, 12, 14, 16, 20, 24, 28, 32, choose_splits_256(n, k, T)}):
+            if (n // 256) * (k // 256) * sp > 8 * 256:
+                continue
+            res[sp] = round(statistics.median(bench(lambda: hip().gemm(dy, False, x, False, g, 1.0, sp, 256))
+                                              for _ in range(3)), 4)
+        best = min(res, key=res.get)
+        fl = 2.0 * n * k * T
+        print(json.dumps({"shape": [n, k], "model_splits": choose_splits_256(n, k, T), "best_splits": best,
+                          "best_tf": round(fl / res[best] / 1e9), "ms": res}), flush=True)
+        del dy, x, g
+
+
 def main():
+    if "--sweep" in sys.argv:
+        return sweep()
     out = {"variant": os.environ.get("BPE_G256_VARIANT", "0")}
     for model, (T, shapes) in SHAPES.items():
         tot_b = tot_o = 0.0

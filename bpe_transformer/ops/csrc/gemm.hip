@@ -95,9 +95,10 @@ gemm_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B
     const int ntiles = (Mo / BM) * tiles_n;
     const int tile = blockIdx.x % ntiles, split = blockIdx.x / ntiles;
     const int i0 = (tile / tiles_n) * BM, j0 = (tile % tiles_n) * BN;
-    const int rlen = R / splits;  // multiple of BK (host-checked)
-    const int rbeg = split * rlen;
-    const int nk = rlen / BK;
+    // split s owns k-steps [s*nkt/splits, (s+1)*nkt/splits): any split count, ranges differ by <= 1 step
+    const int nkt = R / BK;
+    const int kb = (int)((long)split * nkt / splits), nk = (int)((long)(split + 1) * nkt / splits) - kb;
+    const int rbeg = kb * BK;
     char* As = smem;                    // [2][16 KiB]
     char* Bs = smem + 2 * TILE_BYTES;   // [2][16 KiB]
     const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
@@ -378,9 +379,12 @@ gemm256_tn_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restri
     const int ntiles = (Mo / BM) * tiles_n;
     const int split = wid / ntiles, tile = wid % ntiles;
     const int i0 = (tile / tiles_n) * BM, j0 = (tile % tiles_n) * BN;
-    const int rlen = R / splits;
-    const int rbeg = split * rlen;
-    const int nk = rlen / BK;  // >= NSTAGE - 1 (host-checked)
+    // split s owns k-steps [s*nkt/splits, (s+1)*nkt/splits) -- any split count (the cost model picks counts
+    // that fill whole waves of CUs, e.g. 28 splits x 9 tiles); nk >= NSTAGE - 1 (host-checked)
+    const int nkt = R / BK;
+    const int kb = (int)((long)split * nkt / splits);
+    const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
+    const int rbeg = kb * BK;
     const int rlast = rbeg + (nk - 1) * BK;
     const int wr = (w >> 2) * 128, wc = (w & 3) * 64;
 
@@ -439,9 +443,9 @@ size_t gemm_lds_bytes() { return 4 * (size_t)TILE_BYTES; }
 
 bool gemm_shape_ok(int Mo, int No, int R, int splits, int tile) {
     if (tile == 256)
-        return Mo % 256 == 0 && No % 256 == 0 && splits >= 1 && R % (g256::BK * splits) == 0 &&
-               R / splits >= g256::BK * (g256::NSTAGE - 1);
-    return Mo % BM == 0 && No % BN == 0 && splits >= 1 && R % (BK * splits) == 0;
+        return Mo % 256 == 0 && No % 256 == 0 && splits >= 1 && R % g256::BK == 0 &&
+               R / g256::BK / splits >= g256::NSTAGE - 1;
+    return Mo % BM == 0 && No % BN == 0 && splits >= 1 && R % BK == 0 && R / BK >= splits;
 }
 
 template <int MF, bool PRIO>

@@ -54,10 +54,12 @@ def choose_splits_256(n: int, k: int, t: int) -> int:
     t_kstep = 0.8e-6  # one 256x256x32 MFMA step at ~50% of the dense bf16 rate
     best, best_cost = 1, None
     for s in range(1, 65):
-        if nk % s or nk // s < 8:
+        if nk // s < 8:
             continue
+        # split ranges may be uneven (the kernel gives split i steps [i*nk/s, (i+1)*nk/s)); a wave lasts as long
+        # as its longest split
         waves = -(-tiles * s // _CUS)
-        cost = waves * (nk // s) * t_kstep + (2 * s * n * k * 4 / 4.0e12 if s > 1 else 0.0)
+        cost = waves * (-(-nk // s)) * t_kstep + (2 * s * n * k * 4 / 4.0e12 if s > 1 else 0.0)
         if best_cost is None or cost < best_cost * 0.97:
             best, best_cost = s, cost
     return best

@@ -232,7 +232,7 @@ def test_grad_norm_clip(gpu_device):
 
 # ---------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("splits", [1, 4, 7])
 @pytest.mark.parametrize("tile", [128, 256])
 def test_gemm_layouts(gpu_device, a_k, b_k, splits, tile):
     if tile == 256 and (a_k or b_k):
@@ -249,7 +249,8 @@ def test_gemm_layouts(gpu_device, a_k, b_k, splits, tile):
     assert rel(C.cpu(), ref.cpu()) < 1e-2
 
 
-@pytest.mark.parametrize("shape", [(2304, 768, 8192), (768, 768, 8192), (11264, 2048, 2048), (2048, 5632, 4096)])
+@pytest.mark.parametrize("shape", [(2304, 768, 8192), (768, 768, 8192), (11264, 2048, 2048), (2048, 5632, 4096),
+                                   (50432, 256, 4096), (768, 768, 65536)])
 def test_weight_grad_shapes(gpu_device, shape):
     """Model dW shapes through the routing in ops.gemm (256-tile kernel, split-K choice)."""
     from bpe_transformer.ops.gemm import accumulate_weight_grad
