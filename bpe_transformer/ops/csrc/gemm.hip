@@ -477,6 +477,12 @@ static void launch_g256(const __bf16* a, long lda, const __bf16* b, long ldb, fl
     }
 }
 
+void splitk_reduce(const float* slab, void* C, long ldc, float beta, int M, int N, int splits, hipStream_t s) {
+    const long total4 = (long)M * N / 4;
+    const int g = (int)std::min<long>((total4 + 255) / 256, 2048);
+    splitk_reduce_kernel<<<g, 256, 0, s>>>(slab, (__bf16*)C, ldc, beta, M, N, splits);
+}
+
 void launch_gemm(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                  float beta, int Mo, int No, int R, int splits, float* slab, int tile, hipStream_t s) {
     const __bf16* a = (const __bf16*)A;
@@ -492,9 +498,5 @@ void launch_gemm(int a_kmajor, int b_kmajor, const void* A, long lda, const void
         else { if (b_kmajor) G(false, true); else G(false, false); }
 #undef G
     }
-    if (splits > 1) {
-        const long total4 = (long)Mo * No / 4;
-        const int g = (int)std::min<long>((total4 + 255) / 256, 2048);
-        splitk_reduce_kernel<<<g, 256, 0, s>>>(slab, c, ldc, beta, Mo, No, splits);
-    }
+    if (splits > 1) splitk_reduce(slab, c, ldc, beta, Mo, No, splits, s);
 }

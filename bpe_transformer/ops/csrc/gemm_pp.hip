@@ -1,0 +1,581 @@
+// 8-wave ping-pong bf16 MFMA GEMM for gfx950 (all three GEMMs of a linear layer).
+//
+//   C[M, N] = beta * C + sum_r A(i, r) B(r, j)        (fp32 accumulation, bf16 or fp32-slab output)
+//
+// Each operand is row-major and either K-major (reduction index contiguous:
+// X [M][R] or W [N][R]) or MN-major (output index contiguous: dY [R][M],
+// W [R][N], X [R][N]).  The forward Y = X W^T is (K, K), the input gradient
+// dX = dY W is (K, MN), the weight gradient dW = dY^T X is (MN, MN).
+//
+// Geometry (guide §5 "The 256² 8-phase template", designed here for both
+// operand layouts): 256 x 256 output tile, BK = 64, 512 threads = 8 waves in
+// two groups of four.  Group g (waves 4g..4g+3) owns output rows
+// [128g, 128g+128); wave wl = w & 3 owns columns [64 wl, 64 wl + 64), i.e.
+// 8 x 4 accumulators of mfma_f32_16x16x32_bf16 (128 registers).  The MFMA is
+// issued as (B fragment, A fragment) so an accumulator register holds four
+// CONSECUTIVE output columns of one row (8-byte packed stores).
+//
+// Ping-pong: waves w and w+4 share a SIMD.  Group 1 runs one barrier behind
+// group 0, so in every barrier interval one wave of each SIMD issues 16 MFMAs
+// (one 64 x 32 quadrant of its tile over K = 64, 256 cycles) while its partner
+// reads the next quadrant's fragments from LDS and issues LDS-DMA for the
+// next K-tile: the matrix pipe alternates between the two waves and never
+// waits for LDS.  Quadrant order (m0,n0) (m0,n1) (m1,n1) (m1,n0) reuses one
+// operand's fragments between neighbours: 12 / 4 / 8 / 4 ds_read_b128 per
+// phase.
+//
+// Staging: two 64 KiB stages (A image 32 KiB + B image 32 KiB), filled by
+// global_load_lds_dwordx4 (LDS-DMA).  K-major images are [256][64] (128-byte
+// rows, 16-byte chunk c of row r at c ^ ((r >> 1) & 7): conflict-free for the
+// 16x16x32 ds_read_b128 lane groups); MN-major images are [64][256] (512-byte
+// rows, chunk c at c ^ sig(r), read with ds_read_b64_tr_b16).  The DMA image
+// is lane-linear, so the swizzle is applied to the SOURCE address.  K-tile
+// kt+1 is DMA'd during phases 0-1 of kt (group 0 the first halves of A and B,
+// group 1 the second halves), retired by each issuing wave's vmcnt(0) in
+// phase 3 before the barrier that precedes the first read of kt+1.  WAR: the
+// buffer refilled in phase 0 of kt was last read in phase 3 of kt-1, whose
+// reads retire (lgkmcnt(0)) before that phase's closing barrier.  Raw
+// s_barrier only: __syncthreads() would drain the DMA (guide §5 "Pipelining
+// across barriers").
+//
+// Split-K (weight gradients: R = all tokens) writes fp32 partial tiles to a
+// slab reduced by splitk_reduce_kernel (gemm.hip) in a fixed order.
+// Epilogue (bf16 output): the tile is staged through the then-free LDS as a
+// [256][512 B] image and written back as whole 512-byte rows.
+#include "fa_common.h"
+#include "kernels.h"
+
+#include <cstdlib>
+
+namespace bpe {
+namespace gpp {
+
+constexpr int NT = 512, BT = 256, BK = 64;
+constexpr int OPB = 32768;          // one operand image per stage
+constexpr int STAGE = 2 * OPB;      // 64 KiB
+constexpr int LDS_BYTES = 2 * STAGE;  // 128 KiB
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+__device__ __forceinline__ int fk(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int sig(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+// Source offset (elements, relative to the tile origin) of 16-byte image chunk e (0..2047).
+template <bool KM>
+__device__ __forceinline__ int src_off(int e, int ld) {
+    if constexpr (KM) {
+        const int row = e >> 3, lc = (e & 7) ^ fk(row);
+        return row * ld + lc * 8;
+    } else {
+        const int row = e >> 5, lc = (e & 31) ^ sig(row);
+        return row * ld + lc * 8;
+    }
+}
+
+// Tile origin of an operand for K-tile starting at k0 (t0 = first output row/column of the tile).
+template <bool KM>
+__device__ __forceinline__ const __bf16* tile_ptr(const __bf16* P, long ld, int t0, long k0) {
+    return KM ? P + (long)t0 * ld + k0 : P + k0 * ld + t0;
+}
+
+// DMA half h (= the issuing group) of one operand image: 4 wave-instructions of 1 KiB.
+__device__ __forceinline__ void dma_half(const __bf16* tile0, const int (&off)[4], char* img, int g, int wl) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_global_load_lds((gbl_void*)(tile0 + off[j]),
+                                         (lds_void*)(img + (g * 1024 + (wl * 4 + j) * 64) * 16), 16, 0, 0);
+}
+
+// MFMA operand fragment of 16-row/col block tb, k-step ks: lane l gets X[t = 16 tb + (l & 15)][k = 32 ks + 8 (l >> 4) + j].
+template <bool KM>
+__device__ __forceinline__ bf16x8 frag(char* img, int tb, int ks, int l) {
+    if constexpr (KM) {
+        const int row = tb * 16 + (l & 15);
+        const int ch = (4 * ks + (l >> 4)) ^ fk(l & 15);
+        return fa::lds_row16(img, row * 128 + (ch << 4));
+    } else {
+        const int r = 32 * ks + 8 * (l >> 4) + ((l & 15) >> 2);
+        const int c = tb * 16 + 4 * (l & 3);
+        const int o0 = r * 512 + (((c >> 3) ^ sig(r)) << 4) + ((c & 7) << 1);
+        const int o1 = (r + 4) * 512 + (((c >> 3) ^ sig(r + 4)) << 4) + ((c & 7) << 1);
+        return fa::lds_tr_pair(img, o0, o1);
+    }
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+struct Frags {
+    bf16x8 a[4][2];  // A (output rows): 4 i-blocks of the current m half x 2 k-steps
+    bf16x8 b[2][2];  // B (output cols): 2 j-blocks of the current n half x 2 k-steps
+};
+
+__device__ __forceinline__ void bar() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool AK, bool BKM>
+__device__ __forceinline__ void load_a(Frags& f, char* img, int g, int m, int l) {
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) f.a[ib][ks] = frag<AK>(img, 8 * g + 4 * m + ib, ks, l);
+}
+template <bool AK, bool BKM>
+__device__ __forceinline__ void load_b(Frags& f, char* img, int wl, int n, int l) {
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) f.b[jb][ks] = frag<BKM>(img, 4 * wl + 2 * n + jb, ks, l);
+}
+
+__device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const Frags& f, int m, int n) {
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+                acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
+}
+
+// One K-tile: four (load section, barrier, MFMA section, barrier) phases.  `cur` is read, `nxt` is the DMA
+// target (the __restrict__ parameters let the wait-count pass see that the fragment reads do not alias the
+// in-flight DMA; without it hipcc drains the DMA before the first read).
+// DIAG (timing diagnostics, numerically wrong): 1 = no DMA in the loop, 2 = fragment reads only in phase 0,
+// 3 = no MFMA, 4 = no stagger between the groups
+template <bool AK, bool BKM, int DIAG>
+__device__ __forceinline__ void ktile(char* __restrict__ cur, char* __restrict__ nxt, bool dma, const __bf16* an,
+                                      const __bf16* bn, const int (&oa)[4], const int (&ob)[4], int g, int wl,
+                                      int l, f32x4 (&acc)[8][4]) {
+    Frags f;
+    char* Ac = cur;
+    char* Bc = cur + OPB;
+    // phase 0: (m0, n0)
+    load_a<AK, BKM>(f, Ac, g, 0, l);
+    load_b<AK, BKM>(f, Bc, wl, 0, l);
+    if (DIAG == 1) dma = false;
+    if (dma) dma_half(an, oa, nxt, g, wl);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    if (DIAG != 3) mma_quadrant(acc, f, 0, 0);
+    bar();
+    // phase 1: (m0, n1)
+    if (DIAG != 2) load_b<AK, BKM>(f, Bc, wl, 1, l);
+    if (dma) dma_half(bn, ob, nxt + OPB, g, wl);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    if (DIAG != 3) mma_quadrant(acc, f, 0, 1);
+    bar();
+    // phase 2: (m1, n1)
+    if (DIAG != 2) load_a<AK, BKM>(f, Ac, g, 1, l);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    if (DIAG != 3) mma_quadrant(acc, f, 1, 1);
+    bar();
+    // phase 3: (m1, n0); retire this wave's DMA of the next K-tile before the barrier
+    if (DIAG != 2) load_b<AK, BKM>(f, Bc, wl, 0, l);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    bar();
+    if (DIAG != 3) mma_quadrant(acc, f, 1, 0);
+    bar();
+    if (DIAG == 3) {  // keep the fragments live
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) acc[ib][0][0] += (float)f.a[ib][0][0] + (float)f.b[ib & 1][1][1];
+    }
+}
+
+template <bool AK, bool BKM, bool SLAB, int DIAG>
+__global__ void __launch_bounds__(NT, 1)
+gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
+               float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int M, int N, int R,
+               int splits) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = w >> 2, wl = w & 3;
+    // XCD-aware bijective remap: consecutive work ids run on one XCD (guide §5, T1)
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    const int tiles_n = N / BT;
+    const int ntiles = (M / BT) * tiles_n;
+    const int split = wid / ntiles, tile = wid % ntiles;
+    const int i0 = (tile / tiles_n) * BT, j0 = (tile % tiles_n) * BT;
+    const int nkt = R / BK;
+    const int kb = (int)((long)split * nkt / splits);
+    const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
+
+    int oa[4], ob[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = g * 1024 + (wl * 4 + j) * 64 + l;
+        oa[j] = src_off<AK>(e, (int)lda);
+        ob[j] = src_off<BKM>(e, (int)ldb);
+    }
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // prologue: K-tile 0, both halves (each group its own), then retire + barrier
+    {
+        const long k0 = (long)kb * BK;
+        dma_half(tile_ptr<AK>(A, lda, i0, k0), oa, smem, g, wl);
+        dma_half(tile_ptr<BKM>(B, ldb, j0, k0), ob, smem + OPB, g, wl);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+    }
+    if (g == 1 && DIAG != 4) bar();  // the stagger: group 1 runs one barrier interval behind group 0
+    for (int kt = 0; kt < nk; ++kt) {
+        char* cur = smem + (kt & 1) * STAGE;
+        char* nxt = smem + ((kt + 1) & 1) * STAGE;
+        const bool dma = kt + 1 < nk;
+        const long k1 = (long)(kb + kt + 1) * BK;
+        ktile<AK, BKM, DIAG>(cur, nxt, dma, tile_ptr<AK>(A, lda, i0, k1), tile_ptr<BKM>(B, ldb, j0, k1), oa, ob, g, wl, l,
+                       acc);
+    }
+    if (g == 0 && DIAG != 4) bar();
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    bar();  // every fragment read done: the LDS is free for the epilogue
+
+    // accumulator (ib, jb) register r of lane l: row i = 128 g + 16 ib + (l & 15), col j = 64 wl + 16 jb + 4 (l >> 4) + r
+    if constexpr (SLAB) {
+        float* sp = slab + (long)split * M * N;
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) {
+                const long i = i0 + 128 * g + 16 * ib + (l & 15);
+                const long j = j0 + 64 * wl + 16 * jb + 4 * (l >> 4);
+                *reinterpret_cast<f32x4*>(sp + i * N + j) = acc[ib][jb];
+            }
+    } else {
+        // stage bf16 tile as [256][512 B], 16-byte chunk c of row i at c ^ (i & 15)
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) {
+                const int i = 128 * g + 16 * ib + (l & 15);
+                const int j = 64 * wl + 16 * jb + 4 * (l >> 4);
+                const f32x4 v = acc[ib][jb];
+                const u16x4 p = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+                *reinterpret_cast<u16x4*>(smem + i * 512 + ((((j >> 3) ^ (i & 15))) << 4) + ((j & 7) << 1)) = p;
+            }
+        __syncthreads();
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+            const int i = q * 16 + (tid >> 5), c = tid & 31;
+            u16x8 v = *reinterpret_cast<const u16x8*>(smem + i * 512 + ((c ^ (i & 15)) << 4));
+            __bf16* cp = C + (long)(i0 + i) * ldc + j0 + c * 8;
+            if (beta != 0.f) {
+                const u16x8 o = *reinterpret_cast<const u16x8*>(cp);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + beta * bf2f(o[e]));
+            }
+            *reinterpret_cast<u16x8*>(cp) = v;
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------------------
+// Persistent form (the default).  A/B builds showed where the one-tile-per-workgroup kernel loses to the
+// library on short reductions (K = 768: 12 K-tiles per tile): every workgroup waits for its first K-tile with
+// an empty pipeline, then all CUs store their 128 KiB tiles at the same moment (an HBM-bound burst that no
+// MFMA work overlaps).  Here one workgroup per CU walks its work items (tile, k-split) with stride gridDim.x;
+// the K-tile prefetch runs on across item boundaries (the next tile's first K-tile is DMA'd during the last
+// K-tile of the current one), and each group stores its finished accumulators straight from registers
+// (8-byte bf16 / 16-byte fp32 stores, merged into lines by the L2) at the start of its next load section, so
+// the stores drain while the next tile computes.  The K loop is the ping-pong loop above, unchanged.
+// (A 5-slot ring of 32-deep half-stages was also tried: 15-25 % slower.)
+// Measured (benchmarks/gemm_pp_bench.py --quick): without its output stores this form runs the K = 768 forward
+// GEMMs at 1.19-1.37 PF/s (one-tile-per-workgroup: 0.85-1.04); with them, 0.74-0.89 -- the 8-byte stores of
+// 32 accumulators per lane cost more than the overlap gains, so BPE_GPP_VER=2 selects it and 1 (the
+// one-tile-per-workgroup kernel with the LDS-staged 512-byte-row epilogue) is the default.
+namespace pers {
+
+struct Item {
+    int i0, j0, kb, nk, split;
+};
+
+__device__ __forceinline__ Item item_info(int it, int tiles_n, int ntiles, int nkt, int splits) {
+    Item r;
+    r.split = it / ntiles;
+    const int tile = it - r.split * ntiles;
+    const int ti = tile / tiles_n;
+    r.i0 = ti * BT;
+    r.j0 = (tile - ti * tiles_n) * BT;
+    r.kb = r.split * nkt / splits;  // split < 64, nkt < 2^20: 32-bit products
+    r.nk = (r.split + 1) * nkt / splits - r.kb;
+    return r;
+}
+
+struct Out {
+    __bf16* C;
+    float* slab;
+    long ldc;
+    int M, N;
+    float beta;
+};
+
+// Store accumulator quadrant (m, n) of item `it` -- row i = 128 g + 16 a + (l & 15), columns
+// 64 wl + 16 b + 4 (l >> 4) + r of register r (a = 4 m + ib, b = 2 n + jb).  Addresses: one wave-uniform
+// 64-bit tile base + a 32-bit per-lane offset (few live VGPRs: this runs beside a full accumulator file).
+template <bool SLAB>
+__device__ __forceinline__ void store_q(const f32x4 (&acc)[8][4], int m, int n, const Item& it, const Out& o, int g,
+                                        int wl, int l) {
+    const int ld = SLAB ? o.N : (int)o.ldc;
+    const int lane = (128 * g + (l & 15)) * ld + 64 * wl + 4 * (l >> 4);
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+            const int a = 4 * m + ib, b = 2 * n + jb;
+            const int off = lane + a * 16 * ld + 16 * b;
+            f32x4 v = acc[a][b];
+            if constexpr (SLAB) {
+                float* base = o.slab + ((long)it.split * o.M + it.i0) * o.N + it.j0;
+                *reinterpret_cast<f32x4*>(base + off) = v;
+            } else {
+                __bf16* base = o.C + (long)it.i0 * o.ldc + it.j0;
+                // beta == 0 here: beta != 0 launches the one-tile-per-workgroup kernel
+                *reinterpret_cast<u16x4*>(base + off) = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+            }
+        }
+}
+
+// First K-tile of an item: MFMAs start from zero (no accumulator reset).  Phase 0 issues both halves of the next
+// K-tile's DMA FIRST and then stores the previous item's accumulators (32 stores per lane) before its MFMAs
+// overwrite them; phase 3 then waits for the DMA with vmcnt(32), leaving the 32 younger stores in flight
+// (vmcnt counts stores too, in issue order -- waiting on a DMA issued after the stores would wait for them).
+// (Spreading the stores over the four phases, one quadrant each, keeps old and new accumulators live together:
+// 60-150 spilled VGPRs.)
+__device__ __forceinline__ void mma_q_first(f32x4 (&acc)[8][4], const Frags& f, int m, int n) {
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+            f32x4& c = acc[4 * m + ib][2 * n + jb];
+            c = mfma16(f.b[jb][0], f.a[ib][0], f32x4{0.f, 0.f, 0.f, 0.f});
+            c = mfma16(f.b[jb][1], f.a[ib][1], c);
+        }
+}
+
+template <bool AK, bool BKM, bool SLAB>
+__device__ __forceinline__ void ktile_first(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
+                                            const __bf16* an, const __bf16* bn, const int (&oa)[4],
+                                            const int (&ob)[4], int g, int wl, int l, f32x4 (&acc)[8][4],
+                                            bool has_prev, const Item& prev, const Out& o) {
+    Frags f;
+    char* Ac = cur;
+    char* Bc = cur + OPB;
+    if (dma) {
+        dma_half(an, oa, nxt, g, wl);
+        dma_half(bn, ob, nxt + OPB, g, wl);
+    }
+    if (has_prev) {
+        store_q<SLAB>(acc, 0, 0, prev, o, g, wl, l);
+        __builtin_amdgcn_sched_barrier(0);
+        store_q<SLAB>(acc, 0, 1, prev, o, g, wl, l);
+        __builtin_amdgcn_sched_barrier(0);
+        store_q<SLAB>(acc, 1, 1, prev, o, g, wl, l);
+        __builtin_amdgcn_sched_barrier(0);
+        store_q<SLAB>(acc, 1, 0, prev, o, g, wl, l);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    load_a<AK, BKM>(f, Ac, g, 0, l);
+    load_b<AK, BKM>(f, Bc, wl, 0, l);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma_q_first(acc, f, 0, 0);
+    bar();
+    load_b<AK, BKM>(f, Bc, wl, 1, l);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma_q_first(acc, f, 0, 1);
+    bar();
+    load_a<AK, BKM>(f, Ac, g, 1, l);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma_q_first(acc, f, 1, 1);
+    bar();
+    load_b<AK, BKM>(f, Bc, wl, 0, l);
+    if (has_prev)
+        asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    bar();
+    mma_q_first(acc, f, 1, 0);
+    bar();
+}
+
+template <bool AK, bool BKM, bool SLAB>
+__global__ void __launch_bounds__(NT, 1)
+gemm_pp_pers_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
+                    float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int M, int N, int R,
+                    int splits) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = w >> 2, wl = w & 3;
+    const int G = gridDim.x;
+    // the workgroups of one XCD (blockIdx % 8) take consecutive work items in every round (T1)
+    const int wid = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);  // G % 8 == 0 (host)
+    const int tiles_n = N / BT;
+    const int ntiles = (M / BT) * tiles_n;
+    const int nitems = ntiles * splits;
+    const int nkt = R / BK;
+    if (wid >= nitems) return;  // wave-uniform: the whole workgroup
+    const Out o{C, slab, ldc, M, N, beta};
+
+    int oa[4], ob[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = g * 1024 + (wl * 4 + j) * 64 + l;
+        oa[j] = src_off<AK>(e, (int)lda);
+        ob[j] = src_off<BKM>(e, (int)ldb);
+    }
+    f32x4 acc[8][4];
+
+    int c = wid, st = 0;
+    Item ci = item_info(c, tiles_n, ntiles, nkt, splits);
+    Item prev = ci;
+    bool has_prev = false;
+    {
+        const long k0 = (long)ci.kb * BK;
+        dma_half(tile_ptr<AK>(A, lda, ci.i0, k0), oa, smem, g, wl);
+        dma_half(tile_ptr<BKM>(B, ldb, ci.j0, k0), ob, smem + OPB, g, wl);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+    }
+    if (g == 1) bar();  // the stagger
+    while (true) {
+        // the item's K-tiles; each prefetches its successor in this workgroup's sequence (across items)
+        const int nc = c + G;
+        const bool more = nc < nitems;
+        const Item ni = more ? item_info(nc, tiles_n, ntiles, nkt, splits) : ci;
+        for (int kt = 0; kt < ci.nk; ++kt) {
+            const bool last = kt + 1 == ci.nk;
+            const Item& di = last ? ni : ci;
+            const long k1 = (long)(di.kb + (last ? 0 : kt + 1)) * BK;
+            const bool dma = !last || more;
+            char* cur = smem + st * STAGE;
+            char* nxt = smem + (st ^ 1) * STAGE;
+            const __bf16* an = tile_ptr<AK>(A, lda, di.i0, k1);
+            const __bf16* bn = tile_ptr<BKM>(B, ldb, di.j0, k1);
+            if (kt == 0)
+                ktile_first<AK, BKM, SLAB>(cur, nxt, dma, an, bn, oa, ob, g, wl, l, acc, has_prev, prev, o);
+            else
+                ktile<AK, BKM, 0>(cur, nxt, dma, an, bn, oa, ob, g, wl, l, acc);
+            st ^= 1;
+        }
+        if (!more) break;
+        prev = ci;  // its tile is stored during the next item's first K-tile
+        has_prev = true;
+        c = nc;
+        ci = ni;
+    }
+    // the last item: all four quadrants
+    store_q<SLAB>(acc, 0, 0, ci, o, g, wl, l);
+    store_q<SLAB>(acc, 0, 1, ci, o, g, wl, l);
+    store_q<SLAB>(acc, 1, 1, ci, o, g, wl, l);
+    store_q<SLAB>(acc, 1, 0, ci, o, g, wl, l);
+    if (g == 0) bar();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+}  // namespace pers
+}  // namespace gpp
+}  // namespace bpe
+
+using namespace bpe::gpp;
+
+bool gemm_pp_shape_ok(int M, int N, int R, int splits) {
+    return M % BT == 0 && N % BT == 0 && R % BK == 0 && splits >= 1 && R / BK >= splits;
+}
+
+template <bool AK, bool BKM, bool SLAB, int DIAG>
+static void launch_pp1(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
+                      float beta, int M, int N, int R, int splits, hipStream_t s) {
+    static bool attr = false;  // > 64 KiB dynamic LDS must be opted into once per instantiation
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<AK, BKM, SLAB, DIAG>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        attr = true;
+    }
+    const int grid = (M / BT) * (N / BT) * splits;
+    gemm_pp_kernel<AK, BKM, SLAB, DIAG><<<grid, NT, LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits);
+}
+
+template <bool AK, bool BKM, bool SLAB>
+static void launch_pers(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
+                        float beta, int M, int N, int R, int splits, hipStream_t s) {
+    static bool attr = false;
+    static int cus = 256;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)pers::gemm_pp_pers_kernel<AK, BKM, SLAB>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        int dev = 0, n = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        if (n >= 8) cus = n / 8 * 8;
+        attr = true;
+    }
+    const int items = (M / BT) * (N / BT) * splits;
+    const int grid = items < cus ? (items + 7) / 8 * 8 : cus;
+    pers::gemm_pp_pers_kernel<AK, BKM, SLAB><<<grid, NT, LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N,
+                                                                          R, splits);
+}
+
+template <bool AK, bool BKM, bool SLAB>
+static void launch_pp(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
+                      float beta, int M, int N, int R, int splits, hipStream_t s) {
+#ifdef BPE_GPP_DIAG
+    static int diag = [] {
+        const char* e = getenv("BPE_GPP_DIAG");
+        return e ? atoi(e) : 0;
+    }();
+#else
+    constexpr int diag = 0;
+#endif
+    static int ver = [] {
+        const char* e = getenv("BPE_GPP_VER");
+        return e ? atoi(e) : 1;
+    }();
+    if (ver == 2 && (SLAB || beta == 0.f)) return launch_pers<AK, BKM, SLAB>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
+    switch (diag) {
+#ifdef BPE_GPP_DIAG
+        case 1: launch_pp1<AK, BKM, SLAB, 1>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
+        case 2: launch_pp1<AK, BKM, SLAB, 2>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
+        case 3: launch_pp1<AK, BKM, SLAB, 3>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
+        case 4: launch_pp1<AK, BKM, SLAB, 4>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
+#endif
+        default: launch_pp1<AK, BKM, SLAB, 0>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
+    }
+}
+
+void splitk_reduce(const float* slab, void* C, long ldc, float beta, int M, int N, int splits, hipStream_t s);
+
+void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
+                    float beta, int M, int N, int R, int splits, float* slab, hipStream_t s) {
+    const __bf16* a = (const __bf16*)A;
+    const __bf16* b = (const __bf16*)B;
+    __bf16* c = (__bf16*)C;
+#define L(AK, BKM, SL) launch_pp<AK, BKM, SL>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s)
+    if (splits > 1) {
+        if (a_kmajor) { if (b_kmajor) L(true, true, true); else L(true, false, true); }
+        else { if (b_kmajor) L(false, true, true); else L(false, false, true); }
+        splitk_reduce(slab, C, ldc, beta, M, N, splits, s);
+    } else {
+        if (a_kmajor) { if (b_kmajor) L(true, true, false); else L(true, false, false); }
+        else { if (b_kmajor) L(false, true, false); else L(false, false, false); }
+    }
+#undef L
+}

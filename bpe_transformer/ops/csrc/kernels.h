@@ -58,6 +58,13 @@ bool gemm_shape_ok(int Mo, int No, int R, int splits, int tile);
 void launch_gemm(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                  float beta, int Mo, int No, int R, int splits, float* slab, int tile, hipStream_t s);
 
+void splitk_reduce(const float* slab, void* C, long ldc, float beta, int M, int N, int splits, hipStream_t s);
+
+// gemm_pp.hip (8-wave ping-pong, 256 x 256 x 64 tiles, any operand layout)
+bool gemm_pp_shape_ok(int M, int N, int R, int splits);
+void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
+                    float beta, int M, int N, int R, int splits, float* slab, hipStream_t s);
+
 // rope.hip
 void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,
                  size_t R, int H, int D, int inverse, hipStream_t s);

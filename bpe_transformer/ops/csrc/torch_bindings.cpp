@@ -299,6 +299,32 @@ void gemm(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor
                 cur_stream());
 }
 
+// 8-wave ping-pong GEMM (256 x 256 x 64 tiles): same operand convention as gemm(); any layout pair.
+void gemm_pp(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor, at::Tensor C, double beta,
+             int64_t splits) {
+    check_cuda(C, "C");
+    TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
+                    C.scalar_type() == at::kBFloat16, "gemm_pp: bf16 operands required");
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
+                    C.stride(1) == 1, "gemm_pp: 2-D row-major operands required");
+    TORCH_CHECK(A.device() == C.device() && B.device() == C.device(), "gemm_pp: operands on different devices");
+    const int M = (int)C.size(0), N = (int)C.size(1);
+    const int R = (int)(a_kmajor ? A.size(1) : A.size(0));
+    TORCH_CHECK((a_kmajor ? A.size(0) : A.size(1)) == M, "gemm_pp: A / C shape mismatch");
+    TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == N && (b_kmajor ? B.size(1) : B.size(0)) == R,
+                "gemm_pp: B shape mismatch");
+    TORCH_CHECK(gemm_pp_shape_ok(M, N, R, (int)splits), "gemm_pp: M, N must be multiples of 256, R of 64 (>= splits)");
+    TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 && C.stride(0) % 8 == 0, "gemm_pp: 16-byte row alignment");
+    TORCH_CHECK((A.stride(0) * 256) < (1L << 31) && (B.stride(0) * 256) < (1L << 31),
+                "gemm_pp: leading dimension too large for 32-bit tile offsets");
+    DevGuard g(C.device());
+    at::Tensor slab;
+    if (splits > 1) slab = at::empty({splits, M, N}, C.options().dtype(at::kFloat));
+    launch_gemm_pp(a_kmajor, b_kmajor, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(),
+                   C.stride(0), (float)beta, M, N, R, (int)splits, splits > 1 ? slab.data_ptr<float>() : nullptr,
+                   cur_stream());
+}
+
 // ---------------------------------------------------------------- FP8 quantisation (delayed scaling)
 void cast_fp8(const at::Tensor& x, const at::Tensor& scale, at::Tensor out, at::Tensor amax_bits) {
     check_cuda(x, "x");
@@ -432,6 +458,7 @@ TORCH_LIBRARY(bpe_hip, m) {
           "float b2, float eps, float wd, float bc1, float bc2_sqrt, Tensor? gscale) -> ()");
     m.def("grad_norm(Tensor[] tensors, float max_norm) -> (Tensor, Tensor)");
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
+    m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
     m.def("update_scales(Tensor(a!) amax_bits, Tensor(b!) hist, Tensor(c!) scale, Tensor(d!) inv_scale, int pos, "
@@ -460,6 +487,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("grad_norm", &grad_norm);
     m.impl("scale_", &scale_);
     m.impl("gemm", &gemm);
+    m.impl("gemm_pp", &gemm_pp);
     m.impl("cast_fp8", &cast_fp8);
     m.impl("update_scales", &update_scales);
     m.impl("softmax_fwd", &softmax_fwd);

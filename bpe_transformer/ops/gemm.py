@@ -83,8 +83,33 @@ _AUTOTUNE = os.environ.get("BPE_GEMM_AUTOTUNE", "1") == "1"
 _route: dict[tuple[int, int, int], str] = {}
 
 
+def choose_splits_pp(n: int, k: int, t: int, cus: int = _CUS) -> int:
+    """Split count for the ping-pong kernel (256 x 256 x 64 tiles): fill whole waves of CUs, keep >= 4 K-tiles
+    per split, and charge the fp32 slab round trip."""
+    tiles = (n // 256) * (k // 256)
+    nk = t // 64
+    best, best_cost = 1, None
+    for s in range(1, 65):
+        if nk // s < 4:
+            break
+        waves = -(-tiles * s // cus)
+        cost = waves * (-(-nk // s)) * 1.6e-6 + (2 * s * n * k * 4 / 4.0e12 if s > 1 else 0.0)
+        if best_cost is None or cost < best_cost * 0.97:
+            best, best_cost = s, cost
+    return best
+
+
+def use_pp(n: int, k: int, t: int) -> bool:
+    return _PP and n % 256 == 0 and k % 256 == 0 and t % 64 == 0
+
+
+_PP = os.environ.get("BPE_GEMM_PP", "1") == "1"
+
+
 def _candidates(n: int, k: int, t: int) -> list[str]:
     c = []
+    if use_pp(n, k, t):
+        c.append("pp")
     if use_tile256(n, k, t):
         c.append("hip256")
     elif supported(n, k, t):
@@ -95,7 +120,9 @@ def _candidates(n: int, k: int, t: int) -> list[str]:
 def _run(route: str, g: Tensor, dy: Tensor, x: Tensor) -> None:
     n, k = g.shape
     t = dy.shape[0]
-    if route == "hip256":
+    if route == "pp":
+        ops().gemm_pp(dy, False, x, False, g, 1.0, choose_splits_pp(n, k, t))
+    elif route == "hip256":
         ops().gemm(dy, False, x, False, g, 1.0, choose_splits_256(n, k, t), 256)
     elif route == "hip128":
         ops().gemm(dy, False, x, False, g, 1.0, choose_splits(n, k, t), 128)

@@ -249,6 +249,36 @@ def test_gemm_layouts(gpu_device, a_k, b_k, splits, tile):
     assert rel(C.cpu(), ref.cpu()) < 1e-2
 
 
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_pp_exact(gpu_device, a_k, b_k, splits):
+    """Ping-pong GEMM on small-integer operands: every output is exact, so any layout/index slip shows."""
+    torch.manual_seed(1)
+    M, N, R = 512, 768, 448
+    A = torch.randint(-1, 2, (M, R), device=gpu_device).to(torch.bfloat16)
+    B = torch.randint(-1, 2, (N, R), device=gpu_device).to(torch.bfloat16)
+    Am = A if a_k else A.t().contiguous()
+    Bm = B if b_k else B.t().contiguous()
+    C = torch.randint(-3, 4, (M, N), device=gpu_device).to(torch.bfloat16)
+    ref = C.float() * 2.0 + A.float() @ B.float().t()
+    torch.ops.bpe_hip.gemm_pp(Am, a_k, Bm, b_k, C, 2.0, splits)
+    assert torch.equal(C.float().cpu(), ref.cpu())
+
+
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
+def test_gemm_pp_random(gpu_device, a_k, b_k):
+    torch.manual_seed(0)
+    M, N, R = 1024, 512, 1536
+    A = torch.randn(M, R, device=gpu_device, dtype=torch.bfloat16)
+    B = torch.randn(N, R, device=gpu_device, dtype=torch.bfloat16)
+    Am = A if a_k else A.t().contiguous()
+    Bm = B if b_k else B.t().contiguous()
+    C = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
+    torch.ops.bpe_hip.gemm_pp(Am, a_k, Bm, b_k, C, 0.0, 1 if a_k else 4)
+    ref = A.float() @ B.float().t()
+    assert rel(C.cpu(), ref.cpu()) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(2304, 768, 8192), (768, 768, 8192), (11264, 2048, 2048), (2048, 5632, 4096),
                                    (50432, 256, 4096), (768, 768, 65536)])
 def test_weight_grad_shapes(gpu_device, shape):
