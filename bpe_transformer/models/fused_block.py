@@ -14,6 +14,8 @@ forward::
     y = xm + a @ W2^T                 hipBLASLt addmm
 
 backward: the mirror image, with
+  * the SwiGLU backward fused into the epilogue of the dY @ W2 GEMM (our
+    ping-pong MFMA kernel): the gate gradient da never goes to HBM;
   * weight gradients ACCUMULATED IN PLACE into the flat gradient buffer
     (``param.main_grad``, set by the training engine) by ``addmm_`` with
     beta = 1 -- no temporary dW, no AccumulateGrad add kernels;
@@ -32,6 +34,7 @@ ordinary per-parameter gradients.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch import Tensor
@@ -57,6 +60,15 @@ def _adjacent_view(ts: list[Tensor]) -> Tensor | None:
 def _cat_weights(ts: list[Tensor]) -> Tensor:
     v = _adjacent_view([t.detach() for t in ts])
     return v if v is not None else torch.cat([t.detach() for t in ts], 0)
+
+
+_FUSE_SWIGLU_BWD = os.environ.get("BPE_FUSE_SWIGLU_BWD", "1") == "1"
+
+
+def _fuse_swiglu_bwd(dy: Tensor, w2: Tensor, gu: Tensor) -> bool:
+    """The fused dX-GEMM + SwiGLU-backward kernel covers tokens and d_ff in multiples of 256, d_model of 64."""
+    return (_FUSE_SWIGLU_BWD and dy.shape[0] % 256 == 0 and w2.shape[1] % 256 == 0 and dy.shape[1] % 64 == 0
+            and gu.is_contiguous() and dy.stride(1) == 1 and w2.stride(1) == 1)
 
 
 def _notify(p: Tensor) -> None:
@@ -158,8 +170,12 @@ class FusedBlockFn(torch.autograd.Function):
 
         # ---- FFN
         acc_weight([w2], dy, a)
-        da = dx(dy, [w2], 3)
-        dgu = hip().swiglu_bwd(da, gu)
+        if w8s is None and _fuse_swiglu_bwd(dy, w2, gu):
+            # da = dy @ W2 with the SwiGLU backward in the GEMM epilogue (csrc/gemm_pp.hip): da never reaches HBM
+            dgu = hip().gemm_swiglu_bwd(dy, w2.detach(), gu)
+        else:
+            da = dx(dy, [w2], 3)
+            dgu = hip().swiglu_bwd(da, gu)
         acc_weight([w1, w3], dgu, h2)
         dh2 = dx(dgu, [w1, w3], 2)
         dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dxm_out)

@@ -189,11 +189,23 @@ __device__ __forceinline__ void ktile(char* __restrict__ cur, char* __restrict__
     }
 }
 
-template <bool AK, bool BKM, bool SLAB, int DIAG>
+// Fused epilogues of the one-tile-per-workgroup kernel.  EPI_SWIGLU_BWD: the GEMM result is da = dY W2 (the
+// gradient of a = silu(g) * u); instead of storing da the epilogue reads g and u from gu = [g | u] ([M][2F])
+// and writes dgu = [dg | du] -- the SwiGLU backward without the da round trip through HBM.  Same math and
+// rounding as swiglu_bwd_kernel (da rounded to bf16 first).
+enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1 };
+struct Epi {
+    const __bf16* gu;
+    __bf16* dgu;
+    long ld;  // row stride of gu / dgu (elements)
+    int F;
+};
+
+template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE>
 __global__ void __launch_bounds__(NT, 1)
 gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
                float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int M, int N, int R,
-               int splits) {
+               int splits, Epi ep = Epi{}) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -273,6 +285,22 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
         for (int q = 0; q < 16; ++q) {
             const int i = q * 16 + (tid >> 5), c = tid & 31;
             u16x8 v = *reinterpret_cast<const u16x8*>(smem + i * 512 + ((c ^ (i & 15)) << 4));
+            if constexpr (EPI == EPI_SWIGLU_BWD) {
+                const long ro = (long)(i0 + i) * ep.ld + j0 + c * 8;
+                const u16x8 gv = *reinterpret_cast<const u16x8*>(ep.gu + ro);
+                const u16x8 uv = *reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F);
+                u16x8 dg, du;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float gg = bf2f(gv[e]), uu = bf2f(uv[e]), d = bf2f(v[e]);
+                    const float sg = 1.f / (1.f + __expf(-gg));
+                    du[e] = f2bf(d * (gg * sg));
+                    dg[e] = f2bf(d * uu * sg * (1.f + gg * (1.f - sg)));
+                }
+                *reinterpret_cast<u16x8*>(ep.dgu + ro) = dg;
+                *reinterpret_cast<u16x8*>(ep.dgu + ro + ep.F) = du;
+                continue;
+            }
             __bf16* cp = C + (long)(i0 + i) * ldc + j0 + c * 8;
             if (beta != 0.f) {
                 const u16x8 o = *reinterpret_cast<const u16x8*>(cp);
@@ -496,6 +524,21 @@ gemm_pp_pers_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __rest
 }  // namespace bpe
 
 using namespace bpe::gpp;
+
+// dgu = swiglu_bwd(dY . W2, gu): A = dY [M][R] (K-major), B = W2 [R][F] (MN-major)
+void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,
+                               long ldg, int M, int F, int R, hipStream_t s) {
+    static bool attr = false;
+    auto* k = &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD>;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        attr = true;
+    }
+    const int grid = (M / BT) * (F / BT);
+    Epi ep{(const __bf16*)gu, (__bf16*)dgu, ldg, F};
+    k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)dY, ldy, (const __bf16*)W2, ldw, nullptr, nullptr, 0, 0.f, M, F, R,
+                                  1, ep);
+}
 
 bool gemm_pp_shape_ok(int M, int N, int R, int splits) {
     return M % BT == 0 && N % BT == 0 && R % BK == 0 && splits >= 1 && R / BK >= splits;

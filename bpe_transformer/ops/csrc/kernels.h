@@ -65,6 +65,9 @@ bool gemm_pp_shape_ok(int M, int N, int R, int splits);
 void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                     float beta, int M, int N, int R, int splits, float* slab, hipStream_t s);
 
+void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,
+                               long ldg, int M, int F, int R, hipStream_t s);
+
 // rope.hip
 void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,
                  size_t R, int H, int D, int inverse, hipStream_t s);

@@ -325,6 +325,24 @@ void gemm_pp(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kma
                    cur_stream());
 }
 
+// dgu = swiglu_bwd(dy @ w2, gu) with the SwiGLU backward in the GEMM epilogue (da never reaches HBM)
+at::Tensor gemm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& w2, const at::Tensor& gu) {
+    check_cuda(gu, "gu");
+    TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && w2.scalar_type() == at::kBFloat16 &&
+                    gu.scalar_type() == at::kBFloat16, "gemm_swiglu_bwd: bf16 tensors required");
+    TORCH_CHECK(dy.dim() == 2 && w2.dim() == 2 && gu.dim() == 2 && dy.stride(1) == 1 && w2.stride(1) == 1 &&
+                    gu.is_contiguous(), "gemm_swiglu_bwd: row-major 2-D tensors required");
+    const int M = (int)dy.size(0), R = (int)dy.size(1), F = (int)w2.size(1);
+    TORCH_CHECK(w2.size(0) == R && gu.size(0) == M && gu.size(1) == 2 * F, "gemm_swiglu_bwd: shape mismatch");
+    TORCH_CHECK(M % 256 == 0 && F % 256 == 0 && R % 64 == 0, "gemm_swiglu_bwd: M, F multiples of 256, d of 64");
+    TORCH_CHECK(dy.stride(0) % 8 == 0 && w2.stride(0) % 8 == 0, "gemm_swiglu_bwd: 16-byte row alignment");
+    DevGuard g(gu.device());
+    auto dgu = at::empty_like(gu);
+    launch_gemm_pp_swiglu_bwd(dy.data_ptr(), dy.stride(0), w2.data_ptr(), w2.stride(0), gu.data_ptr(),
+                              dgu.data_ptr(), 2 * (long)F, M, F, R, cur_stream());
+    return dgu;
+}
+
 // ---------------------------------------------------------------- FP8 quantisation (delayed scaling)
 void cast_fp8(const at::Tensor& x, const at::Tensor& scale, at::Tensor out, at::Tensor amax_bits) {
     check_cuda(x, "x");
@@ -458,6 +476,7 @@ TORCH_LIBRARY(bpe_hip, m) {
           "float b2, float eps, float wd, float bc1, float bc2_sqrt, Tensor? gscale) -> ()");
     m.def("grad_norm(Tensor[] tensors, float max_norm) -> (Tensor, Tensor)");
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
+    m.def("gemm_swiglu_bwd(Tensor dy, Tensor w2, Tensor gu) -> Tensor");
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
@@ -488,6 +507,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("scale_", &scale_);
     m.impl("gemm", &gemm);
     m.impl("gemm_pp", &gemm_pp);
+    m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
     m.impl("cast_fp8", &cast_fp8);
     m.impl("update_scales", &update_scales);
     m.impl("softmax_fwd", &softmax_fwd);

@@ -249,6 +249,23 @@ def test_gemm_layouts(gpu_device, a_k, b_k, splits, tile):
     assert rel(C.cpu(), ref.cpu()) < 1e-2
 
 
+def test_gemm_swiglu_bwd(gpu_device):
+    """dY @ W2 with the SwiGLU backward in the epilogue vs the fp32 oracle of the same two steps."""
+    torch.manual_seed(2)
+    M, d, F = 512, 192, 768
+    dy = torch.randn(M, d, device=gpu_device, dtype=torch.bfloat16)
+    w2 = (0.1 * torch.randn(d, F, device=gpu_device)).to(torch.bfloat16)
+    gu = torch.randn(M, 2 * F, device=gpu_device, dtype=torch.bfloat16)
+    dgu = torch.ops.bpe_hip.gemm_swiglu_bwd(dy, w2, gu)
+    da = (dy.float() @ w2.float()).to(torch.bfloat16).float()  # the kernel rounds da to bf16 like the unfused path
+    g, u = gu.float()[:, :F], gu.float()[:, F:]
+    s = torch.sigmoid(g)
+    ref = torch.cat([da * u * s * (1 + g * (1 - s)), da * g * s], 1)
+    assert rel(dgu.cpu(), ref.cpu()) < 2e-2
+    unfused = torch.ops.bpe_hip.swiglu_bwd((dy @ w2).contiguous(), gu)
+    assert rel(dgu.cpu(), unfused.cpu()) < 2e-2
+
+
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("splits", [1, 3])
 def test_gemm_pp_exact(gpu_device, a_k, b_k, splits):
