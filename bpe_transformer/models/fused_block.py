@@ -25,7 +25,9 @@ backward: the mirror image, with
   * both residual-gradient additions folded into the RMSNorm backward kernel;
   * a data-parallel "gradient ready" notification per parameter right after
     its gradient lands, so bucketed all-reduces start while the rest of the
-    backward runs.
+    backward runs;
+  * the weight-gradient GEMMs issued on a side stream (ops/streams.py), so
+    they overlap the serial input-gradient chain.
 
 Without ``main_grad`` (e.g. a plain module, tests) the same function returns
 ordinary per-parameter gradients.
@@ -39,6 +41,7 @@ import os
 import torch
 from torch import Tensor
 
+from ..ops import streams
 from ..ops._ext import ops as hip
 from ..ops.gemm import accumulate_weight_grad
 
@@ -136,19 +139,26 @@ class FusedBlockFn(torch.autograd.Function):
         grads: dict[int, Tensor] = {}
 
         def acc_weight(ps: list[Tensor], g_out: Tensor, x_in: Tensor) -> None:
-            """dW = g_out^T x_in for the row-stacked weights ``ps``."""
+            """dW = g_out^T x_in for the row-stacked weights ``ps`` (on the side stream: ops/streams.py)."""
             if main:
-                view = _adjacent_view([p.main_grad for p in ps])
-                if view is not None:
-                    accumulate_weight_grad(view, g_out, x_in)
-                else:
-                    off = 0
+                def run():
+                    view = _adjacent_view([p.main_grad for p in ps])
+                    if view is not None:
+                        accumulate_weight_grad(view, g_out, x_in)
+                    else:
+                        off = 0
+                        for p in ps:
+                            n = p.shape[0]
+                            accumulate_weight_grad(p.main_grad, g_out[:, off : off + n], x_in)
+                            off += n
                     for p in ps:
-                        n = p.shape[0]
-                        accumulate_weight_grad(p.main_grad, g_out[:, off : off + n], x_in)
-                        off += n
-                for p in ps:
-                    _notify(p)
+                        _notify(p)
+
+                if streams.enabled(g_out):
+                    with streams.after_compute(g_out.device, keep=(g_out, x_in)):
+                        run()
+                else:
+                    run()
             else:
                 dw = torch.matmul(g_out.t(), x_in)
                 off = 0

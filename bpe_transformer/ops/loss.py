@@ -50,12 +50,20 @@ class _LMHeadCEFn(torch.autograd.Function):
             return dh, torch.matmul(dlogits.t(), hs)[: ctx.w_param.shape[0]], None, None
         if mg is not None:
             # weight gradient accumulated in place into the flat gradient buffer (no temporary, no grad add)
+            from . import streams
             from .gemm import accumulate_weight_grad
 
-            accumulate_weight_grad(mg, dlogits, hs)
-            cb = getattr(ctx.w_param, "_bpe_grad_ready", None)
-            if cb is not None:
-                cb(ctx.w_param)
+            def run():
+                accumulate_weight_grad(mg, dlogits, hs)
+                cb = getattr(ctx.w_param, "_bpe_grad_ready", None)
+                if cb is not None:
+                    cb(ctx.w_param)
+
+            if streams.enabled(hs):  # overlaps the blocks' backward (side stream, ordered: ops/streams.py)
+                with streams.after_compute(hs.device, keep=(dlogits, hs)):
+                    run()
+            else:
+                run()
             return dh, None, None, None
         return dh, torch.matmul(dlogits.t(), hs), None, None
 

@@ -1,0 +1,67 @@
+"""A side HIP stream for weight-gradient GEMMs, overlapped with the input-gradient chain of backward.
+
+In a block's backward the input-gradient chain (dX GEMMs, attention backward, norm backward) is serial, but
+each weight gradient dW = dY^T X only needs tensors that already exist when it is issued.  Issuing the dW
+GEMMs on a second stream lets the GPU run them beside the next kernels of the dX chain (their tails, the
+attention backward's partially occupied waves, the memory-bound norm/activation kernels) instead of in
+series with them.
+
+Ordering rules (every one enforced here, none relies on timing):
+  * a dW launch first makes the side stream wait for everything issued so far on the compute stream
+    (its inputs were produced there);
+  * tensors read on the side stream are ``record_stream``-ed so the caching allocator cannot hand their
+    memory to the compute stream while the side stream still reads them;
+  * gradient-ready notifications for those parameters (which may launch a bucketed all-reduce) are issued
+    from the side stream, and a bucket's collective is always launched from the side stream after it waited
+    for the compute stream -- so the all-reduce is ordered after BOTH streams' writes to its slice;
+  * :func:`join` (called by the training engine after backward) makes the compute stream wait for the side
+    stream before the optimizer reads the gradients and before the next step zeroes them.
+
+``BPE_DW_STREAM=0`` runs everything on the compute stream; graph capture also falls back to it.
+"""
+
+from __future__ import annotations
+
+import os
+from contextlib import contextmanager
+
+import torch
+
+_ENABLED = os.environ.get("BPE_DW_STREAM", "1") == "1"
+_side: dict[int, torch.cuda.Stream] = {}
+
+
+def enabled(t: torch.Tensor) -> bool:
+    return _ENABLED and t.is_cuda and not torch.cuda.is_current_stream_capturing()
+
+
+def side_stream(device: torch.device) -> torch.cuda.Stream:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _side.get(idx)
+    if s is None:
+        s = _side[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+@contextmanager
+def after_compute(device: torch.device, keep: tuple[torch.Tensor, ...] = ()):
+    """Run the body on the side stream, ordered after all work issued so far on the current stream."""
+    main = torch.cuda.current_stream(device)
+    side = side_stream(device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        yield side
+    for t in keep:
+        t.record_stream(side)
+
+
+def join(device: torch.device | None = None) -> None:
+    """Make the current stream wait for every side-stream launch so far."""
+    if not _side:
+        return
+    if device is None:
+        for idx, s in _side.items():
+            if idx == torch.cuda.current_device():
+                torch.cuda.current_stream().wait_stream(s)
+        return
+    torch.cuda.current_stream(device).wait_stream(side_stream(device))

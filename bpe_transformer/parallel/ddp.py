@@ -26,6 +26,7 @@ from contextlib import contextmanager
 import torch
 import torch.distributed as dist
 
+from ..ops import streams
 from ..optim.flat import FlatParameters
 
 
@@ -84,10 +85,14 @@ class BucketedAllReduce:
             return
         s, e = self.buckets[b]
         view = self.flat.grad[s:e]
-        if self.average and self._use_avg:
-            self._works[b] = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
+        op = dist.ReduceOp.AVG if (self.average and self._use_avg) else dist.ReduceOp.SUM
+        if view.is_cuda and streams.enabled(view):
+            # weight gradients may be written on the side stream (ops/streams.py): issue the collective from
+            # there, after it waited for the compute stream, so it is ordered after both streams' writes
+            with streams.after_compute(view.device):
+                self._works[b] = dist.all_reduce(view, op=op, group=self.pg, async_op=True)
         else:
-            self._works[b] = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            self._works[b] = dist.all_reduce(view, op=op, group=self.pg, async_op=True)
 
     # -- step API ----------------------------------------------------------
     def start(self) -> None:
