@@ -43,11 +43,22 @@ def side_stream(device: torch.device) -> torch.cuda.Stream:
     return s
 
 
+_compute: dict[int, torch.cuda.Stream] = {}
+
+
 @contextmanager
 def after_compute(device: torch.device, keep: tuple[torch.Tensor, ...] = ()):
-    """Run the body on the side stream, ordered after all work issued so far on the current stream."""
-    main = torch.cuda.current_stream(device)
+    """Run the body on the side stream, ordered after all work issued so far on the compute stream.
+
+    Entered from the side stream itself (a gradient notification issued there launching a bucket's
+    collective), the compute stream is the one the outermost entry came from, not the side stream."""
     side = side_stream(device)
+    idx = side.device_index
+    cur = torch.cuda.current_stream(device)
+    if cur == side:
+        main = _compute.get(idx, torch.cuda.default_stream(device))
+    else:
+        main = _compute[idx] = cur
     side.wait_stream(main)
     with torch.cuda.stream(side):
         yield side

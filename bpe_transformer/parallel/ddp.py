@@ -63,6 +63,7 @@ class BucketedAllReduce:
                 self.bucket_of[id(slots[i].param)] = b
         self._members = [len(m) for m in members]
         self._pending = list(self._members)
+        self._seen: set[int] = set()
         self._works: list = [None] * len(self.buckets)
         self._hooks = []
         if overlap and self.world > 1:
@@ -73,8 +74,13 @@ class BucketedAllReduce:
 
     # -- hooks -------------------------------------------------------------
     def _on_grad(self, p: torch.Tensor) -> None:
-        if not self.enabled:
+        # Idempotent per backward: a parameter whose gradient a fused kernel writes into main_grad notifies
+        # right after that write, and its AccumulateGrad node still runs afterwards (with an undefined grad)
+        # and fires the post-accumulate hook a second time -- counting both would launch the bucket's
+        # collective before its other members' gradients exist.
+        if not self.enabled or id(p) in self._seen:
             return
+        self._seen.add(id(p))
         b = self.bucket_of[id(p)]
         self._pending[b] -= 1
         if self._pending[b] == 0:
@@ -98,6 +104,7 @@ class BucketedAllReduce:
     def start(self) -> None:
         """Call before each backward that should all-reduce."""
         self._pending = list(self._members)
+        self._seen = set()
         self._works = [None] * len(self.buckets)
 
     def finish(self) -> None:

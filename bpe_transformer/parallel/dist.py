@@ -59,7 +59,7 @@ def init_distributed(device: str | None = None, backend: str | None = None, time
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kwargs = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_cuda:
+        if use_cuda and backend == "nccl":
             kwargs["device_id"] = dev
         dist.init_process_group(**kwargs)
     return DistInfo(rank, world, local, dev, backend)

@@ -99,3 +99,26 @@ def test_launcher_spawns_ranks(tmp_path):
     launch(_launched, 2, str(tmp_path))
     for r in range(2):
         assert (tmp_path / f"rank{r}.txt").read_text() == "2 3.0 127.0.0.1"
+
+
+def test_bucket_notifications_idempotent():
+    """A parameter notified twice in one backward (fused main_grad write + its AccumulateGrad hook) must
+    count once: the bucket's collective may only start when every member's gradient exists."""
+    from bpe_transformer.optim.flat import FlatParameters
+    from bpe_transformer.parallel.ddp import BucketedAllReduce
+
+    flat = FlatParameters.from_module(_model())
+    ar = BucketedAllReduce.__new__(BucketedAllReduce)
+    BucketedAllReduce.__init__(ar, flat, bucket_mb=1e9, overlap=False)  # world 1: no hooks, one bucket
+    launched = []
+    ar._launch = lambda b: launched.append(b)
+    ar.start()
+    params = [s.param for s in flat.slots]
+    for p in params[:-1]:
+        ar._on_grad(p)
+        ar._on_grad(p)  # the duplicate must not count
+    assert launched == []
+    ar._on_grad(params[-1])
+    assert launched == [0]
+    ar.start()
+    assert ar._seen == set() and ar._pending == ar._members
