@@ -125,7 +125,8 @@ def main() -> int:
     value = tokens / dt
     flops_tok = cfg.train_flops_per_token(args.seq)
     out = {
-        "metric": METRIC,
+        # the headline metric names the GPT-2-small config; other models report under their own name
+        "metric": METRIC if args.model == "gpt2-small" else f"training tokens/sec (whole node), {args.model}",
         "value": round(value, 1),
         "unit": "tokens/s",
         "n_gpus": n,
