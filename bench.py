@@ -151,6 +151,9 @@ def main() -> int:
         "gemm_tuning": tuning,
     }
     if info.is_main:
+        from bpe_transformer.ops import gemm as _gemm
+
+        print(f"dW GEMM routes: {_gemm._route}", file=sys.stderr)
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

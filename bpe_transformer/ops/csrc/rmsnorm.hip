@@ -173,6 +173,115 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ 
     }
 }
 
+// Wide rows (N / V >= 256, e.g. d_model 2048 in bf16): the 4 waves of a block share each row -- thread t owns
+// vectors t + 256 c -- and the block processes RPI rows at a time, so every thread keeps only C2 (usually 1)
+// vectors per row in registers.  The one-wave-per-row kernel above needs C = 4 chunks per lane there (182
+// VGPRs, 2 waves per SIMD, one row's loads in flight per wave: ~1.5 TB/s); this one runs at high occupancy
+// with RPI rows of loads in flight per thread.  Per-row dot products: wave sums, then the 4 waves through LDS.
+template <typename T> struct RawV;
+template <> struct RawV<__bf16> {
+    typedef u16x8 type;
+    static __device__ __forceinline__ float get(const u16x8& r, int j) { return bf2f(r[j]); }
+};
+template <> struct RawV<float> {
+    typedef f32x4 type;
+    static __device__ __forceinline__ float get(const f32x4& r, int j) { return r[j]; }
+};
+
+template <typename T, int C2, int RPI>
+__global__ void __launch_bounds__(256) rmsnorm_bwd_wide_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               const T* __restrict__ w,
+                                                               const float* __restrict__ rstd, T* __restrict__ dx,
+                                                               float* __restrict__ dw_partial,
+                                                               const T* __restrict__ dres, int M, int N) {
+    constexpr int V = Vec<T>::N;
+    typedef typename RawV<T>::type R;  // rows stay in registers as raw 16-byte vectors (few VGPRs)
+    __shared__ float red[2][RPI][4];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nvec = N / V;
+    float dwacc[C2][V], wv[C2][V];
+#pragma unroll
+    for (int c = 0; c < C2; ++c) {
+        const int i = tid + 256 * c;
+#pragma unroll
+        for (int j = 0; j < V; ++j) { dwacc[c][j] = 0.f; wv[c][j] = 0.f; }
+        if (i < nvec) {
+            Vec<T> g;
+            g.load(w + i * V);
+#pragma unroll
+            for (int j = 0; j < V; ++j) wv[c][j] = g.v[j];
+        }
+    }
+    int par = 0;
+    for (int r0 = blockIdx.x * RPI; r0 < M; r0 += gridDim.x * RPI, par ^= 1) {
+        R xr[RPI][C2], gr[RPI][C2];
+        float dot[RPI], rr[RPI];
+#pragma unroll
+        for (int k = 0; k < RPI; ++k) {
+            const int row = r0 + k;
+            const bool ok = row < M;
+            rr[k] = ok ? rstd[row] : 0.f;
+#pragma unroll
+            for (int c = 0; c < C2; ++c) {
+                const int i = tid + 256 * c;
+                if (ok && i < nvec) {
+                    xr[k][c] = *reinterpret_cast<const R*>(x + (size_t)row * N + i * V);
+                    gr[k][c] = *reinterpret_cast<const R*>(dy + (size_t)row * N + i * V);
+                } else {
+                    xr[k][c] = R{};
+                    gr[k][c] = R{};
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < RPI; ++k) {
+            dot[k] = 0.f;
+#pragma unroll
+            for (int c = 0; c < C2; ++c)
+#pragma unroll
+                for (int j = 0; j < V; ++j)
+                    dot[k] += RawV<T>::get(gr[k][c], j) * wv[c][j] * (RawV<T>::get(xr[k][c], j) * rr[k]);
+            dot[k] = wave_sum(dot[k]);
+            if (lane == 0) red[par][k][wid] = dot[k];
+        }
+        __syncthreads();  // double-buffered red[]: one barrier per row group
+#pragma unroll
+        for (int k = 0; k < RPI; ++k) {
+            const int row = r0 + k;
+            const float dk = (red[par][k][0] + red[par][k][1] + red[par][k][2] + red[par][k][3]) / (float)N;
+            if (row >= M) continue;
+#pragma unroll
+            for (int c = 0; c < C2; ++c) {
+                const int i = tid + 256 * c;
+                if (i < nvec) {
+                    Vec<T> o;
+#pragma unroll
+                    for (int j = 0; j < V; ++j) {
+                        const float xh = RawV<T>::get(xr[k][c], j) * rr[k], g = RawV<T>::get(gr[k][c], j);
+                        o.v[j] = rr[k] * (g * wv[c][j] - xh * dk);
+                        dwacc[c][j] += g * xh;
+                    }
+                    if (dres) {
+                        Vec<T> q;
+                        q.load(dres + (size_t)row * N + i * V);
+#pragma unroll
+                        for (int j = 0; j < V; ++j) o.v[j] += q.v[j];
+                    }
+                    o.store(dx + (size_t)row * N + i * V);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C2; ++c) {
+        const int i = tid + 256 * c;
+        if (i < nvec) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) dw_partial[(size_t)blockIdx.x * N + i * V + j] = dwacc[c][j];
+        }
+    }
+}
+
 // Column sum of the per-block partials [rows, N] -> dw [N]: 16 waves per block,
 // lane = column (coalesced 256-B rows), waves split the rows, fixed-order LDS
 // combine (deterministic).
@@ -216,6 +325,15 @@ template <typename T>
 static void rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* rstd, T* dx, float* partial,
                              const T* dres, int grid, int M, int N, hipStream_t s) {
     constexpr int V = Vec<T>::N;
+    if (N / V >= 256 && (N / V) % 256 == 0 && N / V <= 1024) {
+        switch (N / V / 256) {
+            case 1: rmsnorm_bwd_wide_kernel<T, 1, 2><<<grid, 256, 0, s>>>(dy, x, w, rstd, dx, partial, dres, M, N); break;
+            case 2: rmsnorm_bwd_wide_kernel<T, 2, 1><<<grid, 256, 0, s>>>(dy, x, w, rstd, dx, partial, dres, M, N); break;
+            case 3: rmsnorm_bwd_wide_kernel<T, 3, 1><<<grid, 256, 0, s>>>(dy, x, w, rstd, dx, partial, dres, M, N); break;
+            default: rmsnorm_bwd_wide_kernel<T, 4, 1><<<grid, 256, 0, s>>>(dy, x, w, rstd, dx, partial, dres, M, N); break;
+        }
+        return;
+    }
     const int chunks = (N / V + 63) / 64;
     const size_t lds = (size_t)4 * N * sizeof(float);
 #define RMS_CASE(CC)                                                                                    \

@@ -84,7 +84,9 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     auto dyc = dy.contiguous();
     const int N = (int)x.size(-1);
     const int M = (int)(x.numel() / N);
-    TORCH_CHECK(N <= 8 * 64 * vec_elems(x), "rmsnorm bwd: hidden size too large");
+    const int nv = N / vec_elems(x);
+    TORCH_CHECK(N <= 8 * 64 * vec_elems(x) || (N % vec_elems(x) == 0 && nv % 256 == 0 && nv <= 1024),
+                "rmsnorm bwd: hidden size too large");
     TORCH_CHECK(dyc.scalar_type() == x.scalar_type(), "rmsnorm bwd: dtype mismatch");
     DevGuard g(x.device());
     auto dx = at::empty_like(x);

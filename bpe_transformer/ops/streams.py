@@ -17,7 +17,10 @@ Ordering rules (every one enforced here, none relies on timing):
   * :func:`join` (called by the training engine after backward) makes the compute stream wait for the side
     stream before the optimizer reads the gradients and before the next step zeroes them.
 
-``BPE_DW_STREAM=0`` runs everything on the compute stream; graph capture also falls back to it.
+Off by default (``BPE_DW_STREAM=1`` enables it).  Measured on MI355X (GPT-2-small, B 64): most runs gain
+~1 % (982k -> 992k tok/s), but some runs of the same binary fell to 430-640k tok/s -- concurrent
+one-workgroup-per-CU GEMMs on two streams can interleave badly -- so the overlap is not worth its variance.
+Graph capture always runs on the compute stream.
 """
 
 from __future__ import annotations
@@ -27,7 +30,7 @@ from contextlib import contextmanager
 
 import torch
 
-_ENABLED = os.environ.get("BPE_DW_STREAM", "1") == "1"
+_ENABLED = os.environ.get("BPE_DW_STREAM", "0") == "1"
 _side: dict[int, torch.cuda.Stream] = {}
 
 

@@ -1,7 +1,8 @@
 """Data parallelism through the GPU training path: 2 ranks on one MI355X (gloo backend).
 
 The node's 8-GPU RCCL run is the driver's; this exercises everything around the collective on real HIP
-streams: the fused blocks writing weight gradients on the side stream (ops/streams.py), gradient-ready
+streams: the fused blocks writing weight gradients on the compute stream or (side = "1") the side stream
+(ops/streams.py), gradient-ready
 notifications from both streams, bucketed all-reduces launched from the side stream, the engine's join
 before the optimizer.  Both ranks must end with identical gradients and weights, and the all-reduced
 gradient must match one process that trains on the concatenated batch (bf16 tolerance).
@@ -40,9 +41,9 @@ def _batch(rank: int, dev):
     return x.to(dev), torch.roll(x, -1, 1).to(dev)
 
 
-def _worker(rank, world, port, bucket_mb, out_q):
+def _worker(rank, world, port, bucket_mb, side, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0")  # both ranks share cuda:0
+                      LOCAL_RANK="0", BPE_DW_STREAM=side)  # both ranks share cuda:0
     from bpe_transformer.parallel import cleanup, init_distributed
     from bpe_transformer.train.engine import TrainEngine
 
@@ -56,12 +57,13 @@ def _worker(rank, world, port, bucket_mb, out_q):
     cleanup()
 
 
+@pytest.mark.parametrize("side", ["0", "1"])
 @pytest.mark.parametrize("bucket_mb", [0.25, 64.0])
-def test_dp2_gpu_side_stream(gpu_device, bucket_mb):
+def test_dp2_gpu(gpu_device, bucket_mb, side):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, side, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {r: (g, d, nb) for r, g, d, nb in (q.get(timeout=240) for _ in range(world))}

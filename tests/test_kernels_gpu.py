@@ -31,7 +31,7 @@ def _ref_grads(fn, inputs, dout):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(64, 768), (3, 5, 2048), (7, 512)])
+@pytest.mark.parametrize("shape", [(64, 768), (3, 5, 2048), (7, 512), (2048, 2048), (33, 4096)])
 def test_rmsnorm(gpu_device, dtype, shape):
     torch.manual_seed(0)
     x = torch.randn(*shape, device=gpu_device, dtype=dtype, requires_grad=True)
