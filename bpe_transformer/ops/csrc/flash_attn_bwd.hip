@@ -105,7 +105,9 @@ __device__ __forceinline__ void softmax_ds(f32x16& sp, f32x16& dp, int hh, float
     }
 }
 
-template <int D, bool CAUSAL, bool ROPE>
+// DBG (timing diagnostics, numerically wrong; built only with -DBPE_FA_DIAG): bit 1 = no dQ phase,
+// bit 2 = no softmax (P = S), bit 3 = no next-tile global loads
+template <int D, bool CAUSAL, bool ROPE, int DBG = 0>
 __global__ void __launch_bounds__(BwdCfg<D>::NW * 64, BwdCfg<D>::WGS)
 fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv, long ld_q,
               long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
@@ -225,7 +227,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     auto body = [&](int it) {
         const int cur = C::QBUF == 2 ? (it & 1) : 0;
         const int m0 = m_start + it * 64;
-        if (it + 1 < total_it) load_tile(it + 1);
+        if (it + 1 < total_it && !(DBG & 8)) load_tile(it + 1);
         char* Qc = Qs + cur * QT;
         char* Oc = dOs + cur * QT;
         const float* lc = lseS + cur * 64;
@@ -256,7 +258,8 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                 }
                 // P = exp2(S * scale*log2e - LSE2), dS = P * (dP - delta); diagonal / ragged tiles (wave-uniform
                 // test, scalar branch) zero P where (unsigned)(q - klim) >= span
-                if (need_mask)
+                if (DBG & 4) {
+                } else if (need_mask)
                     softmax_ds<true>(sp, dp, hh, scale_log2, m0 + qt * 32 - klim, span);
                 else
                     softmax_ds<false>(sp, dp, hh, scale_log2, 0, 0u);
@@ -297,7 +300,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
         //      of a wave share their query block, so the dS^T fragments are read once per 32-key step.
         //      dQacc rows are padded to a multiple of 64 per batch: rows q >= S of the last tile land in
         //      padding (carrying zeros: P = 0 there), so the atomics need no per-element guard.
-        {
+        if (!(DBG & 2)) {
             constexpr int DB = D / 16, TPW = 4 * DB / NW;
             const int t0 = w * TPW, qb = t0 / DB;
             f32x4 acc[TPW];
@@ -455,6 +458,20 @@ using namespace bpe::fa;
 
 size_t fa_bwd_lds_bytes(int D) { return D == 64 ? BwdCfg<64>::LDS : BwdCfg<128>::LDS; }
 
+template <int D, bool C, bool R, int DBG>
+static void bwd_main(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
+    using Cfg = BwdCfg<D>;
+    static bool lds_attr = false;  // > 64 KiB of dynamic LDS: opt in once (before any graph capture)
+    if (!lds_attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fa_bwd_kernel<D, C, R, DBG>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+        lds_attr = true;
+    }
+    fa_bwd_kernel<D, C, R, DBG><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
+        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv,
+        a.dkv_part, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, dbg);
+}
+
 template <int D, bool C, bool R>
 static void bwd_launch(const FaArgs& a, hipStream_t s) {
     using Cfg = BwdCfg<D>;
@@ -472,15 +489,21 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
     }();
     {
         const int nkb = (a.S + Cfg::KB - 1) / Cfg::KB;
-        static bool lds_attr = false;  // > 64 KiB of dynamic LDS: opt in once (before any graph capture)
-        if (!lds_attr) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fa_bwd_kernel<D, C, R>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
-            lds_attr = true;
+#ifdef BPE_FA_DIAG
+        static const int diag = [] {
+            const char* e = getenv("BPE_FA_DIAG");
+            return e ? atoi(e) : 0;
+        }();
+        switch (diag) {
+            case 2: bwd_main<D, C, R, 2>(a, s, nkb, dbg); break;
+            case 4: bwd_main<D, C, R, 4>(a, s, nkb, dbg); break;
+            case 8: bwd_main<D, C, R, 8>(a, s, nkb, dbg); break;
+            case 14: bwd_main<D, C, R, 14>(a, s, nkb, dbg); break;
+            default: bwd_main<D, C, R, 0>(a, s, nkb, dbg); break;
         }
-        fa_bwd_kernel<D, C, R><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
-            a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv,
-            a.dkv_part, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, dbg);
+#else
+        bwd_main<D, C, R, 0>(a, s, nkb, dbg);
+#endif
     }
     if (a.Hkv < a.H) {
         const long tkv = (long)a.B * a.S * a.Hkv * (D / 4);
