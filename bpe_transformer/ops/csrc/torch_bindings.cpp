@@ -361,6 +361,22 @@ void cast_fp8(const at::Tensor& x, const at::Tensor& scale, at::Tensor out, at::
                     reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
 }
 
+// W [N][K] bf16 -> e4m3 copies w8 [N][K] and w8t [K][N] in one pass (amax folded into amax_bits)
+void cast_fp8_t(const at::Tensor& w, const at::Tensor& scale, at::Tensor w8, at::Tensor w8t, at::Tensor amax_bits) {
+    check_cuda(w, "w");
+    TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.scalar_type() == at::kBFloat16, "cast_fp8_t: bf16 [N, K]");
+    const int N = (int)w.size(0), K = (int)w.size(1);
+    TORCH_CHECK(N % 64 == 0 && K % 64 == 0, "cast_fp8_t: N and K must be multiples of 64");
+    TORCH_CHECK(w8.is_contiguous() && w8t.is_contiguous() && w8.numel() == w.numel() && w8t.numel() == w.numel() &&
+                    w8.scalar_type() == at::kFloat8_e4m3fn && w8t.scalar_type() == at::kFloat8_e4m3fn &&
+                    w8t.size(0) == K, "cast_fp8_t: e4m3 outputs [N, K] and [K, N] required");
+    TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1 && amax_bits.scalar_type() == at::kInt &&
+                    amax_bits.numel() == 1, "cast_fp8_t: one fp32 scale and one int32 amax slot");
+    DevGuard g(w.device());
+    launch_cast_fp8_t(w.data_ptr(), N, K, scale.data_ptr<float>(), w8.data_ptr(), w8t.data_ptr(),
+                      reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
+}
+
 void update_scales(at::Tensor amax_bits, at::Tensor hist, at::Tensor scale, at::Tensor inv_scale, int64_t pos,
                    double margin, int64_t fmt) {
     check_cuda(hist, "hist");
@@ -482,6 +498,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
+    m.def("cast_fp8_t(Tensor w, Tensor scale, Tensor(a!) w8, Tensor(b!) w8t, Tensor(c!) amax_bits) -> ()");
     m.def("update_scales(Tensor(a!) amax_bits, Tensor(b!) hist, Tensor(c!) scale, Tensor(d!) inv_scale, int pos, "
           "float margin, int fmt=0) -> ()");
     m.def("softmax_fwd(Tensor x) -> Tensor");
@@ -511,6 +528,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("gemm_pp", &gemm_pp);
     m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
     m.impl("cast_fp8", &cast_fp8);
+    m.impl("cast_fp8_t", &cast_fp8_t);
     m.impl("update_scales", &update_scales);
     m.impl("softmax_fwd", &softmax_fwd);
     m.impl("softmax_bwd", &softmax_bwd);

@@ -66,22 +66,36 @@ class Fp8State:
         self.pos = int(sd["pos"])
         self.margin = float(sd["margin"])
 
+    def cast_t(self, w: Tensor, slot: int) -> tuple[Tensor, Tensor]:
+        """Weight cast: (w8 [N, K], w8t [K, N]) in one pass (csrc/fp8.hip cast_fp8_t)."""
+        w = w.contiguous()
+        w8 = torch.empty(w.shape, dtype=self.dtype, device=w.device)
+        w8t = torch.empty(w.shape[1], w.shape[0], dtype=self.dtype, device=w.device)
+        ops().cast_fp8_t(w, self.scale[slot : slot + 1], w8, w8t, self.amax[slot : slot + 1])
+        return w8, w8t
+
     def matmul(self, x: Tensor, w: Tensor, x_slot: int, w_slot: int, keep_w8: bool = False):
         """``x @ w.T`` in fp8 with bf16 output; x: [M, K] bf16, w: [N, K] bf16.  ``keep_w8`` also returns the
-        quantised weight (reused by the input-gradient GEMM)."""
+        quantised weight in the [K, N] layout the input-gradient GEMM needs (written by the same cast pass)."""
         x8 = self.cast(x, x_slot)
-        w8 = self.cast(w, w_slot)
+        t_ok = keep_w8 and self.fmt == "e4m3" and w.dtype == torch.bfloat16 and w.shape[0] % 64 == 0 \
+            and w.shape[1] % 64 == 0
+        if t_ok:
+            w8, w8t = self.cast_t(w, w_slot)
+        else:
+            w8, w8t = self.cast(w, w_slot), None
         y = torch._scaled_mm(x8, w8.t(), scale_a=self.inv_scale[x_slot], scale_b=self.inv_scale[w_slot],
                              out_dtype=torch.bfloat16)
-        return (y, w8) if keep_w8 else y
+        if not keep_w8:
+            return y
+        return y, (w8t if w8t is not None else w8.t().contiguous())
 
 
-def dgrad(g_state: Fp8State, g: Tensor, g_slot: int, w8: Tensor, w_state: Fp8State, w_slot: int) -> Tensor:
+def dgrad(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8State, w_slot: int) -> Tensor:
     """``g @ W`` with g: [M, N] bf16 quantised to e5m2 (slot ``g_slot`` of ``g_state``) and W the forward's e4m3
-    copy w8: [N, K] (its scale in slot ``w_slot`` of ``w_state``).  The library wants the second operand
-    column-major, i.e. W^T contiguous."""
+    copy in the [K, N] layout ``w8t`` (its scale in slot ``w_slot`` of ``w_state``): the library wants the
+    second operand column-major, i.e. W^T contiguous."""
     g8 = g_state.cast(g.contiguous(), g_slot)
-    w8t = w8.t().contiguous()
     return torch._scaled_mm(g8, w8t.t(), scale_a=g_state.inv_scale[g_slot], scale_b=w_state.inv_scale[w_slot],
                             out_dtype=torch.bfloat16)
 

@@ -398,6 +398,24 @@ def test_cast_fp8_and_amax(gpu_device, dtype, n, fmt):
     assert amax.view(torch.float32).item() == x.float().abs().max().item()
 
 
+def test_cast_fp8_transposed(gpu_device):
+    """Weight cast: both e4m3 layouts from one pass, identical bytes to the plain cast, amax folded in."""
+    torch.manual_seed(3)
+    N, K = 192, 320
+    w = torch.randn(N, K, device=gpu_device, dtype=torch.bfloat16) * 3
+    scale = torch.tensor([4.0], device=gpu_device)
+    amax = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+    w8 = torch.empty(N, K, dtype=torch.float8_e4m3fn, device=gpu_device)
+    w8t = torch.empty(K, N, dtype=torch.float8_e4m3fn, device=gpu_device)
+    torch.ops.bpe_hip.cast_fp8_t(w, scale, w8, w8t, amax)
+    ref = torch.empty_like(w8)
+    torch.ops.bpe_hip.cast_fp8(w, scale, ref, torch.zeros(1, dtype=torch.int32, device=gpu_device))
+    assert torch.equal(w8.view(torch.uint8), ref.view(torch.uint8))
+    assert torch.equal(w8t.view(torch.uint8), ref.view(torch.uint8).t().contiguous())
+    am = amax.view(torch.float32).item()
+    assert am == float(w.float().abs().max())
+
+
 def test_update_scales(gpu_device):
     n, H = 3, 4
     amax = torch.tensor([2.0, 0.0, 1000.0], device=gpu_device).view(torch.int32).clone()
