@@ -59,6 +59,7 @@ class TrainConfig:
     profile: bool = False
     phase_timing: bool = False  # log fwd / bwd / exposed-comm / optimizer ms (device events) at each log step
     nan_guard: bool = True
+    ddp_check_every: int = 0  # >0: every N steps assert bit-identical grads / weights across DP ranks
 
     def to_dict(self) -> dict:
         d = dataclasses.asdict(self)

@@ -35,6 +35,7 @@ class TrainEngine:
         max_grad_norm: float | None = 1.0,
         bucket_mb: float = 64.0,
         time_phases: bool = False,
+        ddp_check_every: int = 0,
     ):
         self.model = model
         self.dist = dist_info or DistInfo()
@@ -48,6 +49,10 @@ class TrainEngine:
             self.ddp.broadcast_parameters(0)
             self.opt.master.copy_(self.flat.data)  # keep fp32 master == broadcast weights
         self.last_grad_norm: Tensor | None = None
+        # DP race / divergence detector: every N steps compare per-bucket gradient and weight checksums across
+        # ranks (parallel/ddp.py check_consistency; raises on mismatch)
+        self.ddp_check_every = ddp_check_every
+        self.steps_done = 0
         # phase timing (SURVEY §5 tracing): device events around forward / backward / exposed all-reduce wait /
         # clip + optimizer, recorded every step and only read (one host sync) when phase_times() is called
         self.time_phases = time_phases and torch.cuda.is_available() and self.flat.data.is_cuda
@@ -99,12 +104,18 @@ class TrainEngine:
         self._mark("bwd")
         if self.ddp is not None:
             self.ddp.finish()
+        check = self.ddp is not None and self.ddp_check_every > 0 and self.steps_done % self.ddp_check_every == 0
+        if check:
+            self.ddp.check_consistency("grad")
         self._mark("comm")
         coef = None
         if self.max_grad_norm is not None and self.max_grad_norm > 0:
             norm, coef = self.opt.clip_grad_norm(self.max_grad_norm)
             self.last_grad_norm = norm
         self.opt.step(lr, coef)
+        if check:
+            self.ddp.check_consistency("data")
+        self.steps_done += 1
         self._mark("opt")
         states = self.model.fp8_states() if hasattr(self.model, "fp8_states") else []
         for fp8 in states:

@@ -64,7 +64,8 @@ class Trainer:
         o = cfg.optim
         self.engine = TrainEngine(self.model, self.info, lr=o.lr, betas=o.betas, eps=o.eps,
                                   weight_decay=o.weight_decay, max_grad_norm=o.max_grad_norm,
-                                  bucket_mb=cfg.bucket_mb, time_phases=cfg.phase_timing)
+                                  bucket_mb=cfg.bucket_mb, time_phases=cfg.phase_timing,
+                                  ddp_check_every=cfg.ddp_check_every)
         self.schedule = CosineSchedule(o.lr, o.min_lr, o.warmup_iters, o.cosine_cycle_iters or cfg.max_iters)
         ctx = cfg.model.context_length
         if cfg.data.train_path:

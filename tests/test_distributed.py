@@ -122,3 +122,41 @@ def test_bucket_notifications_idempotent():
     assert launched == [0]
     ar.start()
     assert ar._seen == set() and ar._pending == ar._members
+
+
+def _check_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from bpe_transformer.parallel import cleanup, init_distributed
+    from bpe_transformer.train.engine import TrainEngine
+
+    info = init_distributed("cpu")
+    eng = TrainEngine(_model(), info, lr=1e-2, bucket_mb=0.01, ddp_check_every=1)
+    eng.train_step([_batches(rank)])  # consistent: must not raise
+    ok = True
+    # inject a divergence: rank 1 perturbs its weights; the next check must catch it on every rank
+    if rank == 1:
+        with torch.no_grad():
+            eng.flat.data[5] += 1.0
+    try:
+        eng.train_step([_batches(rank)])
+        ok = False
+    except RuntimeError as e:
+        ok = "divergence" in str(e)
+    out_q.put((rank, ok))
+    cleanup()
+
+
+def test_ddp_consistency_check_detects_divergence():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_check_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
+
