@@ -48,7 +48,8 @@ def _worker(rank, world, port, bucket_mb, side, out_q):
     from bpe_transformer.train.engine import TrainEngine
 
     info = init_distributed("cuda", backend="gloo")
-    eng = TrainEngine(_model(info.device), info, lr=1e-3, weight_decay=0.0, max_grad_norm=1.0, bucket_mb=bucket_mb)
+    eng = TrainEngine(_model(info.device), info, lr=1e-3, weight_decay=0.0, max_grad_norm=1.0, bucket_mb=bucket_mb,
+                      ddp_check_every=1)  # also asserts bit-identical grads / weights across the ranks
     eng.train_step([_batch(rank, info.device)])
     g1 = eng.flat.grad.float().cpu()
     eng.train_step([_batch(rank, info.device)])
