@@ -12,12 +12,15 @@ from .layers import (
     SwiGLU,
     TransformerBlock,
 )
+from .generation import DecodeSession, KVCache
 from .transformer import TransformerLM
 
 __all__ = [
     "PRESETS",
     "ActFFN",
+    "DecodeSession",
     "Embedding",
+    "KVCache",
     "Linear",
     "ModelConfig",
     "MultiHeadSelfAttention",

@@ -135,10 +135,22 @@ class TransformerLM(nn.Module):
         top_p: float | None = None,
         eos_token_id: int | None = None,
         generator: torch.Generator | None = None,
+        use_cache: bool = True,
     ) -> Tensor:
-        """Autoregressive sampling (temperature + nucleus).  ``prompt``: ``[S]`` or ``[B, S]``."""
+        """Autoregressive sampling (temperature + nucleus).  ``prompt``: ``[S]`` or ``[B, S]``.
+
+        With ``use_cache`` (and prompt + new tokens within ``context_length``) decoding runs through a KV-cache
+        :class:`~bpe_transformer.models.generation.DecodeSession` (HIP-graph-captured decode step on the GPU);
+        otherwise every step re-runs the model on the last ``context_length`` tokens.
+        """
         squeeze = prompt.dim() == 1
         ids = prompt.unsqueeze(0) if squeeze else prompt
+        if use_cache and ids.shape[1] + max_new_tokens <= self.context_length and max_new_tokens > 0:
+            from .generation import DecodeSession
+
+            sess = DecodeSession(self, ids.shape[0], max_len=ids.shape[1] + max_new_tokens)
+            out = sess.generate(ids, max_new_tokens, temperature, top_p, eos_token_id, generator)
+            return out[0] if squeeze else out
         for _ in range(max_new_tokens):
             ctx = ids[:, -self.context_length :]
             logits = self.forward(ctx)[:, -1, :].float()

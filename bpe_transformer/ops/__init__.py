@@ -11,6 +11,7 @@ training step is here.
 from ._ext import is_built, library_path, load
 from .activations import gelu, silu, swiglu_gate
 from .attention import attention_qkv_reference, flash_attention_qkv, flash_supported
+from .decode import decode_attention, kv_append
 from .embedding import embedding
 from .loss import IGNORE_INDEX, cross_entropy, lm_head_cross_entropy
 from .norm import rmsnorm
@@ -24,6 +25,7 @@ __all__ = [
     "attention_qkv_reference",
     "clip_grad_norm_",
     "cross_entropy",
+    "decode_attention",
     "embedding",
     "flash_attention_qkv",
     "flash_supported",
@@ -31,6 +33,7 @@ __all__ = [
     "gelu",
     "grad_norm",
     "is_built",
+    "kv_append",
     "library_path",
     "lm_head_cross_entropy",
     "load",

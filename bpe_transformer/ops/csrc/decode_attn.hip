@@ -1,0 +1,248 @@
+// KV-cache decode attention and KV-cache append, gfx950.  Serving path of the framework: the reference has no
+// inference engine (SURVEY §1 "absent layers"); generation with a KV cache reuses the training model's weights
+// (`models/generation.py`).
+//
+//   q [B, H, D] (RoPE already applied), cache K / V [B, Hkv, Lmax, D] (roped K), valid length L = *pos + 1:
+//   out[b, h] = softmax(q . K[b, h / G, :L]^T * scale) . V[b, h / G, :L]          (G = H / Hkv)
+//
+// The position lives in device memory (int32), so one decode step -- append + attention for every layer -- is
+// shape-static and is captured once into a HIP graph (the host never passes the growing length).
+//
+// Memory-bound (one pass over K and V per token), so the design is about bandwidth, not MFMA (guide
+// Appendix B "Attention decode": K/V straight to VGPRs): the key range is split into chunks of CH keys, one
+// workgroup per (batch, kv head, chunk) handles all G query heads of that kv head, so K and V are read once
+// for the G heads.
+//   1. scores: thread t owns key t of the chunk, streams its K row (16-byte loads) and dots it with the G query
+//      rows (fp32, broadcast from LDS);
+//   2. per head: block max / sum of exp over the chunk (fp32);
+//   3. o[g][d] = sum_t p[g][t] V[t][d]: thread = (key partition, 8-wide d vector), 16-byte V loads; partitions
+//      are reduced inside the wave with lane shuffles, then across the 4 waves through LDS;
+//   4. the partial (o, m, l) of every (b, h, chunk) goes to fp32 scratch; a combine kernel merges the chunks
+//      (flash-decoding) and writes bf16.  Chunks past the valid length write m = -inf and are skipped.
+#include "common.h"
+#include "kernels.h"
+
+namespace bpe {
+namespace dec {
+
+constexpr int CH = 256;  // keys per chunk (= threads per workgroup)
+
+// G (query heads per kv head) is a template parameter: the per-head registers (m, l, o accumulators) must be
+// statically indexed (guide §5.4 rule 20: runtime-indexed register arrays go to scratch).
+template <int D, int G>
+__global__ void __launch_bounds__(256) decode_attn_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ Kc,
+                                                          const __bf16* __restrict__ Vc, float* __restrict__ part,
+                                                          const int* __restrict__ pos, int H, int Hkv, int Lmax,
+                                                          int nsplit, float scale) {
+    constexpr int DV = D / 8;     // 16-byte vectors per row
+    constexpr int KP = 256 / DV;  // key partitions of the P.V step
+    __shared__ float qs[G][D];
+    __shared__ float ps[G][CH];
+    __shared__ float red[2][4];
+    __shared__ float ob[4][G][D];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int bk = blockIdx.x / nsplit, split = blockIdx.x % nsplit;  // bk = b * Hkv + hk
+    const int b = bk / Hkv, hk = bk % Hkv;
+    const int L = min(pos[0] + 1, Lmax);
+    const int s0 = split * CH;
+    if (s0 >= L) {  // uniform per workgroup: an empty chunk contributes nothing
+        if (tid < G) {
+            float* pr = part + (((long)b * H + hk * G + tid) * nsplit + split) * (D + 2);
+            pr[D] = -INFINITY;
+            pr[D + 1] = 0.f;
+        }
+        return;
+    }
+    const int n = min(CH, L - s0);
+    // query rows of the G heads -> LDS (fp32, pre-scaled)
+    for (int e = tid; e < G * D; e += 256) {
+        const int g = e / D, d = e % D;
+        qs[g][d] = bf2f(reinterpret_cast<const u16*>(q)[((long)b * H + hk * G + g) * D + d]) * scale;
+    }
+    __syncthreads();
+    const long kvbase = ((long)bk * Lmax + s0) * D;
+    // 1. scores
+    {
+        const bool ok = tid < n;
+        float s[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = 0.f;
+        if (ok) {
+            const u16x8* kp = reinterpret_cast<const u16x8*>(Kc + kvbase + (long)tid * D);
+#pragma unroll 4
+            for (int v = 0; v < DV; ++v) {
+                const u16x8 t = kp[v];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float kx = bf2f(t[j]);
+#pragma unroll
+                    for (int g = 0; g < G; ++g) s[g] += qs[g][8 * v + j] * kx;
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) ps[g][tid] = ok ? s[g] : -INFINITY;
+    }
+    __syncthreads();
+    // 2. per-head max / exp / sum over the chunk
+    float mg[G], lg[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        float m = wave_max(ps[g][tid]);
+        if (lane == 0) red[0][wv] = m;
+        __syncthreads();
+        m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+        const float p = tid < n ? __expf(ps[g][tid] - m) : 0.f;
+        ps[g][tid] = p;
+        float sm = wave_sum(p);
+        if (lane == 0) red[1][wv] = sm;
+        __syncthreads();
+        mg[g] = m;
+        lg[g] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        __syncthreads();  // red[] reused by the next head
+    }
+    // 3. o[g][d] = sum_t p[g][t] V[t][d]; thread = (key partition kp, vector dv)
+    const int dv = tid % DV, kp = tid / DV;
+    float acc[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+    for (int t = kp; t < n; t += KP) {
+        const u16x8 vv = *reinterpret_cast<const u16x8*>(Vc + kvbase + (long)t * D + dv * 8);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float p = ps[g][t];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[g][j] += p * bf2f(vv[j]);
+        }
+    }
+    // lanes that share dv differ by multiples of DV: butterfly over the wave's key partitions
+#pragma unroll
+    for (int off = DV; off < 64; off <<= 1)
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[g][j] += __shfl_xor(acc[g][j], off);
+    if (lane < DV) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ob[wv][g][dv * 8 + j] = acc[g][j];
+    }
+    __syncthreads();
+    // 4. partial results: part[(b, h, split)] = {o[D], m, l}
+    for (int e = tid; e < G * D; e += 256) {
+        const int g = e / D, dd = e % D;
+        const float o = ob[0][g][dd] + ob[1][g][dd] + ob[2][g][dd] + ob[3][g][dd];
+        float* pr = part + (((long)b * H + hk * G + g) * nsplit + split) * (D + 2);
+        pr[dd] = o;
+    }
+    if (tid < G) {  // the head statistics (registers, identical in every thread)
+        float m = mg[0], l = lg[0];
+#pragma unroll
+        for (int g = 1; g < G; ++g)
+            if (tid == g) { m = mg[g]; l = lg[g]; }
+        float* pr = part + (((long)b * H + hk * G + tid) * nsplit + split) * (D + 2);
+        pr[D] = m;
+        pr[D + 1] = l;
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restrict__ part, __bf16* __restrict__ out,
+                                                           int nsplit) {
+    const long bh = blockIdx.x;
+    const int d = threadIdx.x;
+    const float* p = part + bh * nsplit * (D + 2);
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, p[s * (D + 2) + D]);
+    float Lsum = 0.f, o = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+        const float m = p[s * (D + 2) + D];
+        if (m == -INFINITY) continue;
+        const float c = __expf(m - M);
+        Lsum += c * p[s * (D + 2) + D + 1];
+        o += c * p[s * (D + 2) + d];
+    }
+    reinterpret_cast<u16*>(out)[bh * D + d] = f2bf(Lsum > 0.f ? o / Lsum : 0.f);
+}
+
+// KV-cache append: fused-QKV rows [B*T, (H + 2*Hkv)*D] of T new tokens per sequence at positions
+// *pos .. *pos+T-1 -> RoPE'd q [B*T, H*D] and roped K / plain V written into the caches [B, Hkv, Lmax, D].
+// One thread per 16-byte vector (8 bf16); the rotation pairs (2i, 2i+1) never straddle a vector.
+__global__ void __launch_bounds__(256) kv_append_kernel(const __bf16* __restrict__ qkv, long ld,
+                                                        __bf16* __restrict__ qo, __bf16* __restrict__ Kc,
+                                                        __bf16* __restrict__ Vc, const float* __restrict__ cosT,
+                                                        const float* __restrict__ sinT, const int* __restrict__ pos,
+                                                        int T, int H, int Hkv, int D, int Lmax, long total) {
+    const int dv = D / 8, W = (H + 2 * Hkv) * dv;
+    const int p0 = pos[0];
+    for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+        const long r = idx / W;
+        const int c = (int)(idx % W), hh = c / dv, d0 = (c % dv) * 8;
+        const int b = (int)(r / T), p = p0 + (int)(r % T);
+        if (p >= Lmax) continue;  // cache full: nothing is written past the end
+        u16x8 x = *reinterpret_cast<const u16x8*>(qkv + r * ld + (long)hh * D + d0);
+        if (hh < H + Hkv && cosT != nullptr) {
+            const float* cs = cosT + (long)p * (D / 2) + d0 / 2;
+            const float* sn = sinT + (long)p * (D / 2) + d0 / 2;
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+                const float x1 = bf2f(x[j]), x2 = bf2f(x[j + 1]), cc = cs[j / 2], ss = sn[j / 2];
+                x[j] = f2bf(x1 * cc - x2 * ss);
+                x[j + 1] = f2bf(x1 * ss + x2 * cc);
+            }
+        }
+        __bf16* dst;
+        if (hh < H) dst = qo + r * (long)H * D + (long)hh * D + d0;
+        else if (hh < H + Hkv) dst = Kc + (((long)b * Hkv + (hh - H)) * Lmax + p) * D + d0;
+        else dst = Vc + (((long)b * Hkv + (hh - H - Hkv)) * Lmax + p) * D + d0;
+        *reinterpret_cast<u16x8*>(dst) = x;
+    }
+}
+
+}  // namespace dec
+}  // namespace bpe
+
+using namespace bpe::dec;
+
+int decode_attn_splits(int Lmax) { return (Lmax + CH - 1) / CH; }
+
+bool decode_attn_ok(int H, int Hkv, int D) {
+    const int G = Hkv > 0 ? H / Hkv : 0;
+    return (D == 64 || D == 128) && Hkv > 0 && H % Hkv == 0 && (G == 1 || G == 2 || G == 4 || G == 8);
+}
+
+template <int D>
+static void launch_d(const void* q, const void* k, const void* v, float* part, void* out, const int* pos, int B,
+                     int H, int Hkv, int Lmax, float scale, hipStream_t s) {
+    const int ns = decode_attn_splits(Lmax);
+    const int grid = B * Hkv * ns;
+#define DEC(GG)                                                                                                   \
+    decode_attn_kernel<D, GG><<<grid, 256, 0, s>>>((const __bf16*)q, (const __bf16*)k, (const __bf16*)v, part, pos, \
+                                                   H, Hkv, Lmax, ns, scale)
+    switch (H / Hkv) {
+        case 1: DEC(1); break;
+        case 2: DEC(2); break;
+        case 4: DEC(4); break;
+        default: DEC(8); break;
+    }
+#undef DEC
+    decode_combine_kernel<D><<<B * H, D, 0, s>>>(part, (__bf16*)out, ns);
+}
+
+void launch_decode_attn(const void* q, const void* k, const void* v, float* part, void* out, const int* pos, int B,
+                        int H, int Hkv, int D, int Lmax, float scale, hipStream_t s) {
+    if (D == 64) launch_d<64>(q, k, v, part, out, pos, B, H, Hkv, Lmax, scale, s);
+    else launch_d<128>(q, k, v, part, out, pos, B, H, Hkv, Lmax, scale, s);
+}
+
+void launch_kv_append(const void* qkv, long ld, void* qo, void* Kc, void* Vc, const float* cosT, const float* sinT,
+                      const int* pos, int B, int T, int H, int Hkv, int D, int Lmax, hipStream_t s) {
+    const long total = (long)B * T * (H + 2 * Hkv) * (D / 8);
+    const long want = (total + 255) / 256;
+    const int grid = (int)(want < 8192 ? want : 8192);
+    kv_append_kernel<<<grid, 256, 0, s>>>((const __bf16*)qkv, ld, (__bf16*)qo, (__bf16*)Kc, (__bf16*)Vc, cosT, sinT,
+                                          pos, T, H, Hkv, D, Lmax, total);
+}

@@ -477,9 +477,71 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     return dqkv;
 }
 
+// ---------------------------------------------------------------- KV-cache decode (serving)
+void check_cache(const at::Tensor& c, int64_t B, int64_t Hkv, const char* name) {
+    check_cuda(c, name);
+    TORCH_CHECK(c.scalar_type() == at::kBFloat16 && c.dim() == 4 && c.is_contiguous(), "kv cache: ", name,
+                " must be a contiguous bf16 [B, Hkv, Lmax, D] tensor");
+    TORCH_CHECK(c.size(0) == B && c.size(1) == Hkv, "kv cache: ", name, " batch / kv-head mismatch");
+    check_aligned(c, name);
+}
+
+void check_pos(const at::Tensor& pos) {
+    check_cuda(pos, "pos");
+    TORCH_CHECK(pos.scalar_type() == at::kInt && pos.numel() == 1, "kv cache: pos must be one device int32");
+}
+
+// qkv [B*T, (H + 2*Hkv)*D] rows of T new tokens at positions *pos.. -> roped q [B*T, H*D]; K (roped) and V are
+// written into the caches at those positions.
+at::Tensor kv_append(const at::Tensor& qkv, at::Tensor kc, at::Tensor vc, const at::Tensor& cos, const at::Tensor& sin,
+                     const at::Tensor& pos, int64_t B, int64_t T, int64_t H, bool use_rope) {
+    const int64_t Hkv = kc.size(1), Lmax = kc.size(2), D = kc.size(3);
+    TORCH_CHECK(D % 8 == 0 && H % Hkv == 0, "kv_append: head dim multiple of 8, H multiple of Hkv");
+    check_qkv(qkv, B * T, (H + 2 * Hkv) * D, "qkv");
+    check_cache(kc, B, Hkv, "k_cache");
+    check_cache(vc, B, Hkv, "v_cache");
+    TORCH_CHECK(vc.sizes() == kc.sizes(), "kv_append: k / v cache shapes differ");
+    check_pos(pos);
+    if (use_rope)
+        TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+                        sin.is_contiguous() && cos.size(0) >= Lmax && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(),
+                    "kv_append: rope tables must be fp32 [>=Lmax, D/2]");
+    DevGuard g(qkv.device());
+    auto q = at::empty({B * T, H * D}, qkv.options());
+    launch_kv_append(qkv.data_ptr(), qkv.stride(0), q.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                     use_rope ? cos.data_ptr<float>() : nullptr, use_rope ? sin.data_ptr<float>() : nullptr,
+                     pos.data_ptr<int>(), (int)B, (int)T, (int)H, (int)Hkv, (int)D, (int)Lmax, cur_stream());
+    return q;
+}
+
+// q [B, H*D] (roped) attends to the first *pos + 1 cache rows -> [B, H*D]
+at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& pos,
+                       int64_t H, double scale) {
+    const int64_t B = kc.size(0), Hkv = kc.size(1), Lmax = kc.size(2), D = kc.size(3);
+    TORCH_CHECK(decode_attn_ok((int)H, (int)Hkv, (int)D),
+                "decode_attn: head dim 64/128 and H / Hkv in {1, 2, 4, 8} required");
+    check_cuda(q, "q");
+    TORCH_CHECK(q.scalar_type() == at::kBFloat16 && q.is_contiguous() && q.numel() == B * H * D,
+                "decode_attn: q must be contiguous bf16 [B, H*D]");
+    check_cache(kc, B, Hkv, "k_cache");
+    check_cache(vc, B, Hkv, "v_cache");
+    TORCH_CHECK(vc.sizes() == kc.sizes(), "decode_attn: k / v cache shapes differ");
+    check_pos(pos);
+    DevGuard g(q.device());
+    const int ns = decode_attn_splits((int)Lmax);
+    auto part = at::empty({B * H * ns * (D + 2)}, q.options().dtype(at::kFloat));
+    auto out = at::empty({B, H * D}, q.options());
+    launch_decode_attn(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), part.data_ptr<float>(), out.data_ptr(),
+                       pos.data_ptr<int>(), (int)B, (int)H, (int)Hkv, (int)D, (int)Lmax, (float)scale, cur_stream());
+    return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(bpe_hip, m) {
+    m.def("kv_append(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor cos, Tensor sin, Tensor pos, int B, "
+          "int T, int H, bool rope) -> Tensor");
+    m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor pos, int H, float scale) -> Tensor");
     m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
     m.def("add_rmsnorm_fwd(Tensor x, Tensor d, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
     m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
@@ -535,4 +597,6 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("rope", &rope);
     m.impl("fa_fwd", &fa_fwd);
     m.impl("fa_bwd", &fa_bwd);
+    m.impl("kv_append", &kv_append);
+    m.impl("decode_attn", &decode_attn);
 }

@@ -1,0 +1,74 @@
+"""KV-cache ops of the serving path (``csrc/decode_attn.hip``).
+
+The reference has no inference engine ("absent layers"); these ops
+let ``models.generation`` decode with a KV cache instead of re-running the
+whole prefix for every new token.
+
+* :func:`kv_append` takes the fused QKV projection of ``T`` new tokens per
+  sequence, applies RoPE at their absolute positions (``pos .. pos+T-1``, with
+  ``pos`` a device int32 tensor), writes K (roped) and V into the caches
+  ``[B, Hkv, Lmax, D]``, and returns the roped queries ``[B*T, H*D]``.
+* :func:`decode_attention` is single-token attention of ``q [B, H*D]`` over the
+  first ``pos + 1`` cache rows (split-K "flash-decoding" with a combine pass).
+
+Both read the position from device memory, so a decode step is shape-static and
+can be captured in a HIP graph.  The CPU versions are the oracle.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import Tensor
+
+from . import reference as F
+from ._ext import ops
+
+
+def kv_append(qkv: Tensor, k_cache: Tensor, v_cache: Tensor, cos: Tensor | None, sin: Tensor | None, pos: Tensor,
+              batch: int, n_new: int, n_heads: int) -> Tensor:
+    if qkv.is_cuda:
+        use_rope = cos is not None
+        c = cos if use_rope else qkv.new_empty(0, dtype=torch.float32)
+        s = sin if use_rope else qkv.new_empty(0, dtype=torch.float32)
+        return ops().kv_append(qkv, k_cache, v_cache, c, s, pos, batch, n_new, n_heads, use_rope)
+    return kv_append_reference(qkv, k_cache, v_cache, cos, sin, pos, batch, n_new, n_heads)
+
+
+def kv_append_reference(qkv, k_cache, v_cache, cos, sin, pos, batch, n_new, n_heads) -> Tensor:
+    _, Hkv, Lmax, D = k_cache.shape
+    H = n_heads
+    p0 = int(pos.reshape(-1)[0])
+    x = qkv.view(batch, n_new, H + 2 * Hkv, D)
+    q, k, v = x[:, :, :H], x[:, :, H : H + Hkv], x[:, :, H + Hkv :]
+    if cos is not None:
+        tp = torch.arange(p0, p0 + n_new, device=qkv.device)
+        q = F.apply_rope(q.float().transpose(1, 2), cos, sin, tp).transpose(1, 2).to(qkv.dtype)
+        k = F.apply_rope(k.float().transpose(1, 2), cos, sin, tp).transpose(1, 2).to(qkv.dtype)
+    n = max(0, min(n_new, Lmax - p0))
+    k_cache[:, :, p0 : p0 + n] = k[:, :n].transpose(1, 2).to(k_cache.dtype)
+    v_cache[:, :, p0 : p0 + n] = v[:, :n].transpose(1, 2).to(v_cache.dtype)
+    return q.reshape(batch * n_new, H * D)
+
+
+def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, pos: Tensor, n_heads: int,
+                     scale: float | None = None) -> Tensor:
+    D = k_cache.shape[-1]
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if q.is_cuda:
+        return ops().decode_attn(q.contiguous(), k_cache, v_cache, pos, n_heads, scale)
+    return decode_attention_reference(q, k_cache, v_cache, pos, n_heads, scale)
+
+
+def decode_attention_reference(q, k_cache, v_cache, pos, n_heads, scale=None) -> Tensor:
+    B, Hkv, Lmax, D = k_cache.shape
+    H = n_heads
+    L = min(int(pos.reshape(-1)[0]) + 1, Lmax)
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    qf = q.float().view(B, Hkv, H // Hkv, D)
+    k = k_cache[:, :, :L].float()
+    v = v_cache[:, :, :L].float()
+    s = torch.einsum("bhgd,bhld->bhgl", qf, k) * scale
+    o = torch.einsum("bhgl,bhld->bhgd", F.softmax(s, -1), v)
+    return o.reshape(B, H * D).to(q.dtype)

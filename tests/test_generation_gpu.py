@@ -1,0 +1,120 @@
+"""KV-cache serving kernels on the MI355X: ``kv_append`` / ``decode_attn`` (``ops/csrc/decode_attn.hip``) vs the
+fp32 oracle, and the HIP-graph decode session vs the bf16 model's full forward."""
+
+from __future__ import annotations
+
+import copy
+import math
+
+import pytest
+import torch
+
+from bpe_transformer.models import DecodeSession, TransformerLM
+from bpe_transformer.ops import decode as dec
+from bpe_transformer.ops.reference import rope_tables
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("rope", [True, False])
+def test_kv_append_matches_reference(gpu_device, D, rope):
+    torch.manual_seed(0)
+    B, T, H, Hkv, Lmax, p0 = 3, 5, 8, 2, 40, 7
+    qkv = torch.randn(B * T, (H + 2 * Hkv) * D).bfloat16()
+    cos, sin = rope_tables(D, Lmax, 10000.0) if rope else (None, None)
+    pos = torch.tensor([p0], dtype=torch.int32)
+    kc = torch.zeros(B, Hkv, Lmax, D, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    q_ref = dec.kv_append_reference(qkv.float(), kc, vc, cos, sin, pos, B, T, H)
+    g = lambda t: None if t is None else t.to(gpu_device)  # noqa: E731
+    kg, vg = torch.zeros_like(kc, device=gpu_device), torch.zeros_like(vc, device=gpu_device)
+    q = dec.kv_append(qkv.to(gpu_device), kg, vg, g(cos), g(sin), pos.to(gpu_device), B, T, H)
+    torch.cuda.synchronize()
+    assert rel(q.cpu(), q_ref) < 1e-2
+    assert rel(kg.cpu(), kc) < 1e-2
+    assert torch.equal(vg.cpu(), vc)  # V is copied, not rotated
+    assert kg[:, :, :p0].abs().sum() == 0 and kg[:, :, p0 + T :].abs().sum() == 0
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+@pytest.mark.parametrize("L", [1, 200, 256, 257, 1000])
+def test_decode_attention_matches_reference(gpu_device, D, G, L):
+    torch.manual_seed(L + G)
+    B, Hkv, Lmax = 2, 2, 1024
+    H = Hkv * G
+    q = torch.randn(B, H * D).bfloat16()
+    kc = torch.randn(B, Hkv, Lmax, D).bfloat16()
+    vc = torch.randn(B, Hkv, Lmax, D).bfloat16()
+    pos = torch.tensor([L - 1], dtype=torch.int32)
+    ref = dec.decode_attention_reference(q.float(), kc, vc, pos, H, 1.0 / math.sqrt(D))
+    out = dec.decode_attention(q.to(gpu_device), kc.to(gpu_device), vc.to(gpu_device), pos.to(gpu_device), H)
+    assert rel(out.cpu(), ref) < 2e-2, rel(out.cpu(), ref)
+
+
+def test_decode_attention_large_scores(gpu_device):
+    """One dominant key per chunk boundary: the cross-chunk combine must rescale correctly."""
+    torch.manual_seed(5)
+    B, H, Hkv, D, Lmax = 1, 4, 4, 64, 768
+    q = torch.randn(B, H * D).bfloat16()
+    kc = torch.randn(B, Hkv, Lmax, D).bfloat16() * 0.1
+    vc = torch.randn(B, Hkv, Lmax, D).bfloat16()
+    kc[:, :, 600] = q.view(B, H, D) * 4  # a key in the third chunk dominates
+    pos = torch.tensor([Lmax - 1], dtype=torch.int32)
+    ref = dec.decode_attention_reference(q.float(), kc, vc, pos, H)
+    out = dec.decode_attention(q.to(gpu_device), kc.to(gpu_device), vc.to(gpu_device), pos.to(gpu_device), H)
+    assert rel(out.cpu(), ref) < 2e-2
+
+
+def _bf16_model(gpu_device, **kw):
+    torch.manual_seed(0)
+    cfg = dict(vocab_size=1000, context_length=256, d_model=256, num_layers=2, num_heads=4, d_ff=512)
+    cfg.update(kw)
+    return TransformerLM(**cfg).to(gpu_device, torch.bfloat16).eval()
+
+
+@pytest.mark.parametrize("kw", [{}, {"num_kv_heads": 2}, {"remove_rope": True}])
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_session_matches_full_forward(gpu_device, kw, use_graph):
+    model = _bf16_model(gpu_device, **kw)
+    ids = torch.randint(0, 1000, (3, 40), device=gpu_device)
+    sess = DecodeSession(model, 3, max_len=64, use_graph=use_graph)
+    assert sess.fast
+    with torch.no_grad():
+        full = model(ids).float()
+        got = [sess.prefill(ids[:, :30])]
+        for t in range(30, 40):
+            got.append(sess.decode(ids[:, t]))
+    torch.cuda.synchronize()
+    want = [full[:, 29]] + [full[:, t] for t in range(30, 40)]
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert rel(a, b) < 3e-2, (i, rel(a, b))
+
+
+def test_graph_replay_equals_eager(gpu_device):
+    model = _bf16_model(gpu_device)
+    ids = torch.randint(0, 1000, (2, 24), device=gpu_device)
+    a = DecodeSession(model, 2, max_len=32, use_graph=True)
+    b = DecodeSession(model, 2, max_len=32, use_graph=False)
+    with torch.no_grad():
+        a.prefill(ids[:, :16])
+        b.prefill(ids[:, :16])
+        for t in range(16, 24):
+            la, lb = a.decode(ids[:, t]), b.decode(ids[:, t])
+            assert rel(la, lb) < 1e-3
+    assert torch.equal(a.cache.k, b.cache.k) and torch.equal(a.cache.v, b.cache.v)
+
+
+def test_generate_uses_cache_on_gpu(gpu_device):
+    model = _bf16_model(gpu_device)
+    prompt = torch.randint(0, 1000, (2, 8), device=gpu_device)
+    out = model.generate(prompt, 12, temperature=0.0)
+    assert out.shape == (2, 20) and torch.equal(out[:, :8], prompt)
+    ref = copy.deepcopy(model)
+    first = ref.generate(prompt, 1, temperature=0.0, use_cache=False)
+    assert torch.equal(out[:, 8], first[:, 8])
