@@ -30,12 +30,16 @@ non-SwiGLU FFN) the same session runs the oracle math over the same cache.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch import Tensor
 
-from ..ops import decode as dec
 from ..ops import reference as F
+
+# decode steps of up to this many sequences run on the fused skinny-GEMM kernels; larger batches use the
+# library GEMMs (hipBLASLt), which are MFMA-efficient there
+_GEMV_MAX_BATCH = int(os.environ.get("BPE_DECODE_GEMV_MAX_BATCH", "8"))
 
 
 class KVCache:
@@ -213,6 +217,8 @@ class DecodeSession:
         self._graph = g
 
     def _forward_fast(self, ids: Tensor, prefill: bool) -> Tensor:
+        if not prefill and ids.shape[0] <= _GEMV_MAX_BATCH:
+            return self._decode_gemv(ids)
         from ..ops._ext import ops as hip
 
         h = hip()
@@ -250,6 +256,35 @@ class DecodeSession:
         _, hf, _ = h.add_rmsnorm_fwd(xr, xd, fin.weight, fin.eps)
         logits = torch.matmul(hf, m.lm_head.weight.t())
         pos.add_(T)
+        return logits
+
+    def _decode_gemv(self, ids: Tensor) -> Tensor:
+        """Decode step for batch <= 8 on the fused skinny-GEMM kernels (``csrc/decode_gemv.hip``): per layer
+        qkv (+RMSNorm, +RoPE, +cache write) -> decode attention -> Wo -> [W1; W3] (+residual add, +RMSNorm,
+        +SwiGLU) -> W2; the residual add of W2's output is folded into the next layer's QKV prologue."""
+        from ..ops._ext import ops as hip
+
+        h = hip()
+        m = self.model
+        H = self.H
+        scale = 1.0 / math.sqrt(self.D)
+        kc, vc, pos = self.cache.k, self.cache.v, self.cache.pos
+        use_rope = self._cos is not None
+        cos = self._cos if use_rope else kc.new_empty(0, dtype=torch.float32)
+        sin = self._sin if use_rope else kc.new_empty(0, dtype=torch.float32)
+        xr = m.token_embeddings(ids).reshape(ids.shape[0], -1)
+        xd = None
+        for li, (ln1, wqkv, wo, ln2, w13, w2, eps) in enumerate(self._w):
+            q, s = h.decode_qkv(xr, xd, ln1, eps, wqkv, kc[li], vc[li], cos, sin, pos, H, use_rope)
+            if xd is not None:
+                xr = s
+            o = h.decode_attn(q, kc[li], vc[li], pos, H, scale)
+            g1, _ = h.decode_gemv(o, None, None, 0.0, wo, 0)
+            a, xr = h.decode_gemv(xr, g1, ln2, eps, w13, 1)
+            xd, _ = h.decode_gemv(a, None, None, 0.0, w2, 0)
+        fin = m.ln_final
+        logits, _ = h.decode_gemv(xr, xd, fin.weight, fin.eps, m.lm_head.weight, 0)
+        pos.add_(1)
         return logits
 
     # ------------------------------------------------------------------ oracle path

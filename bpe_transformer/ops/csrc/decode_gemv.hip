@@ -1,0 +1,186 @@
+// Skinny GEMM (GEMV-like, M <= 8 token rows) with fused prologue / epilogues for the decode step, gfx950.
+//
+// At decode time a projection is y[m, n] = sum_k h[m, k] W[n, k] with M = batch (1..8): pure weight streaming
+// (HBM-bound), where library GEMMs cost ~7 us per call and each elementwise op around them another launch.
+// This kernel folds the neighbours in, so a transformer layer is 4 of these launches + the decode attention:
+//   prologue  h = RMSNorm(x (+ xd)) * ln, computed redundantly by every workgroup from the (L2-resident) input
+//             rows; workgroup 0 also writes the residual sum x + xd for the next layer;
+//   epilogue  0: y = h W^T                                   (output projection, W2, LM head)
+//             1: y[:, j] = silu(g_j) * u_j over [W1; W3]    (SwiGLU; rows j and F + j in one wave)
+//             2: fused-QKV with RoPE at the device-side position and the K / V cache write (rows n, n + 1 of
+//                a rotation pair in one wave) -- replaces the separate kv_append launch.
+// Rounding matches the training kernels exactly (bf16 residual sum, (s * rstd) * g, bf16 GEMM outputs before
+// SwiGLU / RoPE), so decode logits agree with the model's forward pass.
+//
+// Mapping (wave64): a 256-thread workgroup owns 16 weight rows, 4 per wave, 16 lanes per row; lane l of a row
+// reads 16-byte W vectors l, l + 16, ... (coalesced 256 B per row per step, 4 loads in flight) and the matching
+// normalized-input vectors from LDS; the 16 partial dots are reduced with xor shuffles inside the row's lanes.
+#include "common.h"
+#include "kernels.h"
+
+namespace bpe {
+namespace gv {
+
+constexpr int LPR = 16;  // lanes per weight row
+constexpr int RPW = 4;   // rows per wave
+constexpr int UNR = 4;   // W vectors in flight per lane
+
+template <int MM, int EPI>
+__global__ void __launch_bounds__(256) gemv_kernel(const GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) u16 hs[];  // [MM][K] normalized input rows (bf16)
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int K = a.K, nv = K / 8;
+    // ---- prologue: wave w normalizes input rows w, w + 4, ...
+    for (int m = wv; m < MM; m += 4) {
+        u16* hr = hs + (long)m * K;
+        if (m >= a.M) {
+            for (int i = lane; i < nv; i += 64) *reinterpret_cast<u16x8*>(hr + 8 * i) = u16x8{};
+            continue;
+        }
+        float ss = 0.f;
+        for (int i = lane; i < nv; i += 64) {
+            u16x8 xv = *reinterpret_cast<const u16x8*>(a.x + (long)m * a.ldx + 8 * i);
+            if (a.xd != nullptr) {
+                const u16x8 dv = *reinterpret_cast<const u16x8*>(a.xd + (long)m * a.ldx + 8 * i);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[j] = f2bf(bf2f(xv[j]) + bf2f(dv[j]));
+                if (a.xsum != nullptr && blockIdx.x == 0)
+                    *reinterpret_cast<u16x8*>(a.xsum + (long)m * K + 8 * i) = xv;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += bf2f(xv[j]) * bf2f(xv[j]);
+            *reinterpret_cast<u16x8*>(hr + 8 * i) = xv;
+        }
+        if (a.ln != nullptr) {
+            ss = wave_sum(ss);
+            const float r = rsqrtf(ss / (float)K + a.eps);
+            for (int i = lane; i < nv; i += 64) {
+                u16x8 hv = *reinterpret_cast<const u16x8*>(hr + 8 * i);
+                const u16x8 g = *reinterpret_cast<const u16x8*>(a.ln + 8 * i);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) hv[j] = f2bf(bf2f(hv[j]) * r * bf2f(g[j]));
+                *reinterpret_cast<u16x8*>(hr + 8 * i) = hv;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- main loop: 4 rows per wave, 16 lanes per row
+    const int slot = lane / LPR, l16 = lane % LPR;
+    const int wslot = wv * RPW + slot;  // row slot within the workgroup (0..15)
+    int n, j = 0;
+    bool valid;
+    if constexpr (EPI == 1) {  // slots (2s, 2s+1) = rows (j, F + j) of logical output column j
+        const int F = a.N / 2;
+        j = blockIdx.x * 8 + wslot / 2;
+        valid = j < F;
+        n = (wslot & 1) ? F + j : j;
+    } else {
+        n = blockIdx.x * 16 + wslot;
+        valid = n < a.N;
+    }
+    float acc[MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m) acc[m] = 0.f;
+    if (valid) {
+        const u16* wr = reinterpret_cast<const u16*>(a.W) + (long)n * a.ldw;
+        for (int i0 = l16; i0 < nv; i0 += LPR * UNR) {
+            u16x8 w[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int i = i0 + LPR * u;
+                w[u] = i < nv ? *reinterpret_cast<const u16x8*>(wr + 8 * i) : u16x8{};
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int i = i0 + LPR * u;
+                if (i >= nv) break;
+#pragma unroll
+                for (int m = 0; m < MM; ++m) {
+                    const u16x8 hv = *reinterpret_cast<const u16x8*>(hs + (long)m * K + 8 * i);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) acc[m] += bf2f(w[u][e]) * bf2f(hv[e]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+#pragma unroll
+        for (int off = LPR / 2; off > 0; off >>= 1) acc[m] += __shfl_xor(acc[m], off);
+    }
+    // ---- epilogues (lane l16 == 0 of each row holds the dots; partners are one row slot apart = 16 lanes)
+    if constexpr (EPI == 0) {
+        if (valid && l16 == 0)
+            for (int m = 0; m < a.M; ++m) reinterpret_cast<u16*>(a.y)[(long)m * a.ldy + n] = f2bf(acc[m]);
+    } else if constexpr (EPI == 1) {
+        float other[MM];
+#pragma unroll
+        for (int m = 0; m < MM; ++m) other[m] = __shfl_xor(acc[m], LPR);
+        if (valid && l16 == 0 && (wslot & 1) == 0)
+            for (int m = 0; m < a.M; ++m) {
+                const float g = bf2f(f2bf(acc[m])), u = bf2f(f2bf(other[m]));
+                reinterpret_cast<u16*>(a.y)[(long)m * a.ldy + j] = f2bf(g * (1.f / (1.f + __expf(-g))) * u);
+            }
+    } else {
+        float other[MM];
+#pragma unroll
+        for (int m = 0; m < MM; ++m) other[m] = __shfl_xor(acc[m], LPR);
+        const int D = a.D, H = a.H, Hkv = a.Hkv;
+        const int hh = n / D, d = n % D, p = a.pos[0];
+        const bool rot = a.cosT != nullptr && hh < H + Hkv;
+        float c = 1.f, s = 0.f;
+        if (rot && valid) {
+            c = a.cosT[(long)p * (D / 2) + d / 2];
+            s = a.sinT[(long)p * (D / 2) + d / 2];
+        }
+        if (valid && l16 == 0)
+            for (int m = 0; m < a.M; ++m) {
+                const float me = bf2f(f2bf(acc[m])), pa = bf2f(f2bf(other[m]));
+                float v = me;
+                if (rot) v = (d & 1) ? pa * s + me * c : me * c - pa * s;
+                const u16 o = f2bf(v);
+                if (hh < H) reinterpret_cast<u16*>(a.y)[(long)m * a.ldy + n] = o;
+                else if (p < a.Lmax) {
+                    const bool isk = hh < H + Hkv;
+                    const int hk = isk ? hh - H : hh - H - Hkv;
+                    u16* cache = reinterpret_cast<u16*>(isk ? a.kc : a.vc);
+                    cache[(((long)m * Hkv + hk) * a.Lmax + p) * D + d] = o;
+                }
+            }
+    }
+}
+
+}  // namespace gv
+}  // namespace bpe
+
+using namespace bpe::gv;
+
+size_t gemv_lds_bytes(int M, int K) {
+    const int MM = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : 8;
+    return (size_t)MM * K * 2;
+}
+
+bool gemv_ok(int M, int K) { return M >= 1 && M <= 8 && K % 8 == 0 && gemv_lds_bytes(M, K) <= 160 * 1024; }
+
+template <int MM, int EPI>
+static void launch_mm(const GemvArgs& a, int grid, size_t lds, hipStream_t s) {
+    if (lds > 64 * 1024)
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<MM, EPI>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    gemv_kernel<MM, EPI><<<grid, 256, lds, s>>>(a);
+}
+
+template <int EPI>
+static void launch_epi(const GemvArgs& a, int grid, size_t lds, hipStream_t s) {
+    if (a.M <= 1) launch_mm<1, EPI>(a, grid, lds, s);
+    else if (a.M <= 2) launch_mm<2, EPI>(a, grid, lds, s);
+    else if (a.M <= 4) launch_mm<4, EPI>(a, grid, lds, s);
+    else launch_mm<8, EPI>(a, grid, lds, s);
+}
+
+void launch_gemv(const GemvArgs& a, int epi, hipStream_t s) {
+    const size_t lds = gemv_lds_bytes(a.M, a.K);
+    if (epi == 1) launch_epi<1>(a, (a.N / 2 + 7) / 8, lds, s);
+    else if (epi == 2) launch_epi<2>(a, (a.N + 15) / 16, lds, s);
+    else launch_epi<0>(a, (a.N + 15) / 16, lds, s);
+}

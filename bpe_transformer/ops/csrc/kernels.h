@@ -108,6 +108,30 @@ void launch_decode_attn(const void* q, const void* k, const void* v, float* part
 void launch_kv_append(const void* qkv, long ld, void* qo, void* Kc, void* Vc, const float* cosT, const float* sinT,
                       const int* pos, int B, int T, int H, int Hkv, int D, int Lmax, hipStream_t s);
 
+// decode_gemv.hip (M <= 8 token rows; epi 0 plain, 1 SwiGLU over [W1; W3], 2 fused QKV + RoPE + KV-cache write)
+struct GemvArgs {
+    const __bf16* x;   // input rows [M][K] (row stride ldx)
+    const __bf16* xd;  // optional delta added to x before the norm (residual add), same layout
+    long ldx;
+    const __bf16* ln;  // optional RMSNorm weight [K]
+    float eps;
+    __bf16* xsum;      // optional: x + xd written here [M][K] (workgroup 0)
+    const __bf16* W;   // weight [N][K] (row stride ldw)
+    long ldw;
+    int N, K, M;
+    __bf16* y;         // output [M][N] (epi 1: [M][N/2]; epi 2: q part [M][H*D]), row stride ldy
+    long ldy;
+    int H, Hkv, D, Lmax;  // epi 2 only
+    const float* cosT;
+    const float* sinT;
+    const int* pos;
+    __bf16* kc;
+    __bf16* vc;
+};
+size_t gemv_lds_bytes(int M, int K);
+bool gemv_ok(int M, int K);
+void launch_gemv(const GemvArgs& a, int epi, hipStream_t s);
+
 size_t fa_fwd_lds_bytes(int D);
 size_t fa_bwd_lds_bytes(int D);
 void launch_fa_fwd(const FaArgs& a, hipStream_t s);

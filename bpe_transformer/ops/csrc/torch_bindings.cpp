@@ -536,9 +536,100 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& kc, const at::Tens
     return out;
 }
 
+// Skinny-GEMM prologue / shape checks shared by decode_gemv and decode_qkv; returns the residual-sum output
+at::Tensor gemv_setup(GemvArgs& a, const at::Tensor& x, const c10::optional<at::Tensor>& xd,
+                      const c10::optional<at::Tensor>& ln, double eps, const at::Tensor& w) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "decode gemv: bf16 required");
+    TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "decode gemv: x must be [M, K] row-major");
+    TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0 && w.size(1) == x.size(1),
+                "decode gemv: weight must be row-major [N, K]");
+    const int M = (int)x.size(0), K = (int)x.size(1);
+    TORCH_CHECK(gemv_ok(M, K), "decode gemv: 1 <= M <= 8 rows and K a multiple of 8 required");
+    check_aligned(x, "x");
+    check_aligned(w, "w");
+    a = GemvArgs{};
+    a.x = (const __bf16*)x.data_ptr();
+    a.ldx = x.stride(0);
+    a.W = (const __bf16*)w.data_ptr();
+    a.ldw = w.stride(0);
+    a.N = (int)w.size(0);
+    a.K = K;
+    a.M = M;
+    a.eps = (float)eps;
+    at::Tensor xsum = at::empty({0}, x.options());  // empty unless a residual sum is produced
+    if (xd.has_value() && xd->defined()) {
+        TORCH_CHECK(xd->sizes() == x.sizes() && xd->strides() == x.strides() && xd->scalar_type() == x.scalar_type(),
+                    "decode gemv: xd must match x");
+        check_aligned(*xd, "xd");
+        a.xd = (const __bf16*)xd->data_ptr();
+        xsum = at::empty({M, K}, x.options());
+        a.xsum = (__bf16*)xsum.data_ptr();
+    }
+    if (ln.has_value() && ln->defined()) {
+        TORCH_CHECK(ln->numel() == K && ln->is_contiguous() && ln->scalar_type() == at::kBFloat16,
+                    "decode gemv: norm weight must be bf16 [K]");
+        a.ln = (const __bf16*)ln->data_ptr();
+    }
+    return xsum;
+}
+
+// y = RMSNorm(x (+ xd)) W^T (epi 0) or SwiGLU over [W1; W3] (epi 1); returns (y, x + xd or an empty tensor)
+std::tuple<at::Tensor, at::Tensor> decode_gemv(const at::Tensor& x, const c10::optional<at::Tensor>& xd,
+                                               const c10::optional<at::Tensor>& ln, double eps, const at::Tensor& w,
+                                               int64_t epi) {
+    TORCH_CHECK(epi == 0 || epi == 1, "decode_gemv: epi must be 0 (plain) or 1 (SwiGLU)");
+    GemvArgs a;
+    auto xsum = gemv_setup(a, x, xd, ln, eps, w);
+    TORCH_CHECK(epi == 0 || a.N % 2 == 0, "decode_gemv: SwiGLU needs an even number of rows");
+    DevGuard g(x.device());
+    auto y = at::empty({(int64_t)a.M, epi == 1 ? a.N / 2 : a.N}, x.options());
+    a.y = (__bf16*)y.data_ptr();
+    a.ldy = y.stride(0);
+    launch_gemv(a, (int)epi, cur_stream());
+    return {y, xsum};
+}
+
+// fused QKV projection for one new token per sequence: q (roped) out, K (roped) / V written into the caches
+std::tuple<at::Tensor, at::Tensor> decode_qkv(const at::Tensor& x, const c10::optional<at::Tensor>& xd,
+                                              const c10::optional<at::Tensor>& ln, double eps, const at::Tensor& w,
+                                              at::Tensor kc, at::Tensor vc, const at::Tensor& cos,
+                                              const at::Tensor& sin, const at::Tensor& pos, int64_t H, bool use_rope) {
+    GemvArgs a;
+    auto xsum = gemv_setup(a, x, xd, ln, eps, w);
+    const int64_t B = a.M, Hkv = kc.size(1), Lmax = kc.size(2), D = kc.size(3);
+    check_cache(kc, B, Hkv, "k_cache");
+    check_cache(vc, B, Hkv, "v_cache");
+    TORCH_CHECK(vc.sizes() == kc.sizes(), "decode_qkv: k / v cache shapes differ");
+    TORCH_CHECK(a.N == (H + 2 * Hkv) * D && D % 2 == 0, "decode_qkv: weight rows must be (H + 2*Hkv) * D");
+    check_pos(pos);
+    if (use_rope)
+        TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.is_contiguous() && sin.is_contiguous() &&
+                        cos.size(0) >= Lmax && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(),
+                    "decode_qkv: rope tables must be fp32 [>=Lmax, D/2]");
+    DevGuard g(x.device());
+    auto q = at::empty({B, H * D}, x.options());
+    a.y = (__bf16*)q.data_ptr();
+    a.ldy = q.stride(0);
+    a.H = (int)H;
+    a.Hkv = (int)Hkv;
+    a.D = (int)D;
+    a.Lmax = (int)Lmax;
+    a.cosT = use_rope ? cos.data_ptr<float>() : nullptr;
+    a.sinT = use_rope ? sin.data_ptr<float>() : nullptr;
+    a.pos = pos.data_ptr<int>();
+    a.kc = (__bf16*)kc.data_ptr();
+    a.vc = (__bf16*)vc.data_ptr();
+    launch_gemv(a, 2, cur_stream());
+    return {q, xsum};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(bpe_hip, m) {
+    m.def("decode_gemv(Tensor x, Tensor? xd, Tensor? ln, float eps, Tensor w, int epi) -> (Tensor, Tensor)");
+    m.def("decode_qkv(Tensor x, Tensor? xd, Tensor? ln, float eps, Tensor w, Tensor(a!) k_cache, "
+          "Tensor(b!) v_cache, Tensor cos, Tensor sin, Tensor pos, int H, bool rope) -> (Tensor, Tensor)");
     m.def("kv_append(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor cos, Tensor sin, Tensor pos, int B, "
           "int T, int H, bool rope) -> Tensor");
     m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor pos, int H, float scale) -> Tensor");
@@ -599,4 +690,6 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("fa_bwd", &fa_bwd);
     m.impl("kv_append", &kv_append);
     m.impl("decode_attn", &decode_attn);
+    m.impl("decode_gemv", &decode_gemv);
+    m.impl("decode_qkv", &decode_qkv);
 }

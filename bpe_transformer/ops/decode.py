@@ -8,6 +8,9 @@ whole prefix for every new token.
   sequence, applies RoPE at their absolute positions (``pos .. pos+T-1``, with
   ``pos`` a device int32 tensor), writes K (roped) and V into the caches
   ``[B, Hkv, Lmax, D]``, and returns the roped queries ``[B*T, H*D]``.
+* :func:`decode_gemv` / :func:`decode_qkv` are the M <= 8 skinny projections of
+  the decode step with RMSNorm / residual-add prologues and SwiGLU / RoPE +
+  cache-write epilogues (``csrc/decode_gemv.hip``).
 * :func:`decode_attention` is single-token attention of ``q [B, H*D]`` over the
   first ``pos + 1`` cache rows (split-K "flash-decoding" with a combine pass).
 
@@ -72,3 +75,42 @@ def decode_attention_reference(q, k_cache, v_cache, pos, n_heads, scale=None) ->
     s = torch.einsum("bhgd,bhld->bhgl", qf, k) * scale
     o = torch.einsum("bhgl,bhld->bhgd", F.softmax(s, -1), v)
     return o.reshape(B, H * D).to(q.dtype)
+
+
+def decode_gemv(x: Tensor, w: Tensor, xd: Tensor | None = None, ln: Tensor | None = None, eps: float = 1e-5,
+                swiglu: bool = False) -> tuple[Tensor, Tensor | None]:
+    """Skinny projection of ``M <= 8`` decode rows (``csrc/decode_gemv.hip``): ``h = RMSNorm(x + xd) * ln``
+    (each part optional), then ``y = h W^T`` or, with ``swiglu``, ``silu(h W1^T) * (h W3^T)`` for
+    ``w = [W1; W3]``.  Returns ``(y, x + xd)`` (the second is ``None`` without ``xd``)."""
+    if x.is_cuda:
+        y, s = ops().decode_gemv(x, xd, ln, eps, w, 1 if swiglu else 0)
+        return y, (s if xd is not None else None)
+    return decode_gemv_reference(x, w, xd, ln, eps, swiglu)
+
+
+def decode_gemv_reference(x, w, xd=None, ln=None, eps=1e-5, swiglu=False):
+    """fp32 oracle with the kernel's rounding points (bf16 residual sum, bf16 GEMM outputs before SwiGLU)."""
+    s = (x.float() + xd.float()).to(x.dtype) if xd is not None else x
+    h = s.float()
+    if ln is not None:
+        h = (h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + eps) * ln.float()).to(x.dtype).float()
+    y = (h @ w.float().t()).to(x.dtype)
+    if swiglu:
+        g, u = y.float().chunk(2, dim=-1)
+        y = (g * torch.sigmoid(g) * u).to(x.dtype)
+    return y, (s if xd is not None else None)
+
+
+def decode_qkv(x: Tensor, w: Tensor, k_cache: Tensor, v_cache: Tensor, cos: Tensor | None, sin: Tensor | None,
+               pos: Tensor, n_heads: int, xd: Tensor | None = None, ln: Tensor | None = None,
+               eps: float = 1e-5) -> tuple[Tensor, Tensor | None]:
+    """Fused decode QKV: ``qkv = RMSNorm(x + xd) W^T`` for one new token per sequence, RoPE at the device-side
+    position, K / V written into the caches; returns ``(q [M, H*D], x + xd)``."""
+    if x.is_cuda:
+        use_rope = cos is not None
+        c = cos if use_rope else x.new_empty(0, dtype=torch.float32)
+        sn = sin if use_rope else x.new_empty(0, dtype=torch.float32)
+        q, s = ops().decode_qkv(x, xd, ln, eps, w, k_cache, v_cache, c, sn, pos, n_heads, use_rope)
+        return q, (s if xd is not None else None)
+    qkv, s = decode_gemv_reference(x, w, xd, ln, eps)
+    return kv_append_reference(qkv, k_cache, v_cache, cos, sin, pos, x.shape[0], 1, n_heads), s

@@ -105,3 +105,23 @@ def test_kv_append_and_decode_reference_match_attention(rope):
     pos.fill_(S - 1)
     o = dec.decode_attention(q.view(B, S, H * D)[:, -1].contiguous(), kc, vc, pos, H, 1.0 / math.sqrt(D))
     assert torch.allclose(o, want[:, -1], atol=1e-5)
+
+
+def test_decode_qkv_oracle_matches_kv_append():
+    """CPU oracle of the fused decode QKV equals RMSNorm -> projection -> kv_append."""
+    torch.manual_seed(0)
+    M, K, H, Hkv, D, Lmax = 2, 64, 4, 2, 16, 12
+    x, xd = torch.randn(M, K), torch.randn(M, K)
+    ln = 1 + 0.1 * torch.randn(K)
+    w = torch.randn((H + 2 * Hkv) * D, K)
+    cos, sin = rope_tables(D, Lmax, 10000.0)
+    pos = torch.tensor([5], dtype=torch.int32)
+    kc, vc = torch.zeros(M, Hkv, Lmax, D), torch.zeros(M, Hkv, Lmax, D)
+    q, s = dec.decode_qkv(x, w, kc, vc, cos, sin, pos, H, xd, ln)
+    assert torch.allclose(s, x + xd)
+    hn = s * torch.rsqrt(s.pow(2).mean(-1, keepdim=True) + 1e-5) * ln
+    k2, v2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    q2 = dec.kv_append_reference(hn @ w.t(), k2, v2, cos, sin, pos, M, 1, H)
+    assert torch.allclose(q, q2, atol=1e-5) and torch.allclose(kc, k2, atol=1e-5) and torch.equal(vc, v2)
+    y, _ = dec.decode_gemv(x, torch.randn(2 * 8, K), swiglu=True)
+    assert y.shape == (M, 8)

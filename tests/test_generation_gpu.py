@@ -118,3 +118,65 @@ def test_generate_uses_cache_on_gpu(gpu_device):
     ref = copy.deepcopy(model)
     first = ref.generate(prompt, 1, temperature=0.0, use_cache=False)
     assert torch.equal(out[:, 8], first[:, 8])
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("K,N", [(256, 1000), (768, 2304), (2048, 512)])
+@pytest.mark.parametrize("prologue", [False, True])
+@pytest.mark.parametrize("swiglu", [False, True])
+def test_decode_gemv_matches_reference(gpu_device, M, K, N, prologue, swiglu):
+    torch.manual_seed(M * 7 + K)
+    x = torch.randn(M, K).bfloat16()
+    w = (torch.randn(N, K) / math.sqrt(K)).bfloat16()
+    xd = torch.randn(M, K).bfloat16() if prologue else None
+    ln = (1 + 0.1 * torch.randn(K)).bfloat16() if prologue else None
+    y_ref, s_ref = dec.decode_gemv_reference(x, w, xd, ln, 1e-5, swiglu)
+    g = lambda t: None if t is None else t.to(gpu_device)  # noqa: E731
+    y, s = dec.decode_gemv(g(x), g(w), g(xd), g(ln), 1e-5, swiglu)
+    torch.cuda.synchronize()
+    assert y.shape == y_ref.shape
+    assert rel(y.cpu(), y_ref) < 2e-2, rel(y.cpu(), y_ref)
+    if prologue:
+        assert torch.equal(s.cpu(), s_ref)
+
+
+@pytest.mark.parametrize("D,G", [(64, 1), (64, 4), (128, 2)])
+@pytest.mark.parametrize("rope", [True, False])
+def test_decode_qkv_matches_reference(gpu_device, D, G, rope):
+    torch.manual_seed(D + G)
+    M, Hkv, Lmax, p0, K = 4, 2, 48, 17, 512
+    H = Hkv * G
+    x = torch.randn(M, K).bfloat16()
+    xd = torch.randn(M, K).bfloat16()
+    ln = (1 + 0.1 * torch.randn(K)).bfloat16()
+    w = (torch.randn((H + 2 * Hkv) * D, K) / math.sqrt(K)).bfloat16()
+    cos, sin = rope_tables(D, Lmax, 10000.0) if rope else (None, None)
+    pos = torch.tensor([p0], dtype=torch.int32)
+    kc = torch.zeros(M, Hkv, Lmax, D, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    q_ref, s_ref = dec.decode_qkv(x, w, kc, vc, cos, sin, pos, H, xd, ln)
+    g = lambda t: None if t is None else t.to(gpu_device)  # noqa: E731
+    kg, vg = torch.zeros_like(kc, device=gpu_device), torch.zeros_like(vc, device=gpu_device)
+    q, s = dec.decode_qkv(g(x), g(w), kg, vg, g(cos), g(sin), g(pos), H, g(xd), g(ln))
+    torch.cuda.synchronize()
+    assert rel(q.cpu(), q_ref) < 2e-2
+    assert rel(kg.cpu(), kc) < 2e-2 and rel(vg.cpu(), vc) < 2e-2
+    assert torch.equal(s.cpu(), s_ref)
+    assert kg[:, :, :p0].abs().sum() == 0 and kg[:, :, p0 + 1 :].abs().sum() == 0
+
+
+def test_gemv_decode_matches_library_decode(gpu_device, monkeypatch):
+    """The fused skinny-GEMM decode step (batch <= 8) agrees with the hipBLASLt + elementwise-kernel step."""
+    from bpe_transformer.models import generation
+
+    model = _bf16_model(gpu_device, num_kv_heads=2)
+    ids = torch.randint(0, 1000, (4, 24), device=gpu_device)
+    outs = []
+    for cap in (8, 0):
+        monkeypatch.setattr(generation, "_GEMV_MAX_BATCH", cap)
+        sess = DecodeSession(model, 4, max_len=32, use_graph=True)
+        with torch.no_grad():
+            sess.prefill(ids[:, :16])
+            outs.append([sess.decode(ids[:, t]) for t in range(16, 24)])
+    for a, b in zip(*outs):
+        assert rel(a, b) < 2e-2, rel(a, b)
