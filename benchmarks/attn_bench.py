@@ -20,11 +20,12 @@ def main():
     ap.add_argument("--kv-heads", type=int, default=None)
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-rope", action="store_true", help="plain attention (isolates the fused-RoPE cost)")
     a = ap.parse_args()
     B, S, H, D = a.batch, a.seq, a.heads, a.dim
     Hkv = a.kv_heads or H
     qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-    cos, sin = R.rope_tables(D, S, 10000.0, device="cuda")
+    cos, sin = (None, None) if a.no_rope else R.rope_tables(D, S, 10000.0, device="cuda")
     do = torch.randn(B * S, H * D, device="cuda", dtype=torch.bfloat16)
     for _ in range(3):
         o = ops.flash_attention_qkv(qkv, B, S, H, Hkv, D, cos, sin, True)
@@ -44,7 +45,7 @@ def main():
     tf /= a.iters
     tb /= a.iters
     fl = 4.0 * B * H * S * S * D / 2
-    print(json.dumps({"shape": [B, S, H, Hkv, D], "fwd_ms": round(tf, 4), "bwd_ms": round(tb, 4),
+    print(json.dumps({"shape": [B, S, H, Hkv, D], "rope": not a.no_rope, "fwd_ms": round(tf, 4), "bwd_ms": round(tb, 4),
                       "fwd_tflops": round(fl / tf / 1e9, 1), "bwd_tflops": round(2.5 * fl / tb / 1e9, 1)}))
 
 
