@@ -260,8 +260,9 @@ class DecodeSession:
 
     def _decode_gemv(self, ids: Tensor) -> Tensor:
         """Decode step for batch <= 8 on the fused skinny-GEMM kernels (``csrc/decode_gemv.hip``): per layer
-        qkv (+RMSNorm, +RoPE, +cache write) -> decode attention -> Wo -> [W1; W3] (+residual add, +RMSNorm,
-        +SwiGLU) -> W2; the residual add of W2's output is folded into the next layer's QKV prologue."""
+        qkv (+RMSNorm, +RoPE, +cache write) -> split-K decode attention -> Wo (+ the split combine) -> [W1; W3]
+        (+residual add, +RMSNorm, +SwiGLU) -> W2; the residual add of W2's output is folded into the next layer's
+        QKV prologue: 5 launches per layer."""
         from ..ops._ext import ops as hip
 
         h = hip()
@@ -278,8 +279,8 @@ class DecodeSession:
             q, s = h.decode_qkv(xr, xd, ln1, eps, wqkv, kc[li], vc[li], cos, sin, pos, H, use_rope)
             if xd is not None:
                 xr = s
-            o = h.decode_attn(q, kc[li], vc[li], pos, H, scale)
-            g1, _ = h.decode_gemv(o, None, None, 0.0, wo, 0)
+            part = h.decode_attn(q, kc[li], vc[li], pos, H, scale, False)
+            g1 = h.decode_attn_proj(part, wo)  # the flash-decoding combine runs in Wo's prologue
             a, xr = h.decode_gemv(xr, g1, ln2, eps, w13, 1)
             xd, _ = h.decode_gemv(a, None, None, 0.0, w2, 0)
         fin = m.ln_final

@@ -18,7 +18,10 @@
 //   3. o[g][d] = sum_t p[g][t] V[t][d]: thread = (key partition, 8-wide d vector), 16-byte V loads; partitions
 //      are reduced inside the wave with lane shuffles, then across the 4 waves through LDS;
 //   4. the partial (o, m, l) of every (b, h, chunk) goes to fp32 scratch; a combine kernel merges the chunks
-//      (flash-decoding) and writes bf16.  Chunks past the valid length write m = -inf and are skipped.
+//      (flash-decoding) and writes bf16.  Chunks past the valid length write m = -inf and are skipped.  The
+//      small-batch decode step skips the combine launch: the output projection's prologue merges the partials
+//      (decode_gemv.hip, GemvArgs::part).
+// All of a chunk's K and V loads are issued at kernel entry (register-resident, <= 128 VGPRs at D = 128).
 #include "common.h"
 #include "kernels.h"
 
@@ -54,24 +57,38 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(const __bf16* __restri
         return;
     }
     const int n = min(CH, L - s0);
+    const long kvbase = ((long)bk * Lmax + s0) * D;
+    // every K and V load of the chunk is issued up front (latency-bound at small batch: the q staging, the
+    // score reductions and the softmax run while they are in flight)
+    const bool ok = tid < n;
+    u16x8 kr[DV];
+    {
+        const u16x8* kp = reinterpret_cast<const u16x8*>(Kc + kvbase + (long)tid * D);
+#pragma unroll
+        for (int v = 0; v < DV; ++v) kr[v] = ok ? kp[v] : u16x8{};
+    }
+    const int dv = tid % DV, kp = tid / DV;
+    u16x8 vr[CH / KP];
+#pragma unroll
+    for (int j = 0; j < CH / KP; ++j) {
+        const int t = kp + KP * j;
+        vr[j] = t < n ? *reinterpret_cast<const u16x8*>(Vc + kvbase + (long)t * D + dv * 8) : u16x8{};
+    }
     // query rows of the G heads -> LDS (fp32, pre-scaled)
     for (int e = tid; e < G * D; e += 256) {
         const int g = e / D, d = e % D;
         qs[g][d] = bf2f(reinterpret_cast<const u16*>(q)[((long)b * H + hk * G + g) * D + d]) * scale;
     }
     __syncthreads();
-    const long kvbase = ((long)bk * Lmax + s0) * D;
     // 1. scores
     {
-        const bool ok = tid < n;
         float s[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) s[g] = 0.f;
         if (ok) {
-            const u16x8* kp = reinterpret_cast<const u16x8*>(Kc + kvbase + (long)tid * D);
-#pragma unroll 4
+#pragma unroll
             for (int v = 0; v < DV; ++v) {
-                const u16x8 t = kp[v];
+                const u16x8 t = kr[v];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float kx = bf2f(t[j]);
@@ -102,14 +119,16 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(const __bf16* __restri
         __syncthreads();  // red[] reused by the next head
     }
     // 3. o[g][d] = sum_t p[g][t] V[t][d]; thread = (key partition kp, vector dv)
-    const int dv = tid % DV, kp = tid / DV;
     float acc[G][8];
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-    for (int t = kp; t < n; t += KP) {
-        const u16x8 vv = *reinterpret_cast<const u16x8*>(Vc + kvbase + (long)t * D + dv * 8);
+#pragma unroll
+    for (int jj = 0; jj < CH / KP; ++jj) {
+        const int t = kp + KP * jj;
+        if (t >= n) break;
+        const u16x8 vv = vr[jj];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const float p = ps[g][t];
@@ -229,7 +248,7 @@ static void launch_d(const void* q, const void* k, const void* v, float* part, v
         default: DEC(8); break;
     }
 #undef DEC
-    decode_combine_kernel<D><<<B * H, D, 0, s>>>(part, (__bf16*)out, ns);
+    if (out != nullptr) decode_combine_kernel<D><<<B * H, D, 0, s>>>(part, (__bf16*)out, ns);
 }
 
 void launch_decode_attn(const void* q, const void* k, const void* v, float* part, void* out, const int* pos, int B,

@@ -13,8 +13,12 @@
 // SwiGLU / RoPE), so decode logits agree with the model's forward pass.
 //
 // Mapping (wave64): a 256-thread workgroup owns 16 weight rows, 4 per wave, 16 lanes per row; lane l of a row
-// reads 16-byte W vectors l, l + 16, ... (coalesced 256 B per row per step, 4 loads in flight) and the matching
-// normalized-input vectors from LDS; the 16 partial dots are reduced with xor shuffles inside the row's lanes.
+// reads 16-byte W vectors l, l + 16, ... (coalesced 256 B per row per step) and the matching normalized-input
+// vectors from LDS; the 16 partial dots are reduced with xor shuffles inside the row's lanes.  The first 8 W
+// vectors of each lane (the whole row for K <= 1024) are loaded before the prologue, so the weight stream's
+// latency overlaps the input read / normalization; the rest streams 4 vectors in flight.
+// Prologue variant (GemvArgs::part): the input rows are the split-K decode attention's partial (o, m, l)
+// triples, merged here -- the output projection absorbs the flash-decoding combine launch.
 #include "common.h"
 #include "kernels.h"
 
@@ -25,16 +29,67 @@ constexpr int LPR = 16;  // lanes per weight row
 constexpr int RPW = 4;   // rows per wave
 constexpr int UNR = 4;   // W vectors in flight per lane
 
+constexpr int PF = 8;     // W vectors per lane issued before the prologue (all of a row for K <= 1024)
+
 template <int MM, int EPI>
 __global__ void __launch_bounds__(256) gemv_kernel(const GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) u16 hs[];  // [MM][K] normalized input rows (bf16)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int K = a.K, nv = K / 8;
+    // ---- this lane's weight row (4 rows per wave, 16 lanes per row)
+    const int slot = lane / LPR, l16 = lane % LPR;
+    const int wslot = wv * RPW + slot;  // row slot within the workgroup (0..15)
+    int n, j = 0;
+    bool valid;
+    if constexpr (EPI == 1) {  // slots (2s, 2s+1) = rows (j, F + j) of logical output column j
+        const int F = a.N / 2;
+        j = blockIdx.x * 8 + wslot / 2;
+        valid = j < F;
+        n = (wslot & 1) ? F + j : j;
+    } else {
+        n = blockIdx.x * 16 + wslot;
+        valid = n < a.N;
+    }
+    const u16* wr = reinterpret_cast<const u16*>(a.W) + (long)(valid ? n : 0) * a.ldw;
+    // the first PF weight vectors are in flight while the prologue reads and normalizes the input rows: the
+    // decode step is latency-bound, and the weight stream does not depend on the prologue
+    u16x8 wp[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+        const int i = l16 + LPR * u;
+        wp[u] = (valid && i < nv) ? *reinterpret_cast<const u16x8*>(wr + 8 * i) : u16x8{};
+    }
     // ---- prologue: wave w normalizes input rows w, w + 4, ...
     for (int m = wv; m < MM; m += 4) {
         u16* hr = hs + (long)m * K;
         if (m >= a.M) {
             for (int i = lane; i < nv; i += 64) *reinterpret_cast<u16x8*>(hr + 8 * i) = u16x8{};
+            continue;
+        }
+        if (a.part != nullptr) {
+            // input row = the split-K decode attention's partials merged (flash-decoding combine): column k is
+            // head k / D, dim k % D; rounding matches decode_combine_kernel
+            const int D = a.D, ns = a.nsplit;
+            for (int i = lane; i < nv; i += 64) {
+                const int h = (8 * i) / D, d0 = (8 * i) % D;
+                const float* pb = a.part + ((long)m * a.H + h) * ns * (D + 2);
+                float mx = -INFINITY;
+                for (int sp = 0; sp < ns; ++sp) mx = fmaxf(mx, pb[sp * (D + 2) + D]);
+                float ls = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                for (int sp = 0; sp < ns; ++sp) {
+                    const float* pr = pb + sp * (D + 2);
+                    const float ms = pr[D];
+                    if (ms == -INFINITY) continue;
+                    const float c = __expf(ms - mx);
+                    ls += c * pr[D + 1];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] += c * pr[d0 + e];
+                }
+                u16x8 hv;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) hv[e] = f2bf(ls > 0.f ? o[e] / ls : 0.f);
+                *reinterpret_cast<u16x8*>(hr + 8 * i) = hv;
+            }
             continue;
         }
         float ss = 0.f;
@@ -65,25 +120,22 @@ __global__ void __launch_bounds__(256) gemv_kernel(const GemvArgs a) {
     }
     __syncthreads();
     // ---- main loop: 4 rows per wave, 16 lanes per row
-    const int slot = lane / LPR, l16 = lane % LPR;
-    const int wslot = wv * RPW + slot;  // row slot within the workgroup (0..15)
-    int n, j = 0;
-    bool valid;
-    if constexpr (EPI == 1) {  // slots (2s, 2s+1) = rows (j, F + j) of logical output column j
-        const int F = a.N / 2;
-        j = blockIdx.x * 8 + wslot / 2;
-        valid = j < F;
-        n = (wslot & 1) ? F + j : j;
-    } else {
-        n = blockIdx.x * 16 + wslot;
-        valid = n < a.N;
-    }
     float acc[MM];
 #pragma unroll
     for (int m = 0; m < MM; ++m) acc[m] = 0.f;
     if (valid) {
-        const u16* wr = reinterpret_cast<const u16*>(a.W) + (long)n * a.ldw;
-        for (int i0 = l16; i0 < nv; i0 += LPR * UNR) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int i = l16 + LPR * u;
+            if (i >= nv) break;
+#pragma unroll
+            for (int m = 0; m < MM; ++m) {
+                const u16x8 hv = *reinterpret_cast<const u16x8*>(hs + (long)m * K + 8 * i);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[m] += bf2f(wp[u][e]) * bf2f(hv[e]);
+            }
+        }
+        for (int i0 = l16 + LPR * PF; i0 < nv; i0 += LPR * UNR) {
             u16x8 w[UNR];
 #pragma unroll
             for (int u = 0; u < UNR; ++u) {

@@ -127,6 +127,8 @@ struct GemvArgs {
     const int* pos;
     __bf16* kc;
     __bf16* vc;
+    const float* part;  // optional prologue: x = merged decode-attention partials [M][H][nsplit][D + 2] (H, D)
+    int nsplit;
 };
 size_t gemv_lds_bytes(int M, int K);
 bool gemv_ok(int M, int K);

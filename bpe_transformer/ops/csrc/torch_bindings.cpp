@@ -515,8 +515,9 @@ at::Tensor kv_append(const at::Tensor& qkv, at::Tensor kc, at::Tensor vc, const 
 }
 
 // q [B, H*D] (roped) attends to the first *pos + 1 cache rows -> [B, H*D]
+// combine = false: return the split partials [B, H, nsplit, D + 2] (o, m, l) for decode_attn_proj instead
 at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& pos,
-                       int64_t H, double scale) {
+                       int64_t H, double scale, bool combine) {
     const int64_t B = kc.size(0), Hkv = kc.size(1), Lmax = kc.size(2), D = kc.size(3);
     TORCH_CHECK(decode_attn_ok((int)H, (int)Hkv, (int)D),
                 "decode_attn: head dim 64/128 and H / Hkv in {1, 2, 4, 8} required");
@@ -529,11 +530,12 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& kc, const at::Tens
     check_pos(pos);
     DevGuard g(q.device());
     const int ns = decode_attn_splits((int)Lmax);
-    auto part = at::empty({B * H * ns * (D + 2)}, q.options().dtype(at::kFloat));
-    auto out = at::empty({B, H * D}, q.options());
-    launch_decode_attn(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), part.data_ptr<float>(), out.data_ptr(),
-                       pos.data_ptr<int>(), (int)B, (int)H, (int)Hkv, (int)D, (int)Lmax, (float)scale, cur_stream());
-    return out;
+    auto part = at::empty({B, H, ns, D + 2}, q.options().dtype(at::kFloat));
+    auto out = combine ? at::empty({B, H * D}, q.options()) : at::Tensor();
+    launch_decode_attn(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), part.data_ptr<float>(),
+                       combine ? out.data_ptr() : nullptr, pos.data_ptr<int>(), (int)B, (int)H, (int)Hkv, (int)D,
+                       (int)Lmax, (float)scale, cur_stream());
+    return combine ? out : part;
 }
 
 // Skinny-GEMM prologue / shape checks shared by decode_gemv and decode_qkv; returns the residual-sum output
@@ -590,6 +592,34 @@ std::tuple<at::Tensor, at::Tensor> decode_gemv(const at::Tensor& x, const c10::o
     return {y, xsum};
 }
 
+// output projection of the decode attention straight from its split partials: y = combine(part) W^T
+at::Tensor decode_attn_proj(const at::Tensor& part, const at::Tensor& w) {
+    check_cuda(part, "part");
+    TORCH_CHECK(part.scalar_type() == at::kFloat && part.dim() == 4 && part.is_contiguous(),
+                "decode_attn_proj: part must be the fp32 [B, H, nsplit, D + 2] partials of decode_attn");
+    const int64_t B = part.size(0), H = part.size(1), ns = part.size(2), D = part.size(3) - 2;
+    TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0 &&
+                    w.size(1) == H * D, "decode_attn_proj: weight must be row-major bf16 [N, H*D]");
+    TORCH_CHECK(D % 8 == 0 && gemv_ok((int)B, (int)(H * D)), "decode_attn_proj: 1 <= B <= 8 and D % 8 == 0");
+    check_aligned(w, "w");
+    DevGuard g(part.device());
+    GemvArgs a{};
+    a.part = part.data_ptr<float>();
+    a.nsplit = (int)ns;
+    a.H = (int)H;
+    a.D = (int)D;
+    a.W = (const __bf16*)w.data_ptr();
+    a.ldw = w.stride(0);
+    a.N = (int)w.size(0);
+    a.K = (int)(H * D);
+    a.M = (int)B;
+    auto y = at::empty({B, a.N}, w.options());
+    a.y = (__bf16*)y.data_ptr();
+    a.ldy = y.stride(0);
+    launch_gemv(a, 0, cur_stream());
+    return y;
+}
+
 // fused QKV projection for one new token per sequence: q (roped) out, K (roped) / V written into the caches
 std::tuple<at::Tensor, at::Tensor> decode_qkv(const at::Tensor& x, const c10::optional<at::Tensor>& xd,
                                               const c10::optional<at::Tensor>& ln, double eps, const at::Tensor& w,
@@ -632,7 +662,9 @@ TORCH_LIBRARY(bpe_hip, m) {
           "Tensor(b!) v_cache, Tensor cos, Tensor sin, Tensor pos, int H, bool rope) -> (Tensor, Tensor)");
     m.def("kv_append(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor cos, Tensor sin, Tensor pos, int B, "
           "int T, int H, bool rope) -> Tensor");
-    m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor pos, int H, float scale) -> Tensor");
+    m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor pos, int H, float scale, "
+          "bool combine=True) -> Tensor");
+    m.def("decode_attn_proj(Tensor part, Tensor w) -> Tensor");
     m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
     m.def("add_rmsnorm_fwd(Tensor x, Tensor d, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
     m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
@@ -692,4 +724,5 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("decode_attn", &decode_attn);
     m.impl("decode_gemv", &decode_gemv);
     m.impl("decode_qkv", &decode_qkv);
+    m.impl("decode_attn_proj", &decode_attn_proj);
 }

@@ -77,6 +77,55 @@ def decode_attention_reference(q, k_cache, v_cache, pos, n_heads, scale=None) ->
     return o.reshape(B, H * D).to(q.dtype)
 
 
+def decode_attention_partials(q: Tensor, k_cache: Tensor, v_cache: Tensor, pos: Tensor, n_heads: int,
+                              scale: float | None = None) -> Tensor:
+    """Split-K decode attention without the combine: fp32 ``[B, H, nsplit, D + 2]`` = (o, m, l) per 256-key chunk
+    (natural-log units; empty chunks have ``m = -inf``), consumed by :func:`decode_attn_proj`."""
+    D = k_cache.shape[-1]
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if q.is_cuda:
+        return ops().decode_attn(q.contiguous(), k_cache, v_cache, pos, n_heads, scale, False)
+    return decode_partials_reference(q, k_cache, v_cache, pos, n_heads, scale)
+
+
+def decode_partials_reference(q, k_cache, v_cache, pos, n_heads, scale=None, chunk: int = 256) -> Tensor:
+    B, Hkv, Lmax, D = k_cache.shape
+    H = n_heads
+    L = min(int(pos.reshape(-1)[0]) + 1, Lmax)
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    ns = (Lmax + chunk - 1) // chunk
+    out = torch.zeros(B, H, ns, D + 2, dtype=torch.float32, device=q.device)
+    out[..., D] = -math.inf
+    qf = q.float().view(B, Hkv, H // Hkv, D)
+    for c in range(ns):
+        s0, s1 = c * chunk, min(L, (c + 1) * chunk)
+        if s0 >= s1:
+            continue
+        s = torch.einsum("bhgd,bhld->bhgl", qf, k_cache[:, :, s0:s1].float()) * scale
+        m = s.amax(-1, keepdim=True)
+        p = torch.exp(s - m)
+        o = torch.einsum("bhgl,bhld->bhgd", p, v_cache[:, :, s0:s1].float())
+        out[:, :, c, :D] = o.reshape(B, H, D)
+        out[:, :, c, D] = m.reshape(B, H)
+        out[:, :, c, D + 1] = p.sum(-1).reshape(B, H)
+    return out
+
+
+def decode_attn_proj(part: Tensor, w: Tensor) -> Tensor:
+    """Output projection of the decode attention from its partials: ``combine(part) @ w.T`` (bf16 rounding of
+    the combined rows as in the unfused path)."""
+    if part.is_cuda:
+        return ops().decode_attn_proj(part, w)
+    B, H, _, D2 = part.shape
+    D = D2 - 2
+    m = part[..., D]
+    mx = m.amax(-1, keepdim=True)
+    c = torch.where(torch.isinf(m), torch.zeros_like(m), torch.exp(m - mx))
+    o = (c[..., None] * part[..., :D]).sum(2) / (c * part[..., D + 1]).sum(-1, keepdim=True).clamp_min(1e-30)
+    x = o.reshape(B, H * D).to(w.dtype)
+    return (x.float() @ w.float().t()).to(w.dtype)
+
+
 def decode_gemv(x: Tensor, w: Tensor, xd: Tensor | None = None, ln: Tensor | None = None, eps: float = 1e-5,
                 swiglu: bool = False) -> tuple[Tensor, Tensor | None]:
     """Skinny projection of ``M <= 8`` decode rows (``csrc/decode_gemv.hip``): ``h = RMSNorm(x + xd) * ln``

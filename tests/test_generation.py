@@ -125,3 +125,18 @@ def test_decode_qkv_oracle_matches_kv_append():
     assert torch.allclose(q, q2, atol=1e-5) and torch.allclose(kc, k2, atol=1e-5) and torch.equal(vc, v2)
     y, _ = dec.decode_gemv(x, torch.randn(2 * 8, K), swiglu=True)
     assert y.shape == (M, 8)
+
+
+def test_decode_partials_combine_to_attention():
+    """CPU oracle: merging the split-K partials (decode_attn_proj with an identity weight) equals attention."""
+    torch.manual_seed(1)
+    B, H, Hkv, D, Lmax = 2, 4, 2, 16, 600
+    q = torch.randn(B, H * D)
+    kc, vc = torch.randn(B, Hkv, Lmax, D), torch.randn(B, Hkv, Lmax, D)
+    pos = torch.tensor([530], dtype=torch.int32)
+    part = dec.decode_attention_partials(q, kc, vc, pos, H)
+    assert part.shape == (B, H, 3, D + 2)
+    eye = torch.eye(H * D)
+    got = dec.decode_attn_proj(part, eye)
+    want = dec.decode_attention_reference(q, kc, vc, pos, H)
+    assert torch.allclose(got, want, atol=1e-5)

@@ -180,3 +180,26 @@ def test_gemv_decode_matches_library_decode(gpu_device, monkeypatch):
             outs.append([sess.decode(ids[:, t]) for t in range(16, 24)])
     for a, b in zip(*outs):
         assert rel(a, b) < 2e-2, rel(a, b)
+
+
+@pytest.mark.parametrize("D,G", [(64, 1), (64, 4), (128, 2)])
+@pytest.mark.parametrize("L", [1, 300, 777])
+@pytest.mark.parametrize("B", [1, 5])
+def test_decode_attn_proj_matches_reference(gpu_device, D, G, L, B):
+    """Split-K partials -> output projection with the combine in its prologue vs the fp32 oracle."""
+    torch.manual_seed(L + G + B)
+    Hkv, Lmax, N = 2, 1024, 384
+    H = Hkv * G
+    q = torch.randn(B, H * D).bfloat16()
+    kc = torch.randn(B, Hkv, Lmax, D).bfloat16()
+    vc = torch.randn(B, Hkv, Lmax, D).bfloat16()
+    w = (torch.randn(N, H * D) / math.sqrt(H * D)).bfloat16()
+    pos = torch.tensor([L - 1], dtype=torch.int32)
+    o_ref = dec.decode_attention_reference(q.float(), kc, vc, pos, H).bfloat16()
+    y_ref = o_ref.float() @ w.float().t()
+    g = lambda t: t.to(gpu_device)  # noqa: E731
+    part = dec.decode_attention_partials(g(q), g(kc), g(vc), g(pos), H)
+    y = dec.decode_attn_proj(part, g(w))
+    torch.cuda.synchronize()
+    assert part.shape == (B, H, Lmax // 256, D + 2)
+    assert rel(y.cpu(), y_ref) < 2e-2, rel(y.cpu(), y_ref)
