@@ -264,36 +264,44 @@ static size_t last_safe_cut(std::string_view text, size_t lo = 0) {
     return std::string_view::npos;
 }
 
-static size_t first_safe_cut(std::string_view text, size_t from) {
+// A position where both halves pre-tokenize to exactly the whole text's pre-tokens: right before the LAST
+// character w of a whitespace run when w is an ASCII control space (\n \r \t \v \f) and the next character is not
+// whitespace.  In the whole text the run then always ends in a token boundary before w (the ` ?` prefixes only
+// take a ' ', and `\s+(?!\S)` stops one short of a run followed by \S); the left half's trailing run matches
+// `\s+(?!\S)` to its end, and the right half starts with `w` + non-space, which `\s+` takes alone.  Blank-line
+// separated text (".\n\nNext") cuts between the two newlines.  "Next" must not be a special token: a run that
+// ends at a special ends its segment, where `\s+(?!\S)` takes the whole run.
+static size_t first_safe_cut(std::string_view text, size_t from, const std::vector<std::string>& specials) {
     const uint8_t* s = reinterpret_cast<const uint8_t*>(text.data());
     const size_t n = text.size();
-    for (size_t p = std::max<size_t>(from, 2); p < n; ++p) {
-        const uint8_t c = s[p - 1];
+    for (size_t p = std::max<size_t>(from, 1); p + 1 < n; ++p) {
+        const uint8_t c = s[p];
         if (c != '\n' && c != '\r' && c != '\t' && c != 0x0B && c != 0x0C) continue;
-        if ((s[p] & 0xC0) == 0x80) continue;
         int l;
-        if (classify(decode(s, p, n, &l)) & C_SPACE) continue;
-        size_t q = p - 2;
-        while (q > 0 && (s[q] & 0xC0) == 0x80) --q;
-        if (classify(decode(s, q, n, &l)) & C_SPACE) continue;
+        if (classify(decode(s, p + 1, n, &l)) & C_SPACE) continue;
+        bool special_next = false;
+        for (const auto& t : specials) special_next |= text.compare(p + 1, t.size(), t) == 0;
+        if (special_next) continue;
         return p;
     }
     return std::string_view::npos;
 }
 
-// chunk boundaries for parallel processing: at special tokens if any, else at safe cuts
+// chunk boundaries for parallel processing: at safe cuts or special-token starts, whichever comes first
 static std::vector<size_t> chunk_bounds(std::string_view text, const SpecialSplitter& sp, int nchunks) {
     std::vector<size_t> b{0};
     const size_t n = text.size();
     for (int c = 1; c < nchunks; ++c) {
         size_t guess = n * (size_t)c / nchunks;
         if (guess <= b.back()) continue;
-        size_t cut = std::string_view::npos;
+        // a pre-token-safe cut after the guess; with special tokens, the start of one that begins first (or
+        // straddles the guess) instead -- a file with few or no specials still splits into nchunks pieces
+        size_t cut = first_safe_cut(text, guess, sp.toks);
         if (!sp.toks.empty()) {
-            auto r = sp.next(text, guess);
-            cut = r.first;
-        } else {
-            cut = first_safe_cut(text, guess);
+            const size_t maxlen = sp.toks[0].size();  // longest first
+            const size_t from = std::max(b.back(), guess > maxlen ? guess - maxlen : (size_t)0);
+            const size_t p = sp.next(text, from).first;
+            if (p != std::string_view::npos && (cut == std::string_view::npos || p < cut)) cut = p;
         }
         if (cut == std::string_view::npos || cut >= n) break;
         if (cut > b.back()) b.push_back(cut);
@@ -587,8 +595,9 @@ struct Encoder {
         const size_t n = text.size();
         const int nchunks = nthreads * 4;
         for (int c = 1; c < nchunks; ++c) {
-            size_t cut = first_safe_cut(text, std::max(b.back() + 1, n * (size_t)c / nchunks));
-            while (cut != std::string_view::npos && inside_special(text, cut)) cut = first_safe_cut(text, cut + 1);
+            size_t cut = first_safe_cut(text, std::max(b.back() + 1, n * (size_t)c / nchunks), specials.toks);
+            while (cut != std::string_view::npos && inside_special(text, cut))
+                cut = first_safe_cut(text, cut + 1, specials.toks);
             if (cut == std::string_view::npos) break;
             b.push_back(cut);
         }

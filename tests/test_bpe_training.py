@@ -145,3 +145,25 @@ def test_trainer_save_roundtrip(tmp_path):
     tr.save_trainer(tmp_path / "tok")
     assert load_vocab(tmp_path / "tok" / "vocab.pkl") == tr.vocab
     assert load_merges(tmp_path / "tok" / "merges.pkl") == tr.merges
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_parallel_pretoken_counts_match_regex_oracle(tmp_path, seed):
+    """Chunked multi-threaded counting (safe cuts at control-space runs, special-token starts) gives exactly the
+    GPT-2 regex's pre-tokens over the whole text: blank lines, CRLF, tabs, space runs, Unicode spaces, specials."""
+    from bpe_transformer.tokenization._native import native
+
+    rng = random.Random(seed)
+    atoms = ["word", " word", "x", "7", "!!", "'s", " ", "  ", "\n", "\n\n", "\r\n", "\t", "　", " ", "é",
+             "<|endoftext|>", "\n<|endoftext|>\n", " \n", "\n ", "\v", "\f"]
+    text = "".join(rng.choice(atoms) for _ in range(rng.randint(2000, 6000)))
+    path = tmp_path / "t.txt"
+    path.write_bytes(text.encode("utf-8"))
+    want = Counter()
+    for part in regex.split(r"<\|endoftext\|>", text):
+        want.update(m.group().encode("utf-8") for m in PAT.finditer(part))
+    for n in (1, 3, 8):
+        got = native.count_pretokens_file(str(path), ["<|endoftext|>"], n)
+        assert Counter(got) == want, n
+    assert Counter(native.count_pretokens_file(str(path), [], 8)) == Counter(
+        m.group().encode("utf-8") for m in PAT.finditer(text))
