@@ -79,6 +79,15 @@ __device__ __forceinline__ void rope8(float* x, const float* cs, const float* sn
     }
 }
 
+__device__ __forceinline__ void rope8v(float* x, const f32x4 c, const f32x4 s) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float a = x[2 * i], b = x[2 * i + 1];
+        x[2 * i] = a * c[i] - b * s[i];
+        x[2 * i + 1] = a * s[i] + b * c[i];
+    }
+}
+
 __device__ __forceinline__ u16x8 pack8(const float* x, float mul) {
     u16x8 t;
 #pragma unroll
