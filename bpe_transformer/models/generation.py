@@ -37,9 +37,21 @@ from torch import Tensor
 
 from ..ops import reference as F
 
-# decode steps of up to this many sequences run on the fused skinny-GEMM kernels; larger batches use the
-# library GEMMs (hipBLASLt), which are MFMA-efficient there
+# decode steps of up to this many sequences run on the fused skinny-GEMM kernels (they take up to 16 -- one MFMA
+# column block -- but every workgroup re-normalises all rows in its prologue, so past ~12 rows the library
+# GEMMs (hipBLASLt) win: GPT-2-small at 16 sequences 0.737 vs 0.699 ms, at 8 0.499 vs 0.672)
 _GEMV_MAX_BATCH = int(os.environ.get("BPE_DECODE_GEMV_MAX_BATCH", "8"))
+
+
+def _gemv_ok(m: int, k: int) -> bool:
+    """Mirror of ``gemv_ok`` (csrc/decode_gemv.hip): rows x K that the skinny kernels take."""
+    if m < 1 or k % 8:
+        return False
+    mfma = m <= 16 and k % 32 == 0 and m * (k + 8) * 2 + 4352 <= 160 * 1024
+    if m > 8:
+        return mfma
+    rows = 1 << (m - 1).bit_length()  # the VALU kernel's LDS holds m rounded up to 1, 2, 4 or 8 rows
+    return rows * k * 2 <= 160 * 1024 or mfma
 
 
 class KVCache:
@@ -217,7 +229,7 @@ class DecodeSession:
         self._graph = g
 
     def _forward_fast(self, ids: Tensor, prefill: bool) -> Tensor:
-        if not prefill and ids.shape[0] <= _GEMV_MAX_BATCH:
+        if not prefill and ids.shape[0] <= _GEMV_MAX_BATCH and self._gemv_fits(ids.shape[0]):
             return self._decode_gemv(ids)
         from ..ops._ext import ops as hip
 
@@ -258,8 +270,12 @@ class DecodeSession:
         pos.add_(T)
         return logits
 
+    def _gemv_fits(self, m: int) -> bool:
+        cfg = self.model.config
+        return all(_gemv_ok(m, k) for k in (cfg.d_model, self.H * self.D, self._w[0][5].shape[1]))
+
     def _decode_gemv(self, ids: Tensor) -> Tensor:
-        """Decode step for batch <= 8 on the fused skinny-GEMM kernels (``csrc/decode_gemv.hip``): per layer
+        """Decode step for batch <= 16 on the fused skinny-GEMM kernels (``csrc/decode_gemv.hip``): per layer
         qkv (+RMSNorm, +RoPE, +cache write) -> split-K decode attention -> Wo (+ the split combine) -> [W1; W3]
         (+residual add, +RMSNorm, +SwiGLU) -> W2; the residual add of W2's output is folded into the next layer's
         QKV prologue: 5 launches per layer."""

@@ -108,7 +108,7 @@ void launch_decode_attn(const void* q, const void* k, const void* v, float* part
 void launch_kv_append(const void* qkv, long ld, void* qo, void* Kc, void* Vc, const float* cosT, const float* sinT,
                       const int* pos, int B, int T, int H, int Hkv, int D, int Lmax, hipStream_t s);
 
-// decode_gemv.hip (M <= 8 token rows; epi 0 plain, 1 SwiGLU over [W1; W3], 2 fused QKV + RoPE + KV-cache write)
+// decode_gemv.hip (M <= 16 token rows; epi 0 plain, 1 SwiGLU over [W1; W3], 2 fused QKV + RoPE + KV-cache write)
 struct GemvArgs {
     const __bf16* x;   // input rows [M][K] (row stride ldx)
     const __bf16* xd;  // optional delta added to x before the norm (residual add), same layout

@@ -547,7 +547,7 @@ at::Tensor gemv_setup(GemvArgs& a, const at::Tensor& x, const c10::optional<at::
     TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0 && w.size(1) == x.size(1),
                 "decode gemv: weight must be row-major [N, K]");
     const int M = (int)x.size(0), K = (int)x.size(1);
-    TORCH_CHECK(gemv_ok(M, K), "decode gemv: 1 <= M <= 8 rows and K a multiple of 8 required");
+    TORCH_CHECK(gemv_ok(M, K), "decode gemv: 1 <= M <= 8 rows (<= 16 with K % 32 == 0) and K % 8 == 0 required");
     check_aligned(x, "x");
     check_aligned(w, "w");
     a = GemvArgs{};
@@ -600,7 +600,7 @@ at::Tensor decode_attn_proj(const at::Tensor& part, const at::Tensor& w) {
     const int64_t B = part.size(0), H = part.size(1), ns = part.size(2), D = part.size(3) - 2;
     TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0 &&
                     w.size(1) == H * D, "decode_attn_proj: weight must be row-major bf16 [N, H*D]");
-    TORCH_CHECK(D % 8 == 0 && gemv_ok((int)B, (int)(H * D)), "decode_attn_proj: 1 <= B <= 8 and D % 8 == 0");
+    TORCH_CHECK(D % 8 == 0 && gemv_ok((int)B, (int)(H * D)), "decode_attn_proj: 1 <= B <= 16 and D % 8 == 0");
     check_aligned(w, "w");
     DevGuard g(part.device());
     GemvArgs a{};

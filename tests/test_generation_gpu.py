@@ -120,7 +120,7 @@ def test_generate_uses_cache_on_gpu(gpu_device):
     assert torch.equal(out[:, 8], first[:, 8])
 
 
-@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("M", [1, 3, 8, 13, 16])
 @pytest.mark.parametrize("K,N", [(256, 1000), (768, 2304), (2048, 512)])
 @pytest.mark.parametrize("prologue", [False, True])
 @pytest.mark.parametrize("swiglu", [False, True])
@@ -170,11 +170,11 @@ def test_gemv_decode_matches_library_decode(gpu_device, monkeypatch):
     from bpe_transformer.models import generation
 
     model = _bf16_model(gpu_device, num_kv_heads=2)
-    ids = torch.randint(0, 1000, (4, 24), device=gpu_device)
+    ids = torch.randint(0, 1000, (12, 24), device=gpu_device)
     outs = []
-    for cap in (8, 0):
+    for cap in (16, 0):
         monkeypatch.setattr(generation, "_GEMV_MAX_BATCH", cap)
-        sess = DecodeSession(model, 4, max_len=32, use_graph=True)
+        sess = DecodeSession(model, 12, max_len=32, use_graph=True)
         with torch.no_grad():
             sess.prefill(ids[:, :16])
             outs.append([sess.decode(ids[:, t]) for t in range(16, 24)])
