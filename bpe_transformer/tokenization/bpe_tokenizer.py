@@ -128,6 +128,13 @@ class BPETokenizer(Tokenizer):
         n = n_workers or cpu_count()
         return self._native.encode_batch([t.encode(ENCODING_STD) for t in texts], int(n))
 
+    def _encode_batch_stream(self, texts: list[str], n_workers: int) -> Iterator[int]:
+        # ids come back as one int32 array (4 bytes per token, not a Python int each) and are handed out as
+        # ints in 64 Ki-token slices: encode_iterable's memory stays O(batch), not O(batch tokens x 40 bytes)
+        ids, _ = self._native.encode_batch_flat([t.encode(ENCODING_STD) for t in texts], int(n_workers))
+        for s in range(0, len(ids), 1 << 16):
+            yield from ids[s : s + (1 << 16)].tolist()
+
     def encode_file(self, path: Path | str, n_workers: int | None = None) -> np.ndarray:
         """Encode a whole utf-8 file with threads; returns int32 token ids."""
         return self._native.encode_file(str(path), int(n_workers or cpu_count()))
@@ -191,11 +198,9 @@ class BPETokenizer(Tokenizer):
             batch.append(piece)
             batch_chars += len(piece)
             if batch_chars >= (1 << 22):
-                for ids in self.encode_batch(batch, n_workers):
-                    yield from ids
+                yield from self._encode_batch_stream(batch, n_workers)
                 batch, batch_chars = [], 0
         if batch:
-            for ids in self.encode_batch(batch, n_workers):
-                yield from ids
+            yield from self._encode_batch_stream(batch, n_workers)
         if buf:
             yield from self.encode(buf)

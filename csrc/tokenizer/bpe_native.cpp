@@ -789,6 +789,32 @@ PYBIND11_MODULE(_bpe_native, m) {
             }
             return outs;
         })
+        // same as encode_batch, returned compactly: (int32 ids of all texts concatenated, int64 offsets [n + 1])
+        .def("encode_batch_flat", [](Encoder& e, const std::vector<std::string>& texts, int nthreads) {
+            std::vector<std::vector<int32_t>> outs(texts.size());
+            {
+                py::gil_scoped_release nogil;
+                std::atomic<size_t> nx{0};
+                auto work = [&]() {
+                    std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>> local;
+                    for (;;) {
+                        const size_t i = nx.fetch_add(1);
+                        if (i >= texts.size()) break;
+                        e.encode_into(texts[i], outs[i], local);
+                    }
+                };
+                std::vector<std::thread> th;
+                for (int t = 1; t < std::max(1, nthreads); ++t) th.emplace_back(work);
+                work();
+                for (auto& x : th) x.join();
+            }
+            std::vector<int64_t> off(texts.size() + 1, 0);
+            for (size_t i = 0; i < outs.size(); ++i) off[i + 1] = off[i] + (int64_t)outs[i].size();
+            py::array_t<int32_t> ids((size_t)off.back());
+            int32_t* dst = ids.mutable_data();
+            for (size_t i = 0; i < outs.size(); ++i) std::copy(outs[i].begin(), outs[i].end(), dst + off[i]);
+            return py::make_tuple(ids, py::array_t<int64_t>(off.size(), off.data()));
+        })
         .def("encode_file", [](Encoder& e, const std::string& path, int nthreads) {
             std::vector<int32_t> out;
             {

@@ -158,3 +158,31 @@ def test_trained_tokenizer_end_to_end(tmp_path):
     text = (FIXTURES / "tinystories_sample.txt").read_text(encoding="utf-8")
     ids = t.encode(text)
     assert t.decode(ids) == text and len(ids) < len(text.encode())
+
+
+@pytest.mark.parametrize("workers", [None, 4])
+def test_encode_iterable_memory_is_bounded(tok, workers):
+    """The reference's ``test_encode_iterable_memory_usage`` (5 MB TinyStories stream under a 1 MB rlimit; the
+    5 MB blob is not shipped) as a tracemalloc bound: streaming ~5 MB through ``encode_iterable`` while only
+    counting ids keeps Python-side peak allocation O(chunk), independent of the stream length (the serial path
+    buffers <= one line + 1 KiB, the parallel one <= one 4 MiB batch)."""
+    import tracemalloc
+
+    sample = (FIXTURES / "tinystories_sample.txt").read_text(encoding="utf-8")
+    lines = sample.splitlines(keepends=True)
+    reps = (5 << 20) // len(sample) + 1
+
+    def stream():
+        for _ in range(reps):
+            yield from lines
+
+    expect = len(tok.encode(sample))
+    tracemalloc.start()
+    try:
+        n = sum(1 for _ in tok.encode_iterable(stream(), n_workers=workers))
+        _, peak = tracemalloc.get_traced_memory()
+    finally:
+        tracemalloc.stop()
+    assert abs(n - reps * expect) <= reps  # chunk cuts may merge a boundary token differently at most once each
+    limit = (1 << 20) if workers is None else (24 << 20)
+    assert peak < limit, peak
