@@ -186,7 +186,9 @@ class BPETokenizer(Tokenizer):
         batch_chars = 0
         for chunk in iterable:
             buf += chunk
-            if len(buf) < 1024 and "\n" not in chunk:
+            # gather ~64 KiB (lines of a file object arrive one at a time) so each native call amortises its
+            # fixed cost; memory stays O(64 KiB + one chunk)
+            if len(buf) < (1 << 16):
                 continue
             cut = self._safe_cut(buf)
             if cut <= 0:
