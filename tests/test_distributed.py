@@ -160,3 +160,31 @@ def test_ddp_consistency_check_detects_divergence():
         p.join(timeout=60)
     assert res == {0: True, 1: True}
 
+
+
+def test_bench_contract_two_ranks_cpu(tmp_path):
+    """bench.py under torch.distributed.run with 2 ranks (gloo, CPU plumbing config) prints exactly one JSON line,
+    from rank 0, with the whole-job numbers the driver's scaling run reads (n_gpus, dp2, global batch)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--device", "cpu", "--model", "tinystories-17m", "--seq", "32", "--batch", "2",
+           "--steps", "2", "--warmup", "1"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1 and out["scaling"] == "weak"
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    assert out["value"] > 0 and abs(out["value"] - 2 * 2 * 2 * 32 / (out["ms_per_step"] * 2 / 1000)) < 0.02 * out["value"]
