@@ -27,6 +27,12 @@
 namespace bpe {
 namespace gv {
 
+// Weight rows are streamed once per decode step, each by one workgroup: non-temporal loads (same-box A/B,
+// GPT-2-small decode step: batch 1 0.372 -> 0.350 ms, batch 8 0.502 -> 0.490 ms)
+__device__ __forceinline__ u16x8 wload(const u16* p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
+}
+
 constexpr int LPR = 16;  // lanes per weight row
 constexpr int RPW = 4;   // rows per wave
 constexpr int UNR = 4;   // W vectors in flight per lane
@@ -59,7 +65,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const GemvArgs a) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
         const int i = l16 + LPR * u;
-        wp[u] = (valid && i < nv) ? *reinterpret_cast<const u16x8*>(wr + 8 * i) : u16x8{};
+        wp[u] = (valid && i < nv) ? wload(wr + 8 * i) : u16x8{};
     }
     // ---- prologue: wave w normalizes input rows w, w + 4, ...
     for (int m = wv; m < MM; m += 4) {
@@ -142,7 +148,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const GemvArgs a) {
 #pragma unroll
             for (int u = 0; u < UNR; ++u) {
                 const int i = i0 + LPR * u;
-                w[u] = i < nv ? *reinterpret_cast<const u16x8*>(wr + 8 * i) : u16x8{};
+                w[u] = i < nv ? wload(wr + 8 * i) : u16x8{};
             }
 #pragma unroll
             for (int u = 0; u < UNR; ++u) {
@@ -297,7 +303,7 @@ __global__ void __launch_bounds__(256) gemv_mfma_kernel(const GemvArgs a) {
 #pragma unroll
     for (int u = 0; u < MF_PF; ++u) {
         const int ks = ks0 + u;
-        wp[u] = (valid && ks < ks1) ? *reinterpret_cast<const u16x8*>(wr + 32 * ks) : u16x8{};
+        wp[u] = (valid && ks < ks1) ? wload(wr + 32 * ks) : u16x8{};
     }
     gemv_prologue_rows(a, hs, ldh, tid);
     __syncthreads();
@@ -317,7 +323,7 @@ __global__ void __launch_bounds__(256) gemv_mfma_kernel(const GemvArgs a) {
         u16x8 w4[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            w4[u] = (valid && ks + u < ks1) ? *reinterpret_cast<const u16x8*>(wr + 32 * (ks + u)) : u16x8{};
+            w4[u] = (valid && ks + u < ks1) ? wload(wr + 32 * (ks + u)) : u16x8{};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (ks + u >= ks1) break;
