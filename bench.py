@@ -60,7 +60,9 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU micro-batch (sequences)")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="per-GPU micro-batch (sequences); 128 x 1024 tokens uses a fraction of the 288 GB HBM and "
+                         "runs ~2 percent faster than 64 (library GEMM tables for both in ops/tuning)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
