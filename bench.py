@@ -33,6 +33,9 @@ METRIC = "training tokens/sec (whole node), GPT-2-small config at 1/2/4/8 MI355X
 TUNING_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bpe_transformer", "ops", "tuning")
 
 
+DEFAULT_BATCH = {"gpt2-small": 128, "llama-1.1b": 8}
+
+
 def load_gemm_tuning(spec: str, model: str, batch: int, seq: int) -> str | None:
     """Point PyTorch's TunableOp at a pre-measured hipBLASLt/rocBLAS solution table (no tuning at run time).
 
@@ -60,9 +63,10 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=128,
-                    help="per-GPU micro-batch (sequences); 128 x 1024 tokens uses a fraction of the 288 GB HBM and "
-                         "runs ~2 percent faster than 64 (library GEMM tables for both in ops/tuning)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU micro-batch (sequences); default per model: gpt2-small 128 (128 x 1024 tokens "
+                         "uses a fraction of the 288 GB HBM and runs ~2 percent faster than 64; library GEMM tables "
+                         "for both in ops/tuning), llama-1.1b 8, otherwise 8")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
@@ -75,6 +79,8 @@ def main() -> int:
                     help="cpu = the plumbing config path (fp32, no HIP kernels), e.g. --model tinystories-17m --seq 256")
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = DEFAULT_BATCH.get(args.model, 8)
 
     from bpe_transformer.data import synthetic_tokens
     from bpe_transformer.models import TransformerLM, get_preset
