@@ -86,6 +86,16 @@ __global__ void __launch_bounds__(256) add_rmsnorm_fwd_kernel(const T* __restric
     }
 }
 
+template <typename T> struct RawV;
+template <> struct RawV<__bf16> {
+    typedef u16x8 type;
+    static __device__ __forceinline__ float get(const u16x8& r, int j) { return bf2f(r[j]); }
+};
+template <> struct RawV<float> {
+    typedef f32x4 type;
+    static __device__ __forceinline__ float get(const f32x4& r, int j) { return r[j]; }
+};
+
 // C = number of 16-byte column chunks each lane owns (ceil(N / V / 64)).
 template <typename T, int C>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
@@ -111,30 +121,39 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ 
             for (int j = 0; j < V; ++j) wv[c][j] = g.v[j];
         }
     }
-    for (int row = blockIdx.x * 4 + wid; row < M; row += gridDim.x * 4) {
-        const T* xr = x + (size_t)row * N;
-        const T* dyr = dy + (size_t)row * N;
-        const float r = rstd[row];
-        float xs[C][V], gs[C][V];
-        float dot = 0.f;
+    // Rows are software-pipelined: the next row's x / dy / dres (raw 16-byte vectors) and rstd are loaded
+    // while this row is reduced and written, and dres comes with the first loads instead of after the
+    // reduction -- each wave keeps one row of loads in flight behind its compute.
+    typedef typename RawV<T>::type R;
+    const R zero{};
+    R xa[C], ga[C], ra[C];
+    float rcur = 0.f;
+    auto load_row = [&](int row, R* xo, R* go, R* ro, float& rr) {
+        rr = rstd[row];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             const int i = c * 64 + lane;
-            if (i < nvec) {
-                Vec<T> a, b;
-                a.load(xr + i * V);
-                b.load(dyr + i * V);
-#pragma unroll
-                for (int j = 0; j < V; ++j) {
-                    xs[c][j] = a.v[j] * r;  // x_hat
-                    gs[c][j] = b.v[j];
-                    dot += b.v[j] * wv[c][j] * xs[c][j];
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < V; ++j) { xs[c][j] = 0.f; gs[c][j] = 0.f; }
-            }
+            const bool ok = i < nvec;
+            xo[c] = ok ? *reinterpret_cast<const R*>(x + (size_t)row * N + i * V) : zero;
+            go[c] = ok ? *reinterpret_cast<const R*>(dy + (size_t)row * N + i * V) : zero;
+            ro[c] = (ok && dres) ? *reinterpret_cast<const R*>(dres + (size_t)row * N + i * V) : zero;
         }
+    };
+    const int stride = gridDim.x * 4;
+    int row = blockIdx.x * 4 + wid;
+    if (row < M) load_row(row, xa, ga, ra, rcur);
+    for (; row < M; row += stride) {
+        R xb[C], gb[C], rb[C];
+        float rnext = 0.f;
+        if (row + stride < M) load_row(row + stride, xb, gb, rb, rnext);
+        const float r = rcur;
+        // x_hat and dy are re-expanded from the raw vectors in both passes (register budget: 4 waves / SIMD)
+        float dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int j = 0; j < V; ++j)
+                dot += RawV<T>::get(ga[c], j) * wv[c][j] * (RawV<T>::get(xa[c], j) * r);
         dot = wave_sum(dot) / (float)N;
         T* dxr = dx + (size_t)row * N;
 #pragma unroll
@@ -144,18 +163,21 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ 
                 Vec<T> o;
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
-                    o.v[j] = r * (gs[c][j] * wv[c][j] - xs[c][j] * dot);
-                    dwacc[c][j] += gs[c][j] * xs[c][j];
-                }
-                if (dres) {  // fused residual-branch gradient: dx += dres
-                    Vec<T> rr;
-                    rr.load(dres + (size_t)row * N + i * V);
-#pragma unroll
-                    for (int j = 0; j < V; ++j) o.v[j] += rr.v[j];
+                    const float xh = RawV<T>::get(xa[c], j) * r, g = RawV<T>::get(ga[c], j);
+                    // fused residual-branch gradient: dx += dres (ra is zero without dres)
+                    o.v[j] = r * (g * wv[c][j] - xh * dot) + RawV<T>::get(ra[c], j);
+                    dwacc[c][j] += g * xh;
                 }
                 o.store(dxr + i * V);
             }
         }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            xa[c] = xb[c];
+            ga[c] = gb[c];
+            ra[c] = rb[c];
+        }
+        rcur = rnext;
     }
     // combine the 4 waves of this block through LDS, then one partial row per block
 #pragma unroll
@@ -178,16 +200,6 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ 
 // vectors per row in registers.  The one-wave-per-row kernel above needs C = 4 chunks per lane there (182
 // VGPRs, 2 waves per SIMD, one row's loads in flight per wave: ~1.5 TB/s); this one runs at high occupancy
 // with RPI rows of loads in flight per thread.  Per-row dot products: wave sums, then the 4 waves through LDS.
-template <typename T> struct RawV;
-template <> struct RawV<__bf16> {
-    typedef u16x8 type;
-    static __device__ __forceinline__ float get(const u16x8& r, int j) { return bf2f(r[j]); }
-};
-template <> struct RawV<float> {
-    typedef f32x4 type;
-    static __device__ __forceinline__ float get(const f32x4& r, int j) { return r[j]; }
-};
-
 template <typename T, int C2, int RPI>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_wide_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                const T* __restrict__ w,
