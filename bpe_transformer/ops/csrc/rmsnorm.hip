@@ -45,10 +45,21 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const T* __restrict__ 
     }
 }
 
+template <typename T> struct RawV;
+template <> struct RawV<__bf16> {
+    typedef u16x8 type;
+    static __device__ __forceinline__ float get(const u16x8& r, int j) { return bf2f(r[j]); }
+};
+template <> struct RawV<float> {
+    typedef f32x4 type;
+    static __device__ __forceinline__ float get(const f32x4& r, int j) { return r[j]; }
+};
+
 // Residual add fused into the norm: s = x + d (rounded to T: the residual stream is stored in T), y = RMSNorm(s).
 // Replaces "addmm(x, o, W^T)" (a full copy of x into the GEMM output, then a beta = 1 GEMM) + rmsnorm with a
-// plain GEMM and one pass here.  The second sweep re-reads s from L2 (just written by the same wave).
-template <typename T>
+// plain GEMM and one pass here.  C > 0: the lane's C chunks of s stay in registers for the second sweep (no
+// read-after-write of the just-stored sum); C == 0: any width, the second sweep re-reads s (L2-resident).
+template <typename T, int C>
 __global__ void __launch_bounds__(256) add_rmsnorm_fwd_kernel(const T* __restrict__ x, const T* __restrict__ d,
                                                               const T* __restrict__ w, T* __restrict__ sum,
                                                               T* __restrict__ y, float* __restrict__ rstd_out, int M,
@@ -60,6 +71,42 @@ __global__ void __launch_bounds__(256) add_rmsnorm_fwd_kernel(const T* __restric
     const size_t off = (size_t)row * N;
     const int nvec = N / V;
     float ss = 0.f;
+    if constexpr (C > 0) {
+        Vec<T> keep[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int i = c * 64 + lane;
+            if (i < nvec) {
+                Vec<T> a, b;
+                a.load(x + off + i * V);
+                b.load(d + off + i * V);
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    float v = a.v[j] + b.v[j];
+                    if constexpr (sizeof(T) == 2) v = bf2f(f2bf(v));  // statistics of the stored (rounded) sum
+                    a.v[j] = v;
+                    ss += v * v;
+                }
+                a.store(sum + off + i * V);
+                keep[c] = a;
+            }
+        }
+        ss = wave_sum(ss);
+        const float r = rsqrtf(ss / (float)N + eps);
+        if (lane == 0 && rstd_out) rstd_out[row] = r;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int i = c * 64 + lane;
+            if (i < nvec) {
+                Vec<T> g;
+                g.load(w + i * V);
+#pragma unroll
+                for (int j = 0; j < V; ++j) keep[c].v[j] = keep[c].v[j] * r * g.v[j];
+                keep[c].store(y + off + i * V);
+            }
+        }
+        return;
+    }
     for (int i = lane; i < nvec; i += 64) {
         Vec<T> a, b;
         a.load(x + off + i * V);
@@ -67,7 +114,7 @@ __global__ void __launch_bounds__(256) add_rmsnorm_fwd_kernel(const T* __restric
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             float v = a.v[j] + b.v[j];
-            if constexpr (sizeof(T) == 2) v = bf2f(f2bf(v));  // statistics of the stored (rounded) sum
+            if constexpr (sizeof(T) == 2) v = bf2f(f2bf(v));
             a.v[j] = v;
             ss += v * v;
         }
@@ -85,16 +132,6 @@ __global__ void __launch_bounds__(256) add_rmsnorm_fwd_kernel(const T* __restric
         a.store(y + off + i * V);
     }
 }
-
-template <typename T> struct RawV;
-template <> struct RawV<__bf16> {
-    typedef u16x8 type;
-    static __device__ __forceinline__ float get(const u16x8& r, int j) { return bf2f(r[j]); }
-};
-template <> struct RawV<float> {
-    typedef f32x4 type;
-    static __device__ __forceinline__ float get(const f32x4& r, int j) { return r[j]; }
-};
 
 // C = number of 16-byte column chunks each lane owns (ceil(N / V / 64)).
 template <typename T, int C>
@@ -360,12 +397,19 @@ static void rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* r
 void launch_add_rmsnorm_fwd(int dtype, const void* x, const void* d, const void* w, void* sum, void* y, float* rstd,
                             int M, int N, float eps, hipStream_t s) {
     const int grid = (M + 3) / 4;
-    if (dtype == DT_BF16)
-        add_rmsnorm_fwd_kernel<__bf16><<<grid, 256, 0, s>>>((const __bf16*)x, (const __bf16*)d, (const __bf16*)w,
-                                                            (__bf16*)sum, (__bf16*)y, rstd, M, N, eps);
-    else
-        add_rmsnorm_fwd_kernel<float><<<grid, 256, 0, s>>>((const float*)x, (const float*)d, (const float*)w,
-                                                           (float*)sum, (float*)y, rstd, M, N, eps);
+#define ADD_RMS(TT, CC)                                                                                        \
+    add_rmsnorm_fwd_kernel<TT, CC><<<grid, 256, 0, s>>>((const TT*)x, (const TT*)d, (const TT*)w, (TT*)sum,   \
+                                                        (TT*)y, rstd, M, N, eps)
+    if (dtype == DT_BF16) {
+        const int chunks = (N / 8 + 63) / 64;
+        if (chunks <= 1) ADD_RMS(__bf16, 1);
+        else if (chunks <= 2) ADD_RMS(__bf16, 2);
+        else if (chunks <= 4) ADD_RMS(__bf16, 4);
+        else ADD_RMS(__bf16, 0);
+    } else {
+        ADD_RMS(float, 0);
+    }
+#undef ADD_RMS
 }
 
 int rmsnorm_bwd_grid(int M) {
