@@ -412,9 +412,13 @@ void launch_add_rmsnorm_fwd(int dtype, const void* x, const void* d, const void*
 #undef ADD_RMS
 }
 
+// one resident round: the narrow kernel holds 3 workgroups per CU (156 VGPRs at C = 2), 256 CUs
+#ifndef BPE_RMS_BWD_GRID
+#define BPE_RMS_BWD_GRID 768
+#endif
 int rmsnorm_bwd_grid(int M) {
     int g = (M + 3) / 4;
-    return g < 1024 ? g : 1024;
+    return g < BPE_RMS_BWD_GRID ? g : BPE_RMS_BWD_GRID;
 }
 
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
