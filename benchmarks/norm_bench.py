@@ -1,5 +1,5 @@
-"""RMSNorm microbenchmark at training shapes (bf16): forward, residual-add forward, backward with the fused
-residual gradient.  Prints ms and effective TB/s (bytes each kernel must move) per op.
+"""Memory-bound block kernels at training shapes (bf16): RMSNorm forward, residual-add forward, backward with
+the fused residual gradient, SwiGLU forward.  Prints ms and effective TB/s (bytes each kernel must move) per op.
 
     python benchmarks/norm_bench.py [--rows 65536] [--dim 768]
 """
@@ -46,6 +46,9 @@ def main():
         "add_rmsnorm_fwd": (lambda: h.add_rmsnorm_fwd(x, d, w, 1e-5), 4 * B),
         "rmsnorm_bwd+dres": (lambda: h.rmsnorm_bwd(dy, x, w, rstd, dres), 4 * B),
     }
+    F = 4 * N if N < 2048 else 2816
+    gu = torch.randn(M, 2 * F, device="cuda", dtype=torch.bfloat16)
+    rows["swiglu_fwd"] = (lambda: h.swiglu_fwd(gu), 3 * M * F * 2)
     for name, (fn, nbytes) in rows.items():
         ms = timeit(fn)
         print(json.dumps({"op": name, "shape": [M, N], "ms": round(ms, 4), "TBps": round(nbytes / ms / 1e9, 2)}))
