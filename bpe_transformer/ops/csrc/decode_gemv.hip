@@ -39,44 +39,13 @@ constexpr int UNR = 4;   // W vectors in flight per lane
 
 constexpr int PF = 8;     // W vectors per lane issued before the prologue (all of a row for K <= 1024)
 
-template <int MM, int EPI>
-__global__ void __launch_bounds__(256) gemv_kernel(const GemvArgs a) {
-    extern __shared__ __attribute__((aligned(16))) u16 hs[];  // [MM][K] normalized input rows (bf16)
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int K = a.K, nv = K / 8;
-    // ---- this lane's weight row (4 rows per wave, 16 lanes per row)
-    const int slot = lane / LPR, l16 = lane % LPR;
-    const int wslot = wv * RPW + slot;  // row slot within the workgroup (0..15)
-    int n, j = 0;
-    bool valid;
-    if constexpr (EPI == 1) {  // slots (2s, 2s+1) = rows (j, F + j) of logical output column j
-        const int F = a.N / 2;
-        j = blockIdx.x * 8 + wslot / 2;
-        valid = j < F;
-        n = (wslot & 1) ? F + j : j;
-    } else {
-        n = blockIdx.x * 16 + wslot;
-        valid = n < a.N;
-    }
-    const u16* wr = reinterpret_cast<const u16*>(a.W) + (long)(valid ? n : 0) * a.ldw;
-    // the first PF weight vectors are in flight while the prologue reads and normalizes the input rows: the
-    // decode step is latency-bound, and the weight stream does not depend on the prologue
-    u16x8 wp[PF];
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-        const int i = l16 + LPR * u;
-        wp[u] = (valid && i < nv) ? wload(wr + 8 * i) : u16x8{};
-    }
-    // ---- prologue: wave w normalizes input rows w, w + 4, ...
-    for (int m = wv; m < MM; m += 4) {
-        u16* hr = hs + (long)m * K;
-        if (m >= a.M) {
-            for (int i = lane; i < nv; i += 64) *reinterpret_cast<u16x8*>(hr + 8 * i) = u16x8{};
-            continue;
-        }
+// Prologue shared by both kernels: input row m (< M) -> LDS row m (stride ldh): x (+ xd, with the sum written
+// to xsum by workgroup 0), RMSNorm'd when ln is given; or, with part, the merged decode-attention partials.
+__device__ __forceinline__ void gemv_prologue_rows(const GemvArgs& a, u16* hs, int ldh, int tid) {
+    const int lane = tid & 63, wv = tid >> 6, K = a.K, nv = K / 8;
+    for (int m = wv; m < a.M; m += 4) {
+        u16* hr = hs + (long)m * ldh;
         if (a.part != nullptr) {
-            // input row = the split-K decode attention's partials merged (flash-decoding combine): column k is
-            // head k / D, dim k % D; rounding matches decode_combine_kernel
             const int D = a.D, ns = a.nsplit;
             for (int i = lane; i < nv; i += 64) {
                 const int h = (8 * i) / D, d0 = (8 * i) % D;
@@ -126,6 +95,40 @@ __global__ void __launch_bounds__(256) gemv_kernel(const GemvArgs a) {
             }
         }
     }
+}
+
+template <int MM, int EPI>
+__global__ void __launch_bounds__(256) gemv_kernel(const GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) u16 hs[];  // [MM][K] normalized input rows (bf16)
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int K = a.K, nv = K / 8;
+    // ---- this lane's weight row (4 rows per wave, 16 lanes per row)
+    const int slot = lane / LPR, l16 = lane % LPR;
+    const int wslot = wv * RPW + slot;  // row slot within the workgroup (0..15)
+    int n, j = 0;
+    bool valid;
+    if constexpr (EPI == 1) {  // slots (2s, 2s+1) = rows (j, F + j) of logical output column j
+        const int F = a.N / 2;
+        j = blockIdx.x * 8 + wslot / 2;
+        valid = j < F;
+        n = (wslot & 1) ? F + j : j;
+    } else {
+        n = blockIdx.x * 16 + wslot;
+        valid = n < a.N;
+    }
+    const u16* wr = reinterpret_cast<const u16*>(a.W) + (long)(valid ? n : 0) * a.ldw;
+    // the first PF weight vectors are in flight while the prologue reads and normalizes the input rows: the
+    // decode step is latency-bound, and the weight stream does not depend on the prologue
+    u16x8 wp[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+        const int i = l16 + LPR * u;
+        wp[u] = (valid && i < nv) ? wload(wr + 8 * i) : u16x8{};
+    }
+    // ---- prologue: rows M..MM-1 of the (rounded-up) LDS tile are zero, rows < M from the shared prologue
+    for (int m = a.M + wv; m < MM; m += 4)
+        for (int i = lane; i < nv; i += 64) *reinterpret_cast<u16x8*>(hs + (long)m * K + 8 * i) = u16x8{};
+    gemv_prologue_rows(a, hs, K, tid);
     __syncthreads();
     // ---- main loop: 4 rows per wave, 16 lanes per row
     float acc[MM];
@@ -220,62 +223,6 @@ __global__ void __launch_bounds__(256) gemv_kernel(const GemvArgs a) {
 // 8 W1 rows and the matching 8 W3 rows.  Input rows sit in LDS with a 16-byte pad per row (the B reads of 16
 // tokens at one k would otherwise hit the same banks).
 constexpr int MF_PF = 8;  // k-steps (32 each) of W in flight per wave
-
-__device__ __forceinline__ void gemv_prologue_rows(const GemvArgs& a, u16* hs, int ldh, int tid) {
-    const int lane = tid & 63, wv = tid >> 6, K = a.K, nv = K / 8;
-    for (int m = wv; m < a.M; m += 4) {
-        u16* hr = hs + (long)m * ldh;
-        if (a.part != nullptr) {
-            const int D = a.D, ns = a.nsplit;
-            for (int i = lane; i < nv; i += 64) {
-                const int h = (8 * i) / D, d0 = (8 * i) % D;
-                const float* pb = a.part + ((long)m * a.H + h) * ns * (D + 2);
-                float mx = -INFINITY;
-                for (int sp = 0; sp < ns; ++sp) mx = fmaxf(mx, pb[sp * (D + 2) + D]);
-                float ls = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-                for (int sp = 0; sp < ns; ++sp) {
-                    const float* pr = pb + sp * (D + 2);
-                    const float ms = pr[D];
-                    if (ms == -INFINITY) continue;
-                    const float c = __expf(ms - mx);
-                    ls += c * pr[D + 1];
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) o[e] += c * pr[d0 + e];
-                }
-                u16x8 hv;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) hv[e] = f2bf(ls > 0.f ? o[e] / ls : 0.f);
-                *reinterpret_cast<u16x8*>(hr + 8 * i) = hv;
-            }
-            continue;
-        }
-        float ss = 0.f;
-        for (int i = lane; i < nv; i += 64) {
-            u16x8 xv = *reinterpret_cast<const u16x8*>(a.x + (long)m * a.ldx + 8 * i);
-            if (a.xd != nullptr) {
-                const u16x8 dv = *reinterpret_cast<const u16x8*>(a.xd + (long)m * a.ldx + 8 * i);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) xv[j] = f2bf(bf2f(xv[j]) + bf2f(dv[j]));
-                if (a.xsum != nullptr && blockIdx.x == 0)
-                    *reinterpret_cast<u16x8*>(a.xsum + (long)m * K + 8 * i) = xv;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) ss += bf2f(xv[j]) * bf2f(xv[j]);
-            *reinterpret_cast<u16x8*>(hr + 8 * i) = xv;
-        }
-        if (a.ln != nullptr) {
-            ss = wave_sum(ss);
-            const float r = rsqrtf(ss / (float)K + a.eps);
-            for (int i = lane; i < nv; i += 64) {
-                u16x8 hv = *reinterpret_cast<const u16x8*>(hr + 8 * i);
-                const u16x8 g = *reinterpret_cast<const u16x8*>(a.ln + 8 * i);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) hv[j] = f2bf(bf2f(hv[j]) * r * bf2f(g[j]));
-                *reinterpret_cast<u16x8*>(hr + 8 * i) = hv;
-            }
-        }
-    }
-}
 
 template <int EPI>
 __global__ void __launch_bounds__(256) gemv_mfma_kernel(const GemvArgs a) {
