@@ -10,6 +10,10 @@ instead:
   RMSNorm, the fused [Wq;Wk;Wv] GEMM, flash attention with fused RoPE -- plus
   ``kv_append``, which writes the roped K and the V of all ``T`` tokens into
   the cache in one launch;
+* **append** to a filled cache (a new turn of a conversation, draft tokens to
+  verify): steps of up to ``8 / G`` tokens per sequence, each a multi-token
+  ``kv_append`` + ``decode_attn`` in which token ``t`` sees the cache and its
+  own causal prefix (``pos + t``), instead of one decode step per token;
 * **decode** (one token per sequence): ``kv_append`` (RoPE at the device-side
   position, cache write, roped q) -> ``decode_attn`` (split-K flash-decoding
   over the cache) for every layer, residual adds fused into the next RMSNorm,
@@ -166,9 +170,12 @@ class DecodeSession:
         if self.fast and self.cache.length == 0 and T > 1:
             out = self._forward_fast(ids, prefill=True)
         elif self.fast:
+            # appending to a filled cache (multi-turn serving, speculative verification): chunks of up to
+            # 8 / G tokens per step, each attending the cache plus its own causal prefix in one decode_attn
             out = None
-            for t in range(T):
-                out = self._forward_fast(ids[:, t : t + 1], prefill=False)
+            step = max(1, 8 // (self.H // self.Hkv))
+            for t in range(0, T, step):
+                out = self._forward_fast(ids[:, t : t + step], prefill=False)
         else:
             out = self._forward_reference(ids)
         self.cache.length += T
@@ -229,7 +236,7 @@ class DecodeSession:
         self._graph = g
 
     def _forward_fast(self, ids: Tensor, prefill: bool) -> Tensor:
-        if not prefill and ids.shape[0] <= _GEMV_MAX_BATCH and self._gemv_fits(ids.shape[0]):
+        if not prefill and ids.shape[1] == 1 and ids.shape[0] <= _GEMV_MAX_BATCH and self._gemv_fits(ids.shape[0]):
             return self._decode_gemv(ids)
         from ..ops._ext import ops as hip
 
@@ -255,8 +262,8 @@ class DecodeSession:
                 o, _ = h.fa_fwd(q, k, v, cos, sin, B, T, H, Hkv, D, True, use_rope, scale)
                 h.kv_append(qkv, kc[li], vc[li], cos, sin, pos, B, T, H, use_rope)
             else:
-                q = h.kv_append(qkv, kc[li], vc[li], cos, sin, pos, B, 1, H, use_rope)
-                o = h.decode_attn(q, kc[li], vc[li], pos, H, scale)
+                q = h.kv_append(qkv, kc[li], vc[li], cos, sin, pos, B, T, H, use_rope)
+                o = h.decode_attn(q, kc[li], vc[li], pos, H, scale, True, T)
             g1 = torch.matmul(o, wo.t())
             xr, h2, _ = h.add_rmsnorm_fwd(xr, g1, ln2, eps)
             a = h.swiglu_fwd(torch.matmul(h2, w13.t()))

@@ -4,6 +4,8 @@
 //
 //   q [B, H, D] (RoPE already applied), cache K / V [B, Hkv, Lmax, D] (roped K), valid length L = *pos + 1:
 //   out[b, h] = softmax(q . K[b, h / G, :L]^T * scale) . V[b, h / G, :L]          (G = H / Hkv)
+// (T > 1 new tokens per sequence -- chunked prefill into a filled cache, speculative verification -- is the same
+// with one query row per (token, head) and token t limited to L = *pos + t + 1.)
 //
 // The position lives in device memory (int32), so one decode step -- append + attention for every layer -- is
 // shape-static and is captured once into a HIP graph (the host never passes the growing length).
@@ -30,27 +32,35 @@ namespace dec {
 
 constexpr int CH = 256;  // keys per chunk (= threads per workgroup)
 
-// G (query heads per kv head) is a template parameter: the per-head registers (m, l, o accumulators) must be
-// statically indexed (guide §5.4 rule 20: runtime-indexed register arrays go to scratch).
-template <int D, int G>
+// MR (query rows per workgroup, >= G * T) is a template parameter: the per-row registers (m, l, o accumulators)
+// must be statically indexed (guide §5.4 rule 20: runtime-indexed register arrays go to scratch).  Row r is
+// new token t = r / G of the sequence and query head g = r % G of the kv head; with T new tokens at positions
+// p0 .. p0 + T - 1 (p0 = *pos, already in the cache), token t attends keys [0, p0 + t] (causal within the chunk).
+template <int D, int MR>
 __global__ void __launch_bounds__(256) decode_attn_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ Kc,
                                                           const __bf16* __restrict__ Vc, float* __restrict__ part,
                                                           const int* __restrict__ pos, int H, int Hkv, int Lmax,
-                                                          int nsplit, float scale) {
+                                                          int nsplit, float scale, int T) {
     constexpr int DV = D / 8;     // 16-byte vectors per row
     constexpr int KP = 256 / DV;  // key partitions of the P.V step
-    __shared__ float qs[G][D];
-    __shared__ float ps[G][CH];
+    __shared__ float qs[MR][D];
+    __shared__ float ps[MR][CH];
     __shared__ float red[2][4];
-    __shared__ float ob[4][G][D];
+    __shared__ float ob[4][MR][D];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int bk = blockIdx.x / nsplit, split = blockIdx.x % nsplit;  // bk = b * Hkv + hk
     const int b = bk / Hkv, hk = bk % Hkv;
-    const int L = min(pos[0] + 1, Lmax);
+    const int G = H / Hkv, R = G * T;
+    const int p0 = pos[0];
+    const int L = min(p0 + T, Lmax);  // keys any row of this workgroup may see
     const int s0 = split * CH;
+    // partial slot of row r: part[(((b * T + t) * H + h) * nsplit + split) * (D + 2)]
+    auto prow = [&](int r) {
+        return part + ((((long)b * T + r / G) * H + hk * G + r % G) * nsplit + split) * (D + 2);
+    };
     if (s0 >= L) {  // uniform per workgroup: an empty chunk contributes nothing
-        if (tid < G) {
-            float* pr = part + (((long)b * H + hk * G + tid) * nsplit + split) * (D + 2);
+        if (tid < R) {
+            float* pr = prow(tid);
             pr[D] = -INFINITY;
             pr[D + 1] = 0.f;
         }
@@ -74,17 +84,19 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(const __bf16* __restri
         const int t = kp + KP * j;
         vr[j] = t < n ? *reinterpret_cast<const u16x8*>(Vc + kvbase + (long)t * D + dv * 8) : u16x8{};
     }
-    // query rows of the G heads -> LDS (fp32, pre-scaled)
-    for (int e = tid; e < G * D; e += 256) {
-        const int g = e / D, d = e % D;
-        qs[g][d] = bf2f(reinterpret_cast<const u16*>(q)[((long)b * H + hk * G + g) * D + d]) * scale;
+    // query rows -> LDS (fp32, pre-scaled); rows >= R are zero
+    for (int e = tid; e < MR * D; e += 256) {
+        const int r = e / D, d = e % D;
+        qs[r][d] = r < R ? bf2f(reinterpret_cast<const u16*>(q)[((((long)b * T + r / G) * H) + hk * G + r % G) * D + d]) *
+                               scale
+                         : 0.f;
     }
     __syncthreads();
-    // 1. scores
+    // 1. scores (key s0 + tid is visible to row r iff it is <= p0 + r / G)
     {
-        float s[G];
+        float s[MR];
 #pragma unroll
-        for (int g = 0; g < G; ++g) s[g] = 0.f;
+        for (int r = 0; r < MR; ++r) s[r] = 0.f;
         if (ok) {
 #pragma unroll
             for (int v = 0; v < DV; ++v) {
@@ -93,76 +105,75 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(const __bf16* __restri
                 for (int j = 0; j < 8; ++j) {
                     const float kx = bf2f(t[j]);
 #pragma unroll
-                    for (int g = 0; g < G; ++g) s[g] += qs[g][8 * v + j] * kx;
+                    for (int r = 0; r < MR; ++r) s[r] += qs[r][8 * v + j] * kx;
                 }
             }
         }
+        const int key = s0 + tid;
 #pragma unroll
-        for (int g = 0; g < G; ++g) ps[g][tid] = ok ? s[g] : -INFINITY;
+        for (int r = 0; r < MR; ++r) ps[r][tid] = (ok && key <= p0 + r / G) ? s[r] : -INFINITY;
     }
     __syncthreads();
-    // 2. per-head max / exp / sum over the chunk
-    float mg[G], lg[G];
+    // 2. per-row max / exp / sum over the chunk (a row with no visible key here: m = -inf, p = 0)
+    float mg[MR], lg[MR];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        float m = wave_max(ps[g][tid]);
+    for (int r = 0; r < MR; ++r) {
+        float m = wave_max(ps[r][tid]);
         if (lane == 0) red[0][wv] = m;
         __syncthreads();
         m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
-        const float p = tid < n ? __expf(ps[g][tid] - m) : 0.f;
-        ps[g][tid] = p;
+        const float p = (tid < n && m != -INFINITY) ? __expf(ps[r][tid] - m) : 0.f;
+        ps[r][tid] = p;
         float sm = wave_sum(p);
         if (lane == 0) red[1][wv] = sm;
         __syncthreads();
-        mg[g] = m;
-        lg[g] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-        __syncthreads();  // red[] reused by the next head
+        mg[r] = m;
+        lg[r] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        __syncthreads();  // red[] reused by the next row
     }
-    // 3. o[g][d] = sum_t p[g][t] V[t][d]; thread = (key partition kp, vector dv)
-    float acc[G][8];
+    // 3. o[r][d] = sum_t p[r][t] V[t][d]; thread = (key partition kp, vector dv)
+    float acc[MR][8];
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+    for (int r = 0; r < MR; ++r)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+        for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
 #pragma unroll
     for (int jj = 0; jj < CH / KP; ++jj) {
         const int t = kp + KP * jj;
         if (t >= n) break;
         const u16x8 vv = vr[jj];
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float p = ps[g][t];
+        for (int r = 0; r < MR; ++r) {
+            const float p = ps[r][t];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) acc[g][j] += p * bf2f(vv[j]);
+            for (int j = 0; j < 8; ++j) acc[r][j] += p * bf2f(vv[j]);
         }
     }
     // lanes that share dv differ by multiples of DV: butterfly over the wave's key partitions
 #pragma unroll
     for (int off = DV; off < 64; off <<= 1)
 #pragma unroll
-        for (int g = 0; g < G; ++g)
+        for (int r = 0; r < MR; ++r)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) acc[g][j] += __shfl_xor(acc[g][j], off);
+            for (int j = 0; j < 8; ++j) acc[r][j] += __shfl_xor(acc[r][j], off);
     if (lane < DV) {
 #pragma unroll
-        for (int g = 0; g < G; ++g)
+        for (int r = 0; r < MR; ++r)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ob[wv][g][dv * 8 + j] = acc[g][j];
+            for (int j = 0; j < 8; ++j) ob[wv][r][dv * 8 + j] = acc[r][j];
     }
     __syncthreads();
-    // 4. partial results: part[(b, h, split)] = {o[D], m, l}
-    for (int e = tid; e < G * D; e += 256) {
-        const int g = e / D, dd = e % D;
-        const float o = ob[0][g][dd] + ob[1][g][dd] + ob[2][g][dd] + ob[3][g][dd];
-        float* pr = part + (((long)b * H + hk * G + g) * nsplit + split) * (D + 2);
-        pr[dd] = o;
+    // 4. partial results per row: {o[D], m, l}
+    for (int e = tid; e < R * D; e += 256) {
+        const int r = e / D, dd = e % D;
+        prow(r)[dd] = ob[0][r][dd] + ob[1][r][dd] + ob[2][r][dd] + ob[3][r][dd];
     }
-    if (tid < G) {  // the head statistics (registers, identical in every thread)
+    if (tid < R) {  // the row statistics (registers, identical in every thread)
         float m = mg[0], l = lg[0];
 #pragma unroll
-        for (int g = 1; g < G; ++g)
-            if (tid == g) { m = mg[g]; l = lg[g]; }
-        float* pr = part + (((long)b * H + hk * G + tid) * nsplit + split) * (D + 2);
+        for (int r = 1; r < MR; ++r)
+            if (tid == r) { m = mg[r]; l = lg[r]; }
+        float* pr = prow(tid);
         pr[D] = m;
         pr[D + 1] = l;
     }
@@ -228,33 +239,33 @@ using namespace bpe::dec;
 
 int decode_attn_splits(int Lmax) { return (Lmax + CH - 1) / CH; }
 
-bool decode_attn_ok(int H, int Hkv, int D) {
+// T new tokens per sequence: the G * T query rows of a kv head share one workgroup (at most 8)
+bool decode_attn_ok(int H, int Hkv, int D, int T) {
     const int G = Hkv > 0 ? H / Hkv : 0;
-    return (D == 64 || D == 128) && Hkv > 0 && H % Hkv == 0 && (G == 1 || G == 2 || G == 4 || G == 8);
+    return (D == 64 || D == 128) && Hkv > 0 && H % Hkv == 0 && T >= 1 && G >= 1 && G * T <= 8;
 }
 
 template <int D>
 static void launch_d(const void* q, const void* k, const void* v, float* part, void* out, const int* pos, int B,
-                     int H, int Hkv, int Lmax, float scale, hipStream_t s) {
+                     int T, int H, int Hkv, int Lmax, float scale, hipStream_t s) {
     const int ns = decode_attn_splits(Lmax);
     const int grid = B * Hkv * ns;
-#define DEC(GG)                                                                                                   \
-    decode_attn_kernel<D, GG><<<grid, 256, 0, s>>>((const __bf16*)q, (const __bf16*)k, (const __bf16*)v, part, pos, \
-                                                   H, Hkv, Lmax, ns, scale)
-    switch (H / Hkv) {
-        case 1: DEC(1); break;
-        case 2: DEC(2); break;
-        case 4: DEC(4); break;
-        default: DEC(8); break;
-    }
+    const int R = (H / Hkv) * T;
+#define DEC(MR)                                                                                                   \
+    decode_attn_kernel<D, MR><<<grid, 256, 0, s>>>((const __bf16*)q, (const __bf16*)k, (const __bf16*)v, part, pos, \
+                                                   H, Hkv, Lmax, ns, scale, T)
+    if (R <= 1) DEC(1);
+    else if (R <= 2) DEC(2);
+    else if (R <= 4) DEC(4);
+    else DEC(8);
 #undef DEC
-    if (out != nullptr) decode_combine_kernel<D><<<B * H, D, 0, s>>>(part, (__bf16*)out, ns);
+    if (out != nullptr) decode_combine_kernel<D><<<B * T * H, D, 0, s>>>(part, (__bf16*)out, ns);
 }
 
 void launch_decode_attn(const void* q, const void* k, const void* v, float* part, void* out, const int* pos, int B,
-                        int H, int Hkv, int D, int Lmax, float scale, hipStream_t s) {
-    if (D == 64) launch_d<64>(q, k, v, part, out, pos, B, H, Hkv, Lmax, scale, s);
-    else launch_d<128>(q, k, v, part, out, pos, B, H, Hkv, Lmax, scale, s);
+                        int T, int H, int Hkv, int D, int Lmax, float scale, hipStream_t s) {
+    if (D == 64) launch_d<64>(q, k, v, part, out, pos, B, T, H, Hkv, Lmax, scale, s);
+    else launch_d<128>(q, k, v, part, out, pos, B, T, H, Hkv, Lmax, scale, s);
 }
 
 void launch_kv_append(const void* qkv, long ld, void* qo, void* Kc, void* Vc, const float* cosT, const float* sinT,

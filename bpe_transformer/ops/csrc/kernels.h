@@ -102,9 +102,9 @@ struct FaArgs {
 };
 // decode_attn.hip (KV-cache serving path; `pos` = device int32 position of the first new token)
 int decode_attn_splits(int Lmax);
-bool decode_attn_ok(int H, int Hkv, int D);
+bool decode_attn_ok(int H, int Hkv, int D, int T);
 void launch_decode_attn(const void* q, const void* k, const void* v, float* part, void* out, const int* pos, int B,
-                        int H, int Hkv, int D, int Lmax, float scale, hipStream_t s);
+                        int T, int H, int Hkv, int D, int Lmax, float scale, hipStream_t s);
 void launch_kv_append(const void* qkv, long ld, void* qo, void* Kc, void* Vc, const float* cosT, const float* sinT,
                       const int* pos, int B, int T, int H, int Hkv, int D, int Lmax, hipStream_t s);
 

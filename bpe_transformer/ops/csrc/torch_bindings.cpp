@@ -515,26 +515,27 @@ at::Tensor kv_append(const at::Tensor& qkv, at::Tensor kc, at::Tensor vc, const 
 }
 
 // q [B, H*D] (roped) attends to the first *pos + 1 cache rows -> [B, H*D]
-// combine = false: return the split partials [B, H, nsplit, D + 2] (o, m, l) for decode_attn_proj instead
+// combine = false: return the split partials [B*T, H, nsplit, D + 2] (o, m, l) for decode_attn_proj instead.
+// T new tokens per sequence (q rows b * T + t, already appended at positions *pos .. *pos + T - 1).
 at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& pos,
-                       int64_t H, double scale, bool combine) {
+                       int64_t H, double scale, bool combine, int64_t T) {
     const int64_t B = kc.size(0), Hkv = kc.size(1), Lmax = kc.size(2), D = kc.size(3);
-    TORCH_CHECK(decode_attn_ok((int)H, (int)Hkv, (int)D),
-                "decode_attn: head dim 64/128 and H / Hkv in {1, 2, 4, 8} required");
+    TORCH_CHECK(decode_attn_ok((int)H, (int)Hkv, (int)D, (int)T),
+                "decode_attn: head dim 64/128, H a multiple of Hkv and (H / Hkv) * T <= 8 required");
     check_cuda(q, "q");
-    TORCH_CHECK(q.scalar_type() == at::kBFloat16 && q.is_contiguous() && q.numel() == B * H * D,
-                "decode_attn: q must be contiguous bf16 [B, H*D]");
+    TORCH_CHECK(q.scalar_type() == at::kBFloat16 && q.is_contiguous() && q.numel() == B * T * H * D,
+                "decode_attn: q must be contiguous bf16 [B*T, H*D]");
     check_cache(kc, B, Hkv, "k_cache");
     check_cache(vc, B, Hkv, "v_cache");
     TORCH_CHECK(vc.sizes() == kc.sizes(), "decode_attn: k / v cache shapes differ");
     check_pos(pos);
     DevGuard g(q.device());
     const int ns = decode_attn_splits((int)Lmax);
-    auto part = at::empty({B, H, ns, D + 2}, q.options().dtype(at::kFloat));
-    auto out = combine ? at::empty({B, H * D}, q.options()) : at::Tensor();
+    auto part = at::empty({B * T, H, ns, D + 2}, q.options().dtype(at::kFloat));
+    auto out = combine ? at::empty({B * T, H * D}, q.options()) : at::Tensor();
     launch_decode_attn(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), part.data_ptr<float>(),
-                       combine ? out.data_ptr() : nullptr, pos.data_ptr<int>(), (int)B, (int)H, (int)Hkv, (int)D,
-                       (int)Lmax, (float)scale, cur_stream());
+                       combine ? out.data_ptr() : nullptr, pos.data_ptr<int>(), (int)B, (int)T, (int)H, (int)Hkv,
+                       (int)D, (int)Lmax, (float)scale, cur_stream());
     return combine ? out : part;
 }
 
@@ -663,7 +664,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("kv_append(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor cos, Tensor sin, Tensor pos, int B, "
           "int T, int H, bool rope) -> Tensor");
     m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor pos, int H, float scale, "
-          "bool combine=True) -> Tensor");
+          "bool combine=True, int T=1) -> Tensor");
     m.def("decode_attn_proj(Tensor part, Tensor w) -> Tensor");
     m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
     m.def("add_rmsnorm_fwd(Tensor x, Tensor d, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");

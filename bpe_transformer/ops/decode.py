@@ -56,25 +56,30 @@ def kv_append_reference(qkv, k_cache, v_cache, cos, sin, pos, batch, n_new, n_he
 
 
 def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, pos: Tensor, n_heads: int,
-                     scale: float | None = None) -> Tensor:
+                     scale: float | None = None, n_new: int = 1) -> Tensor:
+    """Attention of ``n_new`` new tokens per sequence (``q [B*n_new, H*D]``, already appended to the caches at
+    positions ``pos .. pos + n_new - 1``) over the cache; token t sees keys ``0 .. pos + t``."""
     D = k_cache.shape[-1]
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if q.is_cuda:
-        return ops().decode_attn(q.contiguous(), k_cache, v_cache, pos, n_heads, scale)
-    return decode_attention_reference(q, k_cache, v_cache, pos, n_heads, scale)
+        return ops().decode_attn(q.contiguous(), k_cache, v_cache, pos, n_heads, scale, True, n_new)
+    return decode_attention_reference(q, k_cache, v_cache, pos, n_heads, scale, n_new)
 
 
-def decode_attention_reference(q, k_cache, v_cache, pos, n_heads, scale=None) -> Tensor:
+def decode_attention_reference(q, k_cache, v_cache, pos, n_heads, scale=None, n_new: int = 1) -> Tensor:
     B, Hkv, Lmax, D = k_cache.shape
-    H = n_heads
-    L = min(int(pos.reshape(-1)[0]) + 1, Lmax)
+    H, T = n_heads, n_new
+    p0 = int(pos.reshape(-1)[0])
+    L = min(p0 + T, Lmax)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
-    qf = q.float().view(B, Hkv, H // Hkv, D)
+    qf = q.float().view(B, T, Hkv, H // Hkv, D)
     k = k_cache[:, :, :L].float()
     v = v_cache[:, :, :L].float()
-    s = torch.einsum("bhgd,bhld->bhgl", qf, k) * scale
-    o = torch.einsum("bhgl,bhld->bhgd", F.softmax(s, -1), v)
-    return o.reshape(B, H * D).to(q.dtype)
+    s = torch.einsum("bthgd,bhld->bthgl", qf, k) * scale
+    visible = torch.arange(L, device=q.device)[None, :] <= (p0 + torch.arange(T, device=q.device))[:, None]
+    s = s.masked_fill(~visible[None, :, None, None, :], float("-inf"))
+    o = torch.einsum("bthgl,bhld->bthgd", F.softmax(s, -1), v)
+    return o.reshape(B * T, H * D).to(q.dtype)
 
 
 def decode_attention_partials(q: Tensor, k_cache: Tensor, v_cache: Tensor, pos: Tensor, n_heads: int,

@@ -140,3 +140,15 @@ def test_decode_partials_combine_to_attention():
     got = dec.decode_attn_proj(part, eye)
     want = dec.decode_attention_reference(q, kc, vc, pos, H)
     assert torch.allclose(got, want, atol=1e-5)
+
+
+def test_multi_token_decode_attention_oracle_is_per_token_causal():
+    """n_new tokens in one call == n_new single-token calls with the position advanced each time."""
+    torch.manual_seed(2)
+    B, H, Hkv, D, Lmax, T, p0 = 2, 4, 2, 16, 40, 3, 17
+    q = torch.randn(B * T, H * D)
+    kc, vc = torch.randn(B, Hkv, Lmax, D), torch.randn(B, Hkv, Lmax, D)
+    got = dec.decode_attention(q, kc, vc, torch.tensor([p0], dtype=torch.int32), H, n_new=T).view(B, T, H * D)
+    for t in range(T):
+        want = dec.decode_attention(q.view(B, T, -1)[:, t], kc, vc, torch.tensor([p0 + t], dtype=torch.int32), H)
+        assert torch.allclose(got[:, t], want, atol=1e-5)

@@ -203,3 +203,39 @@ def test_decode_attn_proj_matches_reference(gpu_device, D, G, L, B):
     torch.cuda.synchronize()
     assert part.shape == (B, H, Lmax // 256, D + 2)
     assert rel(y.cpu(), y_ref) < 2e-2, rel(y.cpu(), y_ref)
+
+
+@pytest.mark.parametrize("D,G,T", [(64, 1, 2), (64, 1, 5), (64, 2, 4), (128, 4, 2), (64, 1, 8)])
+@pytest.mark.parametrize("p0", [0, 250, 700])
+def test_multi_token_decode_attention(gpu_device, D, G, T, p0):
+    """T new tokens per sequence in one decode_attn (chunked prefill into a filled cache): per-token causal."""
+    torch.manual_seed(p0 + T)
+    B, Hkv, Lmax = 2, 2, 1024
+    H = Hkv * G
+    q = torch.randn(B * T, H * D).bfloat16()
+    kc = torch.randn(B, Hkv, Lmax, D).bfloat16()
+    vc = torch.randn(B, Hkv, Lmax, D).bfloat16()
+    pos = torch.tensor([p0], dtype=torch.int32)
+    ref = dec.decode_attention_reference(q.float(), kc, vc, pos, H, None, T)
+    g = lambda t: t.to(gpu_device)  # noqa: E731
+    out = dec.decode_attention(g(q), g(kc), g(vc), g(pos), H, n_new=T)
+    torch.cuda.synchronize()
+    assert rel(out.cpu(), ref) < 2e-2, rel(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("kw", [{}, {"num_kv_heads": 2}])
+def test_append_to_filled_cache_matches_full_forward(gpu_device, kw):
+    """prefill, then a 7-token chunk appended to the filled cache (multi-token decode steps), then decode."""
+    model = _bf16_model(gpu_device, **kw)
+    ids = torch.randint(0, 1000, (3, 34), device=gpu_device)
+    sess = DecodeSession(model, 3, max_len=64)
+    with torch.no_grad():
+        full = model(ids).float()
+        sess.prefill(ids[:, :20])
+        got = [sess.prefill(ids[:, 20:27])]
+        for t in range(27, 34):
+            got.append(sess.decode(ids[:, t]))
+    torch.cuda.synchronize()
+    want = [full[:, 26]] + [full[:, t] for t in range(27, 34)]
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert rel(a, b) < 3e-2, (i, rel(a, b))
