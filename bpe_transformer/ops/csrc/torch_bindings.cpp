@@ -152,8 +152,10 @@ at::Tensor act_bwd(const at::Tensor& dy, const at::Tensor& x, int64_t kind) {
 }
 
 // ---------------------------------------------------------------- cross entropy
+// nvalid (optional fp32 scalar): the gradient's 1 / n denominator when this call covers only a slice of the
+// rows (chunked LM head); default = the valid targets of this call
 std::tuple<at::Tensor, at::Tensor> ce_fwd_bwd(at::Tensor logits, const at::Tensor& targets, int64_t ignore_index,
-                                              bool write_grad) {
+                                              bool write_grad, const c10::optional<at::Tensor>& nvalid_in) {
     check_cuda(logits, "logits");
     TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "ce: logits must be [M, V] with unit column stride");
     TORCH_CHECK(targets.scalar_type() == at::kLong && targets.is_contiguous(), "ce: targets must be int64");
@@ -162,7 +164,14 @@ std::tuple<at::Tensor, at::Tensor> ce_fwd_bwd(at::Tensor logits, const at::Tenso
     DevGuard g(logits.device());
     auto loss = at::empty({M}, logits.options().dtype(at::kFloat));
     auto lse = at::empty({M}, logits.options().dtype(at::kFloat));
-    auto nvalid = targets.ne(ignore_index).sum().to(at::kFloat);
+    at::Tensor nvalid;
+    if (nvalid_in.has_value() && nvalid_in->defined()) {
+        TORCH_CHECK(nvalid_in->scalar_type() == at::kFloat && nvalid_in->numel() == 1 && nvalid_in->is_cuda(),
+                    "ce: nvalid must be a fp32 scalar on the device");
+        nvalid = *nvalid_in;
+    } else {
+        nvalid = targets.ne(ignore_index).sum().to(at::kFloat);
+    }
     launch_ce_fwd_bwd(dt_code(logits), logits.data_ptr(), logits.stride(0), targets.data_ptr<int64_t>(),
                       loss.data_ptr<float>(), lse.data_ptr<float>(), nvalid.data_ptr<float>(), M, V, ignore_index,
                       write_grad ? 1 : 0, cur_stream());
@@ -673,7 +682,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("swiglu_bwd(Tensor dout, Tensor gu) -> Tensor");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");
     m.def("act_bwd(Tensor dy, Tensor x, int kind) -> Tensor");
-    m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index, bool write_grad) -> (Tensor, Tensor)");
+    m.def("ce_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index, bool write_grad, Tensor? nvalid=None) "
+          "-> (Tensor, Tensor)");
     m.def("embed_fwd(Tensor weight, Tensor ids) -> Tensor");
     m.def("embed_bwd(Tensor dout, Tensor ids, int vocab) -> Tensor");
     m.def("adamw_step(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor grad, Tensor(d!)? pout, float lr, float b1, "

@@ -12,6 +12,8 @@ Reference contract K13 (``tests/adapters.py:440-455``).
 
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import Tensor
 
@@ -19,6 +21,8 @@ from . import reference as F
 from ._ext import ops
 
 IGNORE_INDEX = -100
+# LM head + CE in token chunks of this many rows (0 = one GEMM + one CE pass over the whole buffer)
+_LMHEAD_CHUNK = int(os.environ.get("BPE_LMHEAD_CHUNK", "0"))
 
 
 class _LMHeadCEFn(torch.autograd.Function):
@@ -31,9 +35,22 @@ class _LMHeadCEFn(torch.autograd.Function):
         wp = getattr(w, "_bpe_padded", None)
         if wp is None or wp.data_ptr() != w.data_ptr():
             wp = w
-        logits = torch.matmul(h, wp.t())  # hipBLASLt
-        loss_rows, _ = ops().ce_fwd_bwd(logits[:, :V], targets, ignore_index, True)
         nvalid = (targets != ignore_index).sum().clamp_min(1).to(torch.float32)
+        M = h.shape[0]
+        chunk = _LMHEAD_CHUNK if 0 < _LMHEAD_CHUNK < M else M
+        if chunk == M:
+            logits = torch.matmul(h, wp.t())  # hipBLASLt
+            loss_rows, _ = ops().ce_fwd_bwd(logits[:, :V], targets, ignore_index, True, nvalid)
+        else:
+            # token chunks: each chunk's logits are still in the Infinity Cache when the CE kernel reads and
+            # rewrites them (one HBM pass instead of three over the [tokens, vocab] buffer)
+            logits = h.new_empty(M, wp.shape[0])
+            parts = []
+            for c0 in range(0, M, chunk):
+                c1 = min(M, c0 + chunk)
+                torch.matmul(h[c0:c1], wp.t(), out=logits[c0:c1])
+                parts.append(ops().ce_fwd_bwd(logits[c0:c1, :V], targets[c0:c1], ignore_index, True, nvalid)[0])
+            loss_rows = torch.cat(parts)
         ctx.save_for_backward(h, wp, logits)
         ctx.w_param = w
         ctx.padded = wp is not w
