@@ -53,18 +53,30 @@ template <int D> struct BwdCfg {
 template <int D>
 __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const __bf16* __restrict__ O, long ld_o,
                                                          const __bf16* __restrict__ dO, long ld_do,
-                                                         float* __restrict__ delta, int B, int H, int S) {
+                                                         float* __restrict__ delta, float* __restrict__ dq_acc,
+                                                         int B, int H, int S, int spad) {
+    // one row per (b, s < spad, h): delta = rowsum(O * dO) for s < S, and the row's fp32 dQ accumulator
+    // zeroed (replaces a separate memset; pad rows s >= S only get the zeros)
     constexpr int LPR = D / 8;
     const long row = ((long)blockIdx.x * 256 + threadIdx.x) / LPR;
     const int sub = threadIdx.x % LPR;
-    const long total = (long)B * S * H;
+    const long total = (long)B * spad * H;
     float acc = 0.f;
-    const bool ok = row < total;
-    long bs = 0;
-    int h = 0;
-    if (ok) {
-        bs = row / H;
+    const bool in = row < total;
+    long b = 0;
+    int s = 0, h = 0;
+    if (in) {
+        const long bsp = row / H;
         h = (int)(row % H);
+        b = bsp / spad;
+        s = (int)(bsp % spad);
+        float4* z = reinterpret_cast<float4*>(dq_acc + row * D + sub * 8);
+        z[0] = float4{0.f, 0.f, 0.f, 0.f};
+        z[1] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+    const bool ok = in && s < S;
+    if (ok) {
+        const long bs = b * S + s;
         u16x8 a = *reinterpret_cast<const u16x8*>(O + bs * ld_o + (long)h * D + sub * 8);
         u16x8 g = *reinterpret_cast<const u16x8*>(dO + bs * ld_do + (long)h * D + sub * 8);
 #pragma unroll
@@ -72,10 +84,7 @@ __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const __bf16* __restric
     }
 #pragma unroll
     for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (ok && sub == 0) {
-        const long b = bs / S, s = bs % S;
-        delta[(b * H + h) * S + s] = acc;
-    }
+    if (ok && sub == 0) delta[(b * H + h) * S + s] = acc;
 }
 
 // P and dS of one 32-query half from its S / dP accumulators (key on the lane, 4 consecutive queries per
@@ -476,13 +485,12 @@ template <int D, bool C, bool R>
 static void bwd_launch(const FaArgs& a, hipStream_t s) {
     using Cfg = BwdCfg<D>;
     {
-        const long rows = (long)a.B * a.S * a.H;
+        const int spad = (a.S + 63) & ~63;  // dq_acc is [B][spad][H][D] fp32
+        const long rows = (long)a.B * spad * a.H;
         const long threads = rows * (D / 8);
         fa_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(a.o, a.ld_o, a.dout, a.ld_do, a.delta,
-                                                                               a.B, a.H, a.S);
+                                                                               a.dq_acc, a.B, a.H, a.S, spad);
     }
-    const size_t spad = (size_t)((a.S + 63) & ~63);
-    (void)hipMemsetAsync(a.dq_acc, 0, (size_t)a.B * spad * a.H * D * sizeof(float), s);
     static const int dbg = [] {
         const char* e = getenv("BPE_FA_DEBUG");  // bit 0: skip the dQ atomics (timing diagnostics only)
         return e ? atoi(e) : 0;
