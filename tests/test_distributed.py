@@ -50,7 +50,9 @@ def _worker(rank, world, port, bucket_mb, out_q):
     assert len(eng.ddp.buckets) >= (2 if bucket_mb < 0.05 else 1)
     for _ in range(3):
         eng.train_step([_batches(rank)])
-    out_q.put((rank, eng.flat.data.clone(), eng.flat.grad.clone()))
+    # numpy copies travel by value; torch tensors would go through fd sharing whose
+    # listener dies with this process (flaky under pytest-xdist)
+    out_q.put((rank, eng.flat.data.numpy().copy(), eng.flat.grad.numpy().copy()))
     cleanup()
 
 
@@ -62,7 +64,7 @@ def test_dp2_matches_single_process(bucket_mb):
     procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (d, g)) for r, d, g in (q.get(timeout=240) for _ in range(world)))
+    res = dict((r, (torch.from_numpy(d), torch.from_numpy(g))) for r, d, g in (q.get(timeout=240) for _ in range(world)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
