@@ -158,10 +158,11 @@ def main() -> int:
         "final_loss": round(loss_v, 4),
         "gemm_tuning": tuning,
     }
-    if info.is_main:
+    if on_gpu:
         from bpe_transformer.ops import gemm as _gemm
 
-        print(f"dW GEMM routes: {_gemm._route}", file=sys.stderr)
+        out["dw_gemm_routes"] = _gemm.routes_summary()  # weight-gradient kernel per shape (ops/tuning/dw_routes.json)
+    if info.is_main:
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

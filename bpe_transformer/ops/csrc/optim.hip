@@ -34,7 +34,25 @@ template <> struct G4<__bf16> {
 
 struct AdamArgs {
     float lr, b1, b2, eps, wd, bc1, bc2_sqrt;
+    double b1d, b2d;  // exact betas for the on-device bias correction (the host computes it in double too)
 };
+
+// Bias-correction terms from the DEVICE count of applied updates (``nstep``, incremented by
+// adam_count_kernel only when the step is not skipped), so a skipped non-finite step does not advance
+// bc1/bc2.  Computed in double, like the host path.
+__device__ __forceinline__ void adam_bias_from_count(AdamArgs& a, const int* nstep) {
+    const double t = (double)*nstep;
+    a.bc1 = (float)(1.0 - pow(a.b1d, t));
+    a.bc2_sqrt = (float)sqrt(1.0 - pow(a.b2d, t));
+}
+
+// One thread: count this update as applied unless the clip coefficient marks a non-finite norm (-1).
+__global__ void adam_count_kernel(int* __restrict__ nstep, const float* __restrict__ gscale) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        const float sc = gscale ? *gscale : 1.f;
+        if (sc >= 0.f) *nstep += 1;
+    }
+}
 
 __device__ __forceinline__ void adam_one(float& p, float& m, float& v, float g, const AdamArgs& a) {
     p = p * (1.f - a.lr * a.wd);
@@ -47,9 +65,11 @@ __device__ __forceinline__ void adam_one(float& p, float& m, float& v, float g, 
 template <typename GT>
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                                     const GT* __restrict__ g, __bf16* __restrict__ pout, size_t n,
-                                                    AdamArgs a, const float* __restrict__ gscale) {
+                                                    AdamArgs a, const float* __restrict__ gscale,
+                                                    const int* __restrict__ nstep) {
     const float sc = gscale ? *gscale : 1.f;
     if (!(sc >= 0.f)) return;  // non-finite gradient norm: the step is skipped on the device (no host sync)
+    if (nstep) adam_bias_from_count(a, nstep);
     const size_t n4 = n / 4;
     const size_t stride = (size_t)gridDim.x * 256;
     for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += stride) {
@@ -143,15 +163,19 @@ __global__ void __launch_bounds__(256) scale_kernel(T* __restrict__ x, size_t n,
 using namespace bpe;
 
 void launch_adamw(int gdtype, float* p, float* m, float* v, const void* g, void* pout_bf16, size_t n, float lr,
-                  float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, const float* gscale,
-                  hipStream_t s) {
+                  double b1, double b2, float eps, float wd, float bc1, float bc2_sqrt, const float* gscale,
+                  const int* nstep, hipStream_t s) {
     if (n == 0) return;
-    AdamArgs a{lr, b1, b2, eps, wd, bc1, bc2_sqrt};
+    AdamArgs a{lr, (float)b1, (float)b2, eps, wd, bc1, bc2_sqrt, b1, b2};
     const int grid = stream_grid(n / 4 + 1, 256, 2048);
     if (gdtype == DT_BF16)
-        adamw_kernel<__bf16><<<grid, 256, 0, s>>>(p, m, v, (const __bf16*)g, (__bf16*)pout_bf16, n, a, gscale);
+        adamw_kernel<__bf16><<<grid, 256, 0, s>>>(p, m, v, (const __bf16*)g, (__bf16*)pout_bf16, n, a, gscale, nstep);
     else
-        adamw_kernel<float><<<grid, 256, 0, s>>>(p, m, v, (const float*)g, (__bf16*)pout_bf16, n, a, gscale);
+        adamw_kernel<float><<<grid, 256, 0, s>>>(p, m, v, (const float*)g, (__bf16*)pout_bf16, n, a, gscale, nstep);
+}
+
+void launch_adam_count(int* nstep, const float* gscale, hipStream_t s) {
+    adam_count_kernel<<<1, 64, 0, s>>>(nstep, gscale);
 }
 
 void launch_sumsq_partial(int dtype, const void* x, size_t n, float* partial, int nblocks, hipStream_t s) {

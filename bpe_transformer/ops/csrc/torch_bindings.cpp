@@ -212,7 +212,7 @@ at::Tensor embed_bwd(const at::Tensor& dout, const at::Tensor& ids, int64_t voca
 // ---------------------------------------------------------------- optimizer
 void adamw_step(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& grad, const c10::optional<at::Tensor>& pout,
                 double lr, double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt,
-                const c10::optional<at::Tensor>& gscale) {
+                const c10::optional<at::Tensor>& gscale, const c10::optional<at::Tensor>& nstep) {
     check_cuda(p, "param");
     TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
                 "adamw: master param / moments must be fp32");
@@ -227,10 +227,25 @@ void adamw_step(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& grad
     }
     const float* gs = nullptr;
     if (gscale.has_value() && gscale->defined()) gs = gscale->data_ptr<float>();
+    const int* ns = nullptr;
+    if (nstep.has_value() && nstep->defined()) {
+        TORCH_CHECK(nstep->scalar_type() == at::kInt && nstep->numel() == 1 && nstep->device() == p.device(),
+                    "adamw: nstep must be a one-element int32 tensor on the parameters' device");
+        ns = nstep->data_ptr<int>();
+    }
     DevGuard g(p.device());
     launch_adamw(dt_code(grad), p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(), po,
-                 p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, gs,
+                 p.numel(), (float)lr, b1, b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, gs, ns,
                  cur_stream());
+}
+
+void adam_count_step(at::Tensor nstep, const c10::optional<at::Tensor>& gscale) {
+    check_cuda(nstep, "nstep");
+    TORCH_CHECK(nstep.scalar_type() == at::kInt && nstep.numel() == 1, "adam_count_step: one-element int32 tensor");
+    const float* gs = nullptr;
+    if (gscale.has_value() && gscale->defined()) gs = gscale->data_ptr<float>();
+    DevGuard g(nstep.device());
+    launch_adam_count(nstep.data_ptr<int>(), gs, cur_stream());
 }
 
 std::tuple<at::Tensor, at::Tensor> grad_norm(at::TensorList tensors, double max_norm) {
@@ -687,7 +702,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("embed_fwd(Tensor weight, Tensor ids) -> Tensor");
     m.def("embed_bwd(Tensor dout, Tensor ids, int vocab) -> Tensor");
     m.def("adamw_step(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor grad, Tensor(d!)? pout, float lr, float b1, "
-          "float b2, float eps, float wd, float bc1, float bc2_sqrt, Tensor? gscale) -> ()");
+          "float b2, float eps, float wd, float bc1, float bc2_sqrt, Tensor? gscale, Tensor? nstep=None) -> ()");
+    m.def("adam_count_step(Tensor(a!) nstep, Tensor? gscale) -> ()");
     m.def("grad_norm(Tensor[] tensors, float max_norm) -> (Tensor, Tensor)");
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
     m.def("gemm_swiglu_bwd(Tensor dy, Tensor w2, Tensor gu) -> Tensor");
@@ -718,6 +734,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("embed_fwd", &embed_fwd);
     m.impl("embed_bwd", &embed_bwd);
     m.impl("adamw_step", &adamw_step);
+    m.impl("adam_count_step", &adam_count_step);
     m.impl("grad_norm", &grad_norm);
     m.impl("scale_", &scale_);
     m.impl("gemm", &gemm);

@@ -14,6 +14,7 @@ Shapes neither covers go to hipBLASLt (``addmm_``).
 
 from __future__ import annotations
 
+import json
 import os
 
 import torch
@@ -81,6 +82,22 @@ def supported(n: int, k: int, t: int) -> bool:
 
 _AUTOTUNE = os.environ.get("BPE_GEMM_AUTOTUNE", "1") == "1"
 _route: dict[tuple[int, int, int], str] = {}
+_ROUTES_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "dw_routes.json")
+
+
+def _load_static_routes(path: str | None = None) -> dict[tuple[int, int, int], str]:
+    """Measured per-shape dW routes (``tuning/dw_routes.json``: ``"N,K,T": route``), so a known training shape gets
+    the same kernel -- and the same numerics -- on every run and every rank.  ``BPE_GEMM_ROUTES`` = another table,
+    or ``off`` to time every shape at first use."""
+    path = path or os.environ.get("BPE_GEMM_ROUTES", _ROUTES_FILE)
+    if path == "off" or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        raw = json.load(f)
+    return {tuple(int(v) for v in k.split(",")): r for k, r in raw.get("routes", raw).items()}
+
+
+_static_route = _load_static_routes()
 
 
 def choose_splits_pp(n: int, k: int, t: int, cus: int = _CUS) -> int:
@@ -131,11 +148,15 @@ def _run(route: str, g: Tensor, dy: Tensor, x: Tensor) -> None:
 
 
 def _tune(key: tuple[int, int, int], cands: list[str], g: Tensor, dy: Tensor, x: Tensor) -> str:
-    """Time each route once per shape on a scratch output (CUDA events, 3 reps) and keep the fastest."""
+    """Time each route once per shape on a scratch output (CUDA events, 3 reps) and keep the fastest.
+
+    Under ``torch.distributed`` the per-route times are MAX-reduced over the ranks before the choice, so every
+    rank takes the same kernel (every rank reaches the first use of a shape in the same program order).
+    """
     if not _AUTOTUNE or len(cands) == 1 or torch.cuda.is_current_stream_capturing():
         return cands[0]
     scratch = torch.empty_like(g)
-    best, best_t = cands[0], float("inf")
+    times = []
     for c in cands:
         _run(c, scratch, dy, x)  # warm (kernel attributes, library heuristics)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -144,15 +165,25 @@ def _tune(key: tuple[int, int, int], cands: list[str], g: Tensor, dy: Tensor, x:
             _run(c, scratch, dy, x)
         e.record()
         e.synchronize()
-        ms = s.elapsed_time(e)
-        if ms < best_t:
-            best, best_t = c, ms
-    return best
+        times.append(s.elapsed_time(e))
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        on_dev = dist.get_backend() == "nccl"
+        tt = torch.tensor(times, dtype=torch.float64, device=g.device if on_dev else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        times = tt.tolist()
+    return cands[min(range(len(cands)), key=lambda i: times[i])]
 
 
 def weight_grad_route(n: int, k: int, t: int) -> str | None:
     """The route chosen for a dW shape (None until first use)."""
     return _route.get((n, k, t))
+
+
+def routes_summary() -> dict[str, str]:
+    """``{"N,K,T": route}`` for every dW shape used so far in this process (for metrics / bench output)."""
+    return {",".join(str(v) for v in k): r for k, r in sorted(_route.items())}
 
 
 def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
@@ -173,7 +204,9 @@ def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
     key = (n, k, t)
     route = _route.get(key)
     if route is None:
-        route = _route[key] = _tune(key, _candidates(n, k, t), g, dy, x)
+        cands = _candidates(n, k, t)
+        fixed = _static_route.get(key)
+        route = _route[key] = fixed if fixed in cands else _tune(key, cands, g, dy, x)
     _run(route, g, dy, x)
 
 

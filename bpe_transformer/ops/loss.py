@@ -21,13 +21,17 @@ from . import reference as F
 from ._ext import ops
 
 IGNORE_INDEX = -100
-# LM head + CE in token chunks of this many rows (0 = one GEMM + one CE pass over the whole buffer)
-_LMHEAD_CHUNK = int(os.environ.get("BPE_LMHEAD_CHUNK", "0"))
+
+
+def default_lmhead_chunk() -> int:
+    """Token-chunk size of the LM head + CE when the caller passes none: ``BPE_LMHEAD_CHUNK`` (0 = one GEMM and one
+    CE pass over the whole buffer, the measured default: ``docs/performance.md``, knob A/B)."""
+    return int(os.environ.get("BPE_LMHEAD_CHUNK", "0"))
 
 
 class _LMHeadCEFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h: Tensor, w: Tensor, targets: Tensor, ignore_index: int):
+    def forward(ctx, h: Tensor, w: Tensor, targets: Tensor, ignore_index: int, chunk: int):
         V = w.shape[0]
         # zero-row padded weight (flat buffer, optim/flat.py): aligned GEMM shapes and logits row stride; the
         # pad columns of the logits are exactly 0 and the CE kernel never touches them, so their "gradient"
@@ -37,13 +41,15 @@ class _LMHeadCEFn(torch.autograd.Function):
             wp = w
         nvalid = (targets != ignore_index).sum().clamp_min(1).to(torch.float32)
         M = h.shape[0]
-        chunk = _LMHEAD_CHUNK if 0 < _LMHEAD_CHUNK < M else M
+        chunk = chunk if 0 < chunk < M else M
         if chunk == M:
             logits = torch.matmul(h, wp.t())  # hipBLASLt
             loss_rows, _ = ops().ce_fwd_bwd(logits[:, :V], targets, ignore_index, True, nvalid)
         else:
             # token chunks: each chunk's logits are still in the Infinity Cache when the CE kernel reads and
-            # rewrites them (one HBM pass instead of three over the [tokens, vocab] buffer)
+            # rewrites them (one HBM pass instead of three over the [tokens, vocab] buffer).  Every chunk divides
+            # by the GLOBAL count of valid targets, so the chunked loss and gradient equal the one-pass ones; the
+            # last chunk may be short.
             logits = h.new_empty(M, wp.shape[0])
             parts = []
             for c0 in range(0, M, chunk):
@@ -64,7 +70,7 @@ class _LMHeadCEFn(torch.autograd.Function):
         hs = h * gg
         mg = getattr(ctx.w_param, "_bpe_padded_grad" if ctx.padded else "main_grad", None)
         if ctx.padded and mg is None:
-            return dh, torch.matmul(dlogits.t(), hs)[: ctx.w_param.shape[0]], None, None
+            return dh, torch.matmul(dlogits.t(), hs)[: ctx.w_param.shape[0]], None, None, None
         if mg is not None:
             # weight gradient accumulated in place into the flat gradient buffer (no temporary, no grad add)
             from . import streams
@@ -81,8 +87,8 @@ class _LMHeadCEFn(torch.autograd.Function):
                     run()
             else:
                 run()
-            return dh, None, None, None
-        return dh, torch.matmul(dlogits.t(), hs), None, None
+            return dh, None, None, None, None
+        return dh, torch.matmul(dlogits.t(), hs), None, None, None
 
 
 class _CrossEntropyFn(torch.autograd.Function):
@@ -113,14 +119,18 @@ def cross_entropy(logits: Tensor, targets: Tensor, ignore_index: int = IGNORE_IN
     return F.cross_entropy(x[valid], t[valid])
 
 
-def lm_head_cross_entropy(h: Tensor, weight: Tensor, targets: Tensor, ignore_index: int = IGNORE_INDEX) -> Tensor:
+def lm_head_cross_entropy(h: Tensor, weight: Tensor, targets: Tensor, ignore_index: int = IGNORE_INDEX,
+                          chunk: int | None = None) -> Tensor:
     """``cross_entropy(h @ weight.T, targets)`` without keeping separate logits/probs/grad buffers.
 
-    h: ``[..., d]``, weight: ``[V, d]``, targets: ``[...]``.
+    h: ``[..., d]``, weight: ``[V, d]``, targets: ``[...]``.  ``chunk``: run the GEMM + CE in token chunks of
+    this many rows (0 = one pass; None = :func:`default_lmhead_chunk`).
     """
+    if chunk is None:
+        chunk = default_lmhead_chunk()
     d = h.shape[-1]
     h2 = h.reshape(-1, d)
     t = targets.reshape(-1).long().contiguous()
     if h.is_cuda and h.dtype in (torch.float32, torch.bfloat16):
-        return _LMHeadCEFn.apply(h2, weight, t, ignore_index)
+        return _LMHeadCEFn.apply(h2, weight, t, ignore_index, int(chunk))
     return cross_entropy(h2 @ weight.t(), t, ignore_index)

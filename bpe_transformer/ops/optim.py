@@ -68,18 +68,25 @@ def fused_adamw_step(
     weight_decay: float,
     step: int,
     grad_scale: Tensor | None = None,
+    nstep: Tensor | None = None,
 ) -> None:
     """One AdamW step over flat fp32 buffers (one kernel launch on the GPU).
 
     ``grad`` may be fp32 or bf16; ``param_bf16_out`` (optional) receives the
     bf16 copy of the updated fp32 master weights; ``grad_scale`` (optional
     0-dim fp32 device tensor) multiplies the gradient first (clip coefficient).
+    ``nstep`` (optional one-element int32 tensor, see :func:`count_adam_step`)
+    is the number of updates applied so far INCLUDING this one; when given,
+    the bias correction is computed from it (on the device) and ``step`` is
+    ignored, so skipped non-finite steps do not shift bc1/bc2.
     """
+    if nstep is not None and not param_fp32.is_cuda:
+        step = int(nstep.item())
     bc1 = 1.0 - beta1**step
     bc2_sqrt = (1.0 - beta2**step) ** 0.5
     if param_fp32.is_cuda:
         ops().adamw_step(param_fp32, exp_avg, exp_avg_sq, grad, param_bf16_out, lr, beta1, beta2, eps, weight_decay,
-                         bc1, bc2_sqrt, grad_scale)
+                         bc1, bc2_sqrt, grad_scale, nstep)
         return
     g = grad.float()
     if grad_scale is not None:
@@ -93,3 +100,14 @@ def fused_adamw_step(
     param_fp32.addcdiv_(exp_avg, denom, value=-lr / bc1)
     if param_bf16_out is not None:
         param_bf16_out.copy_(param_fp32)
+
+
+def count_adam_step(nstep: Tensor, grad_scale: Tensor | None = None) -> None:
+    """``nstep += 1`` unless ``grad_scale`` is the non-finite-norm sentinel (-1); on the device, no host sync.
+
+    Run once per optimizer step before the :func:`fused_adamw_step` launches that read ``nstep``.
+    """
+    if nstep.is_cuda:
+        ops().adam_count_step(nstep, grad_scale)
+    elif grad_scale is None or bool(grad_scale >= 0):
+        nstep.add_(1)

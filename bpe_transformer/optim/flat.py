@@ -32,7 +32,7 @@ from dataclasses import dataclass
 import torch
 from torch import Tensor, nn
 
-from ..ops.optim import fused_adamw_step, grad_norm
+from ..ops.optim import count_adam_step, fused_adamw_step, grad_norm
 
 ALIGN = 64
 
@@ -101,6 +101,11 @@ class FlatAdamW:
     Weight decay is applied to params with ``ndim >= 2`` by default (norm gains
     are not decayed); set ``decay_all=True`` for uniform decay.  Consecutive
     params with the same decay form one kernel launch.
+
+    The number of APPLIED updates lives on the device (``self.nstep``): a step
+    whose gradient norm is non-finite is skipped by the kernels and does not
+    advance it, so the bias correction and the checkpointed ``step`` count
+    only real updates.  ``calls`` counts :meth:`step` invocations on the host.
     """
 
     def __init__(self, flat: FlatParameters, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
@@ -109,20 +114,31 @@ class FlatAdamW:
         self.lr = lr
         self.betas = betas
         self.eps = eps
-        self.weight_decay = weight_decay
-        self.step_count = 0
+        self.decay_all = decay_all
+        self.calls = 0
+        self.nstep = torch.zeros(1, dtype=torch.int32, device=flat.device)
         self.master = flat.data.float() if flat.dtype != torch.float32 else flat.data
         self.exp_avg = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
         self.exp_avg_sq = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
-        # contiguous runs of equal weight decay
+        self.weight_decay = weight_decay
+        self._build_segments()
+
+    def _build_segments(self) -> None:
+        """Contiguous runs of equal weight decay (one kernel launch each), from ``self.weight_decay``."""
+        flat = self.flat
         self.segments: list[tuple[int, int, float]] = []
         for i, s in enumerate(flat.slots):
-            wd = weight_decay if (decay_all or s.param.dim() >= 2) else 0.0
+            wd = self.weight_decay if (self.decay_all or s.param.dim() >= 2) else 0.0
             end = flat.slots[i + 1].offset if i + 1 < len(flat.slots) else flat.numel
             if self.segments and self.segments[-1][2] == wd and self.segments[-1][1] == s.offset:
                 self.segments[-1] = (self.segments[-1][0], end, wd)
             else:
                 self.segments.append((s.offset, end, wd))
+
+    @property
+    def step_count(self) -> int:
+        """Updates actually applied (reads the device counter: a host sync)."""
+        return int(self.nstep.item())
 
     @torch.no_grad()
     def clip_grad_norm(self, max_norm: float) -> tuple[Tensor, Tensor]:
@@ -133,13 +149,14 @@ class FlatAdamW:
     def step(self, lr: float | None = None, grad_scale: Tensor | None = None) -> None:
         if lr is not None:
             self.lr = lr
-        self.step_count += 1
+        self.calls += 1
         b1, b2 = self.betas
         out = self.flat.data if self.flat.dtype == torch.bfloat16 else None
+        count_adam_step(self.nstep, grad_scale)
         for s, e, wd in self.segments:
             fused_adamw_step(
                 self.master[s:e], self.exp_avg[s:e], self.exp_avg_sq[s:e], self.flat.grad[s:e],
-                out[s:e] if out is not None else None, self.lr, b1, b2, self.eps, wd, self.step_count, grad_scale,
+                out[s:e] if out is not None else None, self.lr, b1, b2, self.eps, wd, 0, grad_scale, self.nstep,
             )
         if out is None and self.master is not self.flat.data:
             self.flat.data.copy_(self.master)
@@ -153,11 +170,12 @@ class FlatAdamW:
 
     @torch.no_grad()
     def load_state_dict(self, sd: dict) -> None:
-        self.step_count = int(sd["step"])
+        self.nstep.fill_(int(sd["step"]))
         self.lr = float(sd["lr"])
         self.betas = tuple(sd["betas"])
         self.eps = float(sd["eps"])
         self.weight_decay = float(sd["weight_decay"])
+        self._build_segments()  # the per-segment decay follows the restored value
         self.master.copy_(sd["master"])
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])

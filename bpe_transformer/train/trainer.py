@@ -150,6 +150,7 @@ class Trainer:
         prof_cm = torch_profile(Path(cfg.ckpt_dir) / "profile") if cfg.profile else None
         prof = prof_cm.__enter__() if prof_cm else None
         try:
+            routes_logged = False
             for it in range(self.start_iter, cfg.max_iters):
                 lr = self.schedule(it)
                 batches = [next(self.loader) for _ in range(cfg.grad_accum)]
@@ -171,6 +172,11 @@ class Trainer:
                                      tokens_per_s=tps,
                                      mfu=tps * flops_tok / (MI355X_BF16_DENSE_FLOPS * self.info.world_size),
                                      mem_gb=device_memory_gb(), **self.engine.phase_times())
+                    if not routes_logged and self.engine.flat.data.is_cuda:
+                        from ..ops.gemm import routes_summary
+
+                        self.metrics.log(step=step, dw_gemm_routes=routes_summary())  # kernel per dW shape
+                        routes_logged = True
                     if cfg.nan_guard and not math.isfinite(loss_v):
                         bad += 1
                         log.warning(f"non-finite loss at step {step} ({bad} consecutive)")

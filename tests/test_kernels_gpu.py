@@ -126,6 +126,43 @@ def test_lm_head_cross_entropy(gpu_device):
     assert rel(w.grad.cpu(), wr.grad) < 3e-2
 
 
+def test_lm_head_ce_chunked_matches_one_pass(gpu_device):
+    """Token-chunked LM head + CE == one pass: M not a multiple of the chunk, ignore_index rows, the row-padded
+    vocab weight from the flat buffer, and the LM-head dW accumulated in place into the flat gradient."""
+    from bpe_transformer.optim import FlatParameters
+
+    V, d, M = 5003, 256, 1000
+    torch.manual_seed(0)
+    head = torch.nn.Linear(d, V, bias=False).to(gpu_device, torch.bfloat16)
+    head.pad_rows = (V + 255) // 256 * 256
+    flat = FlatParameters.from_module(head)
+    assert head.weight._bpe_padded.shape[0] == head.pad_rows
+    h0 = torch.randn(M, d, device=gpu_device, dtype=torch.bfloat16)
+    t = torch.randint(0, V, (M,), device=gpu_device)
+    t[::7] = -100
+    out = {}
+    for chunk in (0, 384):
+        flat.zero_grad()
+        h = h0.clone().requires_grad_(True)
+        loss = ops.lm_head_cross_entropy(h, head.weight, t, chunk=chunk)
+        (3.0 * loss).backward()
+        torch.cuda.synchronize()
+        out[chunk] = (loss.detach().float(), h.grad.float(), flat.grad.float().clone())
+    (l0, dh0, g0), (l1, dh1, g1) = out[0], out[384]
+    # same math; only the library GEMM's per-chunk kernel choice (rounding of the bf16 logits) may differ
+    assert abs(l0.item() - l1.item()) < 1e-3
+    assert rel(dh1, dh0) < 1e-2
+    assert rel(g1, g0) < 1e-2
+    assert float(g0.view(-1)[V * d :].abs().max()) == 0.0  # pad rows get no gradient
+    hr = h0.float().cpu().requires_grad_(True)
+    wr = head.weight.detach().float().cpu().requires_grad_(True)
+    lr_ = torch.nn.functional.cross_entropy(hr @ wr.t(), t.cpu(), ignore_index=-100)
+    (3.0 * lr_).backward()
+    assert abs(l1.item() - lr_.item()) < 2e-2
+    assert rel(dh1.cpu(), hr.grad) < 3e-2
+    assert rel(g1[: V * d].view(V, d).cpu(), wr.grad) < 3e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_embedding(gpu_device, dtype):
     torch.manual_seed(0)
@@ -210,6 +247,19 @@ def test_flat_adamw_bf16_master(gpu_device):
         oref.step()
     for p, r in zip(lin.parameters(), ref):
         assert rel(p.detach(), r.detach().to(torch.bfloat16)) < 1e-2
+
+
+def test_flat_adamw_skip_keeps_bias_correction(gpu_device):
+    """HIP path: a skipped non-finite step does not advance the device step counter (bias correction), so the
+    run with an inf gradient in the middle ends at the same weights as the run without it (vs the CPU path)."""
+    from .test_trainer import _flat_opt_run
+
+    opt, flat = _flat_opt_run(gpu_device, skip_at=1)
+    ref, fref = _flat_opt_run(gpu_device)
+    cpu, fcpu = _flat_opt_run("cpu")
+    assert opt.calls == 5 and opt.step_count == 4
+    assert torch.equal(flat.data, fref.data)
+    torch.testing.assert_close(flat.data.cpu(), fcpu.data, rtol=1e-5, atol=1e-6)
 
 
 def test_grad_norm_clip(gpu_device):

@@ -78,6 +78,48 @@ def test_nonfinite_grad_skips_update():
     assert torch.equal(flat.data, before)
 
 
+def _flat_opt_run(device, skip_at=None, steps=4, wd=0.1):
+    from bpe_transformer.optim import FlatAdamW, FlatParameters
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(8, 8).to(device)
+    flat = FlatParameters.from_module(lin)
+    opt = FlatAdamW(flat, lr=1e-2, weight_decay=wd)
+    g = torch.Generator().manual_seed(3)
+    grads = [torch.randn(flat.numel, generator=g).to(device) for _ in range(steps)]
+    it = iter(grads)
+    for i in range(steps + (skip_at is not None)):
+        if i == skip_at:
+            flat.grad.fill_(float("inf"))
+        else:
+            flat.grad.copy_(next(it))
+        _, coef = opt.clip_grad_norm(1e9)
+        opt.step(grad_scale=coef)
+    return opt, flat
+
+
+def test_skipped_step_does_not_advance_bias_correction():
+    """A non-finite step is skipped WITHOUT counting: the updates after it equal a run that never saw it, and the
+    checkpointed step is the number of applied updates (bias correction drifted on skipped steps)."""
+    ref, fref = _flat_opt_run("cpu")
+    opt, flat = _flat_opt_run("cpu", skip_at=2)
+    assert opt.calls == 5 and opt.step_count == 4 and opt.state_dict()["step"] == 4
+    torch.testing.assert_close(flat.data, fref.data, rtol=0, atol=0)
+
+
+def test_load_state_dict_rebuilds_weight_decay_segments():
+    from bpe_transformer.optim import FlatAdamW, FlatParameters
+
+    lin = torch.nn.Linear(4, 4)
+    flat = FlatParameters.from_module(lin)
+    src = FlatAdamW(flat, lr=1e-2, weight_decay=0.3)
+    dst = FlatAdamW(flat, lr=1e-2, weight_decay=0.0)
+    dst.load_state_dict(src.state_dict())
+    assert dst.weight_decay == 0.3
+    assert {wd for _, _, wd in dst.segments} == {0.3, 0.0}  # weight decayed, bias not
+    assert dst.segments == src.segments
+
+
 def test_config_overrides_and_cli(tmp_path, capsys):
     cfg = apply_overrides(TrainConfig(), ["optim.lr=0.01", "batch_size=3", "model.num_layers=1"])
     assert cfg.optim.lr == 0.01 and cfg.batch_size == 3 and cfg.model.num_layers == 1
