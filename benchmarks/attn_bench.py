@@ -21,31 +21,60 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-rope", action="store_true", help="plain attention (isolates the fused-RoPE cost)")
+    ap.add_argument("--mode", choices=["block", "fused"], default="block",
+                    help="block = the training path (rope_qk_ in place, then pre-rotated kernels; rope time reported "
+                         "separately and included in fwd_ms); fused = RoPE inside the attention kernels")
     a = ap.parse_args()
     B, S, H, D = a.batch, a.seq, a.heads, a.dim
     Hkv = a.kv_heads or H
     qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     cos, sin = (None, None) if a.no_rope else R.rope_tables(D, S, 10000.0, device="cuda")
     do = torch.randn(B * S, H * D, device="cuda", dtype=torch.bfloat16)
+    from bpe_transformer.ops._ext import ops as _ops
+
+    hip = _ops()
+    scale = 1.0 / D ** 0.5
+    rope = cos is not None
+    pre = a.mode == "block" and rope
+    x = qkv.detach().clone()
+    q, k, v = x[:, : H * D], x[:, H * D : (H + Hkv) * D], x[:, (H + Hkv) * D :]
+    c = cos if rope else torch.empty(0, 0, device="cuda")
+    s_ = sin if rope else torch.empty(0, 0, device="cuda")
+
+    def fwd():
+        if pre:
+            hip.rope_qk_(x, c, s_, B, S, H, Hkv, D)  # in place, as the fused block does (values drift: timing only)
+        return hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
+
+    def bwd(o, lse):
+        return hip.fa_bwd(do, q, k, v, o, lse, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
+
     for _ in range(3):
-        o = ops.flash_attention_qkv(qkv, B, S, H, Hkv, D, cos, sin, True)
-        o.backward(do)
+        o, lse = fwd()
+        bwd(o, lse)
     torch.cuda.synchronize()
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    tf, tb = 0.0, 0.0
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    tf, tb, tr = 0.0, 0.0, 0.0
     for _ in range(a.iters):
+        x.copy_(qkv.detach())
         e[0].record()
-        o = ops.flash_attention_qkv(qkv, B, S, H, Hkv, D, cos, sin, True)
+        if pre:
+            hip.rope_qk_(x, c, s_, B, S, H, Hkv, D)
+        e[3].record()
+        o, lse = hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
         e[1].record()
-        o.backward(do)
+        bwd(o, lse)
         e[2].record()
         torch.cuda.synchronize()
+        tr += e[0].elapsed_time(e[3])
         tf += e[0].elapsed_time(e[1])
         tb += e[1].elapsed_time(e[2])
     tf /= a.iters
     tb /= a.iters
+    tr /= a.iters
     fl = 4.0 * B * H * S * S * D / 2
-    print(json.dumps({"shape": [B, S, H, Hkv, D], "rope": not a.no_rope, "fwd_ms": round(tf, 4), "bwd_ms": round(tb, 4),
+    print(json.dumps({"shape": [B, S, H, Hkv, D], "rope": rope, "mode": a.mode, "rope_ms": round(tr, 4),
+                      "fwd_ms": round(tf, 4), "bwd_ms": round(tb, 4),
                       "fwd_tflops": round(fl / tf / 1e9, 1), "bwd_tflops": round(2.5 * fl / tb / 1e9, 1)}))
 
 

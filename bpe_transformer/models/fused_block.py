@@ -6,7 +6,8 @@ forward::
 
     h1 = rmsnorm(x; ln1)              HIP
     qkv = h1 @ [Wq;Wk;Wv]^T           hipBLASLt (one GEMM)
-    o = flash_attn(qkv) (+RoPE)       HIP
+    rope_qk_(qkv)                     HIP, in place on Q / K (D = 64; D = 128 rotates inside attention)
+    o = flash_attn(qkv)               HIP
     xm = x + o @ Wo^T                 hipBLASLt addmm (residual folded into the GEMM)
     h2 = rmsnorm(xm; ln2)             HIP
     gu = h2 @ [W1;W3]^T               hipBLASLt (one GEMM)
@@ -43,6 +44,7 @@ from torch import Tensor
 
 from ..ops import streams
 from ..ops._ext import ops as hip
+from ..ops.attention import prerotate_default
 from ..ops.gemm import accumulate_weight_grad
 
 
@@ -112,8 +114,11 @@ class FusedBlockFn(torch.autograd.Function):
             qkv = mm(h1, w_qkv, 0)
         else:
             qkv = torch.matmul(h1, w_qkv.t())
+        pre = use_rope and prerotate_default(D)
+        if pre:  # RoPE once, in place on Q / K of the QKV activation (saved rotated for the backward)
+            hip().rope_qk_(qkv, cos, sin, B, S, H, Hkv, D)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
-        o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale)
+        o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, pre)
         g1 = mm(o, wo.detach(), 1) if fp8 is not None else torch.matmul(o, wo.t())
         xm, h2, r2 = hip().add_rmsnorm_fwd(x2, g1, ln2, eps)
         gu = mm(h2, w_13, 2) if fp8 is not None else torch.matmul(h2, w_13.t())
@@ -124,6 +129,7 @@ class FusedBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x2, r1, h1, qkv, o, lse, xm, r2, h2, gu, a, cos, sin)
         ctx.params = (ln1, wq, wk, wv, wo, ln2, w1, w3, w2)
         ctx.meta = meta
+        ctx.prerotated = pre
         return xm, g2  # block output = xm + g2, added by the consumer
 
     @staticmethod
@@ -193,7 +199,7 @@ class FusedBlockFn(torch.autograd.Function):
         acc_weight([wo], dxm, o)
         do = dx(dxm, [wo], 1)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
-        dqkv = hip().fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, use_rope, scale)
+        dqkv = hip().fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, ctx.prerotated)
         acc_weight([wq, wk, wv], dqkv, h1)
         dh1 = dx(dqkv, [wq, wk, wv], 0)
         dx2, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm)

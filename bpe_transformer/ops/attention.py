@@ -10,6 +10,7 @@ directly.  Reference contracts K7/K9/K10 (``tests/adapters.py:92-184``).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch import Tensor
@@ -30,29 +31,41 @@ def _empty(dev: torch.device) -> Tensor:
     return t
 
 
+def prerotate_default(head_dim: int) -> bool:
+    """Rotate Q / K once in the QKV activation (``rope_qk_``) instead of inside the attention kernels: the
+    D = 64 forward (v3) then stages K by LDS-DMA with no per-tile rotation.  ``BPE_ROPE_PREROTATE=0`` keeps the
+    fused-RoPE kernels."""
+    return head_dim == 64 and os.environ.get("BPE_ROPE_PREROTATE", "1") == "1"
+
+
 class _FlashAttnQKVFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv: Tensor, cos, sin, B: int, S: int, H: int, Hkv: int, D: int, causal: bool, scale: float):
-        q = qkv[:, : H * D]
-        k = qkv[:, H * D : (H + Hkv) * D]
-        v = qkv[:, (H + Hkv) * D :]
+    def forward(ctx, qkv: Tensor, cos, sin, B: int, S: int, H: int, Hkv: int, D: int, causal: bool, scale: float,
+                prerotate: bool):
         use_rope = cos is not None
         c = cos if use_rope else _empty(qkv.device)
         s = sin if use_rope else _empty(qkv.device)
-        o, lse = ops().fa_fwd(q, k, v, c, s, B, S, H, Hkv, D, causal, use_rope, scale)
+        pre = use_rope and prerotate
+        if pre:  # rotate a copy (the input belongs to autograd); the backward re-reads the rotated copy
+            qkv = qkv.clone()
+            ops().rope_qk_(qkv, c, s, B, S, H, Hkv, D)
+        q = qkv[:, : H * D]
+        k = qkv[:, H * D : (H + Hkv) * D]
+        v = qkv[:, (H + Hkv) * D :]
+        o, lse = ops().fa_fwd(q, k, v, c, s, B, S, H, Hkv, D, causal, use_rope, scale, pre)
         ctx.save_for_backward(qkv, o, lse, c, s)
-        ctx.meta = (B, S, H, Hkv, D, causal, use_rope, scale)
+        ctx.meta = (B, S, H, Hkv, D, causal, use_rope, scale, pre)
         return o
 
     @staticmethod
     def backward(ctx, do: Tensor):
         qkv, o, lse, c, s = ctx.saved_tensors
-        B, S, H, Hkv, D, causal, use_rope, scale = ctx.meta
+        B, S, H, Hkv, D, causal, use_rope, scale, pre = ctx.meta
         q = qkv[:, : H * D]
         k = qkv[:, H * D : (H + Hkv) * D]
         v = qkv[:, (H + Hkv) * D :]
-        dqkv = ops().fa_bwd(do, q, k, v, o, lse, c, s, B, S, H, Hkv, D, causal, use_rope, scale)
-        return dqkv, None, None, None, None, None, None, None, None, None
+        dqkv = ops().fa_bwd(do, q, k, v, o, lse, c, s, B, S, H, Hkv, D, causal, use_rope, scale, pre)
+        return dqkv, None, None, None, None, None, None, None, None, None, None
 
 
 def flash_supported(x: Tensor, head_dim: int) -> bool:
@@ -70,13 +83,18 @@ def flash_attention_qkv(
     sin: Tensor | None = None,
     causal: bool = True,
     scale: float | None = None,
+    prerotate: bool | None = None,
 ) -> Tensor:
     """Attention over a fused QKV activation.
 
     qkv: ``[batch*seq, (n_heads + 2*n_kv_heads) * head_dim]`` bf16 on the GPU.
     cos/sin: fp32 ``[>=seq, head_dim/2]`` RoPE tables (positions ``0..seq-1``),
     or ``None`` for no RoPE.  Returns ``[batch*seq, n_heads*head_dim]``.
+    ``prerotate``: apply RoPE to a copy of Q / K first (``rope_qk_``) and run the
+    kernels in pre-rotated mode (default :func:`prerotate_default`).
     """
+    if prerotate is None:
+        prerotate = prerotate_default(head_dim)
     scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
     if qkv.is_cuda:
         if qkv.stride(1) != 1 or qkv.stride(0) % 8 != 0:
@@ -84,7 +102,8 @@ def flash_attention_qkv(
         if cos is not None:
             cos = cos.float().contiguous()
             sin = sin.float().contiguous()
-        return _FlashAttnQKVFn.apply(qkv, cos, sin, batch, seq, n_heads, n_kv_heads, head_dim, causal, scale)
+        return _FlashAttnQKVFn.apply(qkv, cos, sin, batch, seq, n_heads, n_kv_heads, head_dim, causal, scale,
+                                     bool(prerotate))
     return attention_qkv_reference(qkv, batch, seq, n_heads, n_kv_heads, head_dim, cos, sin, causal, scale)
 
 

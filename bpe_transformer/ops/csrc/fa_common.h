@@ -15,6 +15,8 @@
 #pragma once
 #include "common.h"
 
+#include <cstdlib>
+
 namespace bpe {
 namespace fa {
 
@@ -100,6 +102,31 @@ __device__ __forceinline__ u16x8 rope_u16x8(u16x8 v, const float* cs, const floa
     unpack8(v, x);
     rope8(x, cs, sn);
     return pack8(x, mul);
+}
+
+// Launch order of the (block, batch*head) work items: heads are taken in groups of `group` (batch, head) pairs
+// and, inside a group, the `nblk` blocks of every pair run heaviest first (index 0 = heaviest).  All blocks of a
+// pair thus run close together in time, so the K / V (forward) or Q / dO (backward) rows they share are re-read
+// from L2 / the Infinity Cache instead of HBM: with the plain "all pairs' heaviest block first" order the whole
+// grid's K / V (393 MB at GPT-2 B 128) streamed through between two uses of a pair.  With group % 8 == 0 the
+// blocks of one pair share blockIdx % 8, i.e. an XCD L2 under round-robin dispatch (speed only, not
+// correctness).  Returns the block rank (0 = heaviest) and the pair index.
+__device__ __forceinline__ void grouped_order(int bid, int nblk, int BH, int group, int& rank, int& bh) {
+    const int per = nblk * group;
+    const int g = bid / per;
+    const int r = bid - g * per;
+    const int gs = min(group, BH - g * group);  // the last group may be short
+    rank = r / gs;
+    bh = g * group + (r - rank * gs);
+}
+
+// Host: pairs per launch-order group, BPE_FA_GROUP (default 64; 0 = one group of all pairs, the old order).
+inline int fa_group(int BH) {
+    static const int g = [] {
+        const char* e = getenv("BPE_FA_GROUP");
+        return e ? atoi(e) : 64;
+    }();
+    return (g <= 0 || g > BH) ? BH : g;
 }
 
 }  // namespace fa

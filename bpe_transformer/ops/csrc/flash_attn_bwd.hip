@@ -115,15 +115,17 @@ __device__ __forceinline__ void softmax_ds(f32x16& sp, f32x16& dp, int hh, float
 }
 
 // DBG (timing diagnostics, numerically wrong; built only with -DBPE_FA_DIAG): bit 1 = no dQ phase,
-// bit 2 = no softmax (P = S), bit 3 = no next-tile global loads
-template <int D, bool CAUSAL, bool ROPE, int DBG = 0>
+// bit 2 = no softmax (P = S), bit 3 = no next-tile global loads.
+// ROPE: dK is un-rotated on output (and dQ by the convert kernel); ROPE_IN: Q / K are rotated on load too
+// (false when ops.rope_qk_ rotated them in the QKV activation already, rope mode 2).
+template <int D, bool CAUSAL, bool ROPE, int DBG = 0, bool ROPE_IN = ROPE>
 __global__ void __launch_bounds__(BwdCfg<D>::NW * 64, BwdCfg<D>::WGS)
 fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv, long ld_q,
               long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
               const float* __restrict__ DELTA, float* __restrict__ dQacc, __bf16* __restrict__ dK,
               __bf16* __restrict__ dV, long ld_dkv, float* __restrict__ dKVpart, const float* __restrict__ cosT,
               const float* __restrict__ sinT, int B, int H, int Hkv, int S, float scale_log2, float scale,
-              int flags) {
+              int flags, int group) {
     using C = BwdCfg<D>;
     constexpr int NW = C::NW, NT = NW * 64, RB = C::RB, CPR = D / 8, QT = C::QT;
     constexpr int SPT = (64 * CPR + NT - 1) / NT;  // staged chunks per thread per tile (Q and dO each)
@@ -142,8 +144,8 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     // parallel (their dK / dV partials are summed by fa_dkv_reduce_kernel) instead of one workgroup sweeping
     // all G heads -- with causal masking that serial sweep left most CUs idle behind the key-block-0 groups.
     const int BH = B * H;
-    const int kb = (int)(blockIdx.x / BH);
-    const int bh = blockIdx.x % BH;
+    int kb, bh;  // kb 0 (the most query tiles under the causal mask) first inside each group of pairs
+    grouped_order((int)blockIdx.x, (S + C::KB - 1) / C::KB, BH, group, kb, bh);
     const int b = bh / H, h = bh % H;
     const int G = H / Hkv;
     const int hk = h / G;
@@ -162,7 +164,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
             const int d0 = 16 * ks + 8 * hh;
             u16x8 tk = key_ok ? *reinterpret_cast<const u16x8*>(kp + d0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
             u16x8 tv = key_ok ? *reinterpret_cast<const u16x8*>(vp + d0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-            if (ROPE) tk = rope_u16x8(tk, cosT + kpos * (D / 2) + d0 / 2, sinT + kpos * (D / 2) + d0 / 2, 1.f);
+            if (ROPE_IN) tk = rope_u16x8(tk, cosT + kpos * (D / 2) + d0 / 2, sinT + kpos * (D / 2) + d0 / 2, 1.f);
             *reinterpret_cast<u16x8*>(Kl + swz<RB>(32 * w + l31, 2 * ks + hh)) = tk;
             *reinterpret_cast<u16x8*>(Vl + swz<RB>(32 * w + l31, 2 * ks + hh)) = tv;
         }
@@ -210,7 +212,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
             const int e = tid + NT * i, row = e / CPR, c = e % CPR;
             if (e >= 64 * CPR) break;
             u16x8 qv = qreg[i];
-            if (ROPE) {
+            if (ROPE_IN) {
                 const long qq = min(m0 + row, S - 1);
                 qv = rope_u16x8(qv, cosT + qq * (D / 2) + c * 4, sinT + qq * (D / 2) + c * 4, 1.f);
             }
@@ -467,18 +469,26 @@ using namespace bpe::fa;
 
 size_t fa_bwd_lds_bytes(int D) { return D == 64 ? BwdCfg<64>::LDS : BwdCfg<128>::LDS; }
 
-template <int D, bool C, bool R, int DBG>
-static void bwd_main(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
+template <int D, bool C, bool R, int DBG, bool RIN>
+static void bwd_main_k(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
     using Cfg = BwdCfg<D>;
     static bool lds_attr = false;  // > 64 KiB of dynamic LDS: opt in once (before any graph capture)
     if (!lds_attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fa_bwd_kernel<D, C, R, DBG>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fa_bwd_kernel<D, C, R, DBG, RIN>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
         lds_attr = true;
     }
-    fa_bwd_kernel<D, C, R, DBG><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
+    fa_bwd_kernel<D, C, R, DBG, RIN><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv,
-        a.dkv_part, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, dbg);
+        a.dkv_part, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, dbg, fa_group(a.B * a.H));
+}
+
+template <int D, bool C, bool R, int DBG>
+static void bwd_main(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
+    if (R && a.rope == 2)
+        bwd_main_k<D, C, R, DBG, false>(a, s, nkb, dbg);  // Q / K pre-rotated: only the outputs are rotated back
+    else
+        bwd_main_k<D, C, R, DBG, R>(a, s, nkb, dbg);
 }
 
 template <int D, bool C, bool R>
@@ -525,6 +535,7 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
 }
 
 void launch_fa_bwd(const FaArgs& a, hipStream_t s) {
+    // a.rope: 0 none, 1 rotate Q / K on load and dQ / dK on output, 2 outputs only (Q / K pre-rotated)
 #define BWD_CASE(DD)                                                                                        \
     if (a.D == DD) {                                                                                        \
         if (a.causal) { if (a.rope) bwd_launch<DD, true, true>(a, s); else bwd_launch<DD, true, false>(a, s); } \

@@ -72,6 +72,8 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
                                long ldg, int M, int F, int R, hipStream_t s);
 
 // rope.hip
+void launch_rope_qk(void* qkv, long ld, const float* cosT, const float* sinT, long rows, int S, int H, int Hkv, int D,
+                    hipStream_t s);
 void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,
                  size_t R, int H, int D, int inverse, hipStream_t s);
 
@@ -87,7 +89,7 @@ struct FaArgs {
     const float* cos;  // [S_max, D/2]
     const float* sin;
     int B, H, Hkv, S, D;
-    int causal, rope;
+    int causal, rope;  // rope: 0 none, 1 fused (rotate Q/K on load, un-rotate dQ/dK), 2 Q/K pre-rotated (rope_qk_)
     float scale;
     // backward only
     const __bf16* dout;

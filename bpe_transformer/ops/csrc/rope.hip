@@ -42,9 +42,45 @@ __global__ void __launch_bounds__(256) rope_kernel(const T* __restrict__ x, T* _
     }
 }
 
+// In-place RoPE on the Q and K column ranges of a fused QKV activation [B*S, (H + 2 Hkv) * D] (row stride ld,
+// positions 0..S-1 in every sequence): the training path rotates Q and K ONCE here, so the flash-attention
+// forward stages K tiles by LDS-DMA with no per-tile rotation and the backward re-reads rotated Q / K (it
+// un-rotates dQ / dK on output).  One 16-byte chunk (4 pairs) per thread step; V columns are not touched.
+__global__ void __launch_bounds__(256) rope_qk_kernel(__bf16* __restrict__ qkv, long ld, const float* __restrict__ cosT,
+                                                      const float* __restrict__ sinT, long rows, int S, int cpr,
+                                                      int D) {
+    const long total = rows * cpr;  // cpr = (H + Hkv) * D / 8 chunks per row
+    const int half = D / 2;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const long r = i / cpr;
+        const int c = (int)(i - r * cpr);
+        const int d0 = (c * 8) % D;
+        const long p = r % S;
+        __bf16* px = qkv + r * ld + c * 8;
+        const u16x8 v = *reinterpret_cast<const u16x8*>(px);
+        const f32x4 cs = *reinterpret_cast<const f32x4*>(cosT + p * half + d0 / 2);
+        const f32x4 sn = *reinterpret_cast<const f32x4*>(sinT + p * half + d0 / 2);
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float a = bf2f(v[2 * j]), b = bf2f(v[2 * j + 1]);
+            o[2 * j] = f2bf(a * cs[j] - b * sn[j]);
+            o[2 * j + 1] = f2bf(a * sn[j] + b * cs[j]);
+        }
+        *reinterpret_cast<u16x8*>(px) = o;
+    }
+}
+
 }  // namespace bpe
 
 using namespace bpe;
+
+void launch_rope_qk(void* qkv, long ld, const float* cosT, const float* sinT, long rows, int S, int H, int Hkv, int D,
+                    hipStream_t s) {
+    const int cpr = (H + Hkv) * D / 8;
+    const int grid = stream_grid((size_t)rows * cpr, 256, 8192);
+    rope_qk_kernel<<<grid, 256, 0, s>>>((__bf16*)qkv, ld, cosT, sinT, rows, S, cpr, D);
+}
 
 void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,
                  size_t R, int H, int D, int inverse, hipStream_t s) {

@@ -439,16 +439,35 @@ void check_qkv(const at::Tensor& t, int64_t rows, int64_t cols, const char* name
                 name, " rows must be 16-byte aligned");
 }
 
+// In-place RoPE of the Q and K heads of a fused QKV activation [B*S, (H + 2 Hkv) * D] (positions 0..S-1 per
+// sequence); attention then runs in rope mode 2 (pre-rotated inputs).
+void rope_qk_(at::Tensor qkv, const at::Tensor& cos, const at::Tensor& sin, int64_t B, int64_t S, int64_t H,
+              int64_t Hkv, int64_t D) {
+    check_cuda(qkv, "qkv");
+    TORCH_CHECK(qkv.scalar_type() == at::kBFloat16, "rope_qk_: bf16 qkv required");
+    TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * S && qkv.size(1) >= (H + Hkv) * D && qkv.stride(1) == 1,
+                "rope_qk_: qkv must be [B*S, >= (H + Hkv) * D] with unit column stride");
+    TORCH_CHECK(qkv.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(qkv.data_ptr()) % 16 == 0 && D % 8 == 0,
+                "rope_qk_: rows must be 16-byte aligned");
+    TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.dim() == 2 && cos.size(0) >= S && cos.size(1) == D / 2 &&
+                    cos.is_contiguous() && sin.is_contiguous() && sin.sizes() == cos.sizes(),
+                "rope_qk_: rope tables must be fp32 [>=S, D/2]");
+    DevGuard g(qkv.device());
+    launch_rope_qk(qkv.data_ptr(), qkv.stride(0), cos.data_ptr<float>(), sin.data_ptr<float>(), B * S, (int)S,
+                   (int)H, (int)Hkv, (int)D, cur_stream());
+}
+
 std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                           const at::Tensor& cos, const at::Tensor& sin, int64_t B, int64_t S, int64_t H,
-                                          int64_t Hkv, int64_t D, bool causal, bool use_rope, double scale) {
+                                          int64_t Hkv, int64_t D, bool causal, bool use_rope, double scale,
+                                          bool prerotated) {
     TORCH_CHECK(D == 64 || D == 128, "flash attention: head dim must be 64 or 128");
     TORCH_CHECK(H % Hkv == 0, "flash attention: H must be a multiple of Hkv");
     check_qkv(q, B * S, H * D, "q");
     check_qkv(k, B * S, Hkv * D, "k");
     check_qkv(v, B * S, Hkv * D, "v");
     TORCH_CHECK(k.stride(0) == v.stride(0), "flash attention: k and v must share a row stride");
-    if (use_rope)
+    if (use_rope && !prerotated)
         TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.size(0) >= S && cos.size(1) == D / 2 && cos.is_contiguous()
                         && sin.is_contiguous(), "flash attention: rope tables must be fp32 [>=S, D/2]");
     DevGuard g(q.device());
@@ -458,9 +477,10 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
     a.q = (const __bf16*)q.data_ptr(); a.k = (const __bf16*)k.data_ptr(); a.v = (const __bf16*)v.data_ptr();
     a.ld_q = q.stride(0); a.ld_kv = k.stride(0);
     a.o = (__bf16*)o.data_ptr(); a.ld_o = H * D; a.lse = lse.data_ptr<float>();
-    a.cos = use_rope ? cos.data_ptr<float>() : nullptr; a.sin = use_rope ? sin.data_ptr<float>() : nullptr;
+    const bool fused_rope = use_rope && !prerotated;
+    a.cos = fused_rope ? cos.data_ptr<float>() : nullptr; a.sin = fused_rope ? sin.data_ptr<float>() : nullptr;
     a.B = (int)B; a.H = (int)H; a.Hkv = (int)Hkv; a.S = (int)S; a.D = (int)D;
-    a.causal = causal; a.rope = use_rope; a.scale = (float)scale;
+    a.causal = causal; a.rope = use_rope ? (prerotated ? 2 : 1) : 0; a.scale = (float)scale;
     launch_fa_fwd(a, cur_stream());
     return {o, lse};
 }
@@ -468,9 +488,13 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
 // Returns dqkv = [B*S, (H + 2*Hkv) * D]: dq | dk | dv in the fused QKV-projection layout.
 at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                   const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cos, const at::Tensor& sin, int64_t B,
-                  int64_t S, int64_t H, int64_t Hkv, int64_t D, bool causal, bool use_rope, double scale) {
+                  int64_t S, int64_t H, int64_t Hkv, int64_t D, bool causal, bool use_rope, double scale,
+                  bool prerotated) {
     TORCH_CHECK(D == 64 || D == 128, "flash attention: head dim must be 64 or 128");
     TORCH_CHECK(Hkv > 0 && H % Hkv == 0, "flash attention: H must be a multiple of Hkv");
+    if (use_rope)
+        TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.size(0) >= S && cos.size(1) == D / 2 && cos.is_contiguous()
+                        && sin.is_contiguous(), "flash attention: rope tables must be fp32 [>=S, D/2]");
     check_qkv(q, B * S, H * D, "q");
     check_qkv(k, B * S, Hkv * D, "k");
     check_qkv(v, B * S, Hkv * D, "v");
@@ -490,7 +514,7 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     a.o = (__bf16*)o.data_ptr(); a.ld_o = o.stride(0); a.lse = lse.data_ptr<float>();
     a.cos = use_rope ? cos.data_ptr<float>() : nullptr; a.sin = use_rope ? sin.data_ptr<float>() : nullptr;
     a.B = (int)B; a.H = (int)H; a.Hkv = (int)Hkv; a.S = (int)S; a.D = (int)D;
-    a.causal = causal; a.rope = use_rope; a.scale = (float)scale;
+    a.causal = causal; a.rope = use_rope ? (prerotated ? 2 : 1) : 0; a.scale = (float)scale;
     a.dout = (const __bf16*)d.data_ptr(); a.ld_do = d.stride(0);
     a.delta = delta.data_ptr<float>(); a.dq_acc = dq_acc.data_ptr<float>();
     __bf16* base = (__bf16*)dqkv.data_ptr();
@@ -717,9 +741,10 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("softmax_bwd(Tensor dy, Tensor y) -> Tensor");
     m.def("rope(Tensor x, Tensor pos, Tensor cos, Tensor sin, bool inverse) -> Tensor");
     m.def("fa_fwd(Tensor q, Tensor k, Tensor v, Tensor cos, Tensor sin, int B, int S, int H, int Hkv, int D, "
-          "bool causal, bool rope, float scale) -> (Tensor, Tensor)");
+          "bool causal, bool rope, float scale, bool prerotated=False) -> (Tensor, Tensor)");
     m.def("fa_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor cos, Tensor sin, int B, "
-          "int S, int H, int Hkv, int D, bool causal, bool rope, float scale) -> Tensor");
+          "int S, int H, int Hkv, int D, bool causal, bool rope, float scale, bool prerotated=False) -> Tensor");
+    m.def("rope_qk_(Tensor(a!) qkv, Tensor cos, Tensor sin, int B, int S, int H, int Hkv, int D) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
@@ -748,6 +773,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("rope", &rope);
     m.impl("fa_fwd", &fa_fwd);
     m.impl("fa_bwd", &fa_bwd);
+    m.impl("rope_qk_", &rope_qk_);
     m.impl("kv_append", &kv_append);
     m.impl("decode_attn", &decode_attn);
     m.impl("decode_gemv", &decode_gemv);

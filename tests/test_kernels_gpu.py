@@ -375,14 +375,14 @@ def test_weight_grad_accumulate(gpu_device):
 
 
 # ---------------------------------------------------------------- flash attention
-def _fa_case(gpu_device, B, S, H, Hkv, D, rope, causal, seed=0):
+def _fa_case(gpu_device, B, S, H, Hkv, D, rope, causal, seed=0, prerotate=None):
     torch.manual_seed(seed)
     W = (H + 2 * Hkv) * D
     qkv = torch.randn(B * S, W, device=gpu_device, dtype=torch.bfloat16).requires_grad_(True)
     cos = sin = None
     if rope:
         cos, sin = R.rope_tables(D, S + 16, 10000.0, device=gpu_device)
-    o = ops.flash_attention_qkv(qkv, B, S, H, Hkv, D, cos, sin, causal)
+    o = ops.flash_attention_qkv(qkv, B, S, H, Hkv, D, cos, sin, causal, prerotate=prerotate)
     do = torch.randn_like(o)
     o.backward(do)
     qr = qkv.detach().float().cpu().requires_grad_(True)
@@ -392,11 +392,13 @@ def _fa_case(gpu_device, B, S, H, Hkv, D, rope, causal, seed=0):
     return o, qkv.grad, orf.detach(), qr.grad
 
 
-@pytest.mark.parametrize("S", [128, 256, 200, 64])
-@pytest.mark.parametrize("rope", [True, False])
+@pytest.mark.parametrize("S", [128, 256, 200, 64, 1000])
+@pytest.mark.parametrize("rope", ["fused", "prerotated", None])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_d64(gpu_device, S, rope, causal):
-    o, g, orf, gr = _fa_case(gpu_device, 2, S, 4, 4, 64, rope, causal)
+    """D = 64: fused-RoPE kernels (rope "fused"), the v3 forward with Q / K rotated by rope_qk_ ("prerotated")
+    and without RoPE (None, v3 forward); S not a multiple of 64 covers the clamped DMA rows and masked tail."""
+    o, g, orf, gr = _fa_case(gpu_device, 2, S, 4, 4, 64, rope is not None, causal, prerotate=rope == "prerotated")
     assert rel(o.cpu(), orf) < 2e-2, rel(o.cpu(), orf)
     HD = 4 * 64
     for name, sl in (("dq", slice(0, HD)), ("dk", slice(HD, 2 * HD)), ("dv", slice(2 * HD, 3 * HD))):
@@ -404,9 +406,10 @@ def test_flash_attention_d64(gpu_device, S, rope, causal):
         assert e < 3e-2, (name, e)
 
 
+@pytest.mark.parametrize("pre", [True, False])
 @pytest.mark.parametrize("D,H,Hkv", [(128, 4, 4), (64, 8, 2), (128, 8, 4), (64, 32, 4)])
-def test_flash_attention_d128_and_gqa(gpu_device, D, H, Hkv):
-    o, g, orf, gr = _fa_case(gpu_device, 2, 192, H, Hkv, D, True, True, seed=1)
+def test_flash_attention_d128_and_gqa(gpu_device, D, H, Hkv, pre):
+    o, g, orf, gr = _fa_case(gpu_device, 2, 192, H, Hkv, D, True, True, seed=1, prerotate=pre)
     assert rel(o.cpu(), orf) < 2e-2
     assert rel(g.cpu(), gr) < 3e-2
 
@@ -415,6 +418,22 @@ def test_flash_attention_gpt2_shape(gpu_device):
     o, g, orf, gr = _fa_case(gpu_device, 1, 1024, 12, 12, 64, True, True, seed=2)
     assert rel(o.cpu(), orf) < 2e-2
     assert rel(g.cpu(), gr) < 3e-2
+
+
+def test_rope_qk_inplace(gpu_device):
+    """rope_qk_ rotates exactly the Q and K heads of the fused activation (positions restart per sequence)."""
+    torch.manual_seed(4)
+    B, S, H, Hkv, D = 2, 100, 4, 2, 64
+    qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device=gpu_device, dtype=torch.bfloat16)
+    cos, sin = R.rope_tables(D, S + 7, 10000.0, device=gpu_device)
+    out = qkv.clone()
+    torch.ops.bpe_hip.rope_qk_(out, cos, sin, B, S, H, Hkv, D)
+    x = qkv.float().cpu().view(B, S, H + 2 * Hkv, D).transpose(1, 2)  # [B, heads, S, D]
+    ref = x.clone()
+    ref[:, : H + Hkv] = R.apply_rope(x[:, : H + Hkv], cos.cpu(), sin.cpu())
+    ref = ref.transpose(1, 2).reshape(B * S, -1)
+    assert rel(out.float().cpu(), ref) < 1e-2
+    assert torch.equal(out[:, (H + Hkv) * D :], qkv[:, (H + Hkv) * D :])  # V untouched
 
 
 def test_flash_attention_large_scores(gpu_device):
