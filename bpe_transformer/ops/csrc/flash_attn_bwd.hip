@@ -115,7 +115,7 @@ __device__ __forceinline__ void softmax_ds(f32x16& sp, f32x16& dp, int hh, float
 }
 
 // DBG (timing diagnostics, numerically wrong; built only with -DBPE_FA_DIAG): bit 1 = no dQ phase,
-// bit 2 = no softmax (P = S), bit 3 = no next-tile global loads.
+// bit 2 = no softmax (P = S), bit 3 = no next-tile global loads, bit 4 = no dQ atomics.
 // ROPE: dK is un-rotated on output (and dQ by the convert kernel); ROPE_IN: Q / K are rotated on load too
 // (false when ops.rope_qk_ rotated them in the QKV activation already, rope mode 2).
 template <int D, bool CAUSAL, bool ROPE, int DBG = 0, bool ROPE_IN = ROPE>
@@ -183,26 +183,23 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     u16x8 qreg[SPT], oreg[SPT];
     float lreg = 0.f, dreg = 0.f;
     auto load_tile = [&](int it) {
+        // every load unconditional (rows past the end clamped to S-1, their values zeroed at the LDS write; the
+        // stats rows loaded by all waves, used by wave 0): straight-line code keeps the wait-count pass's
+        // in-order vmcnt count exact, so write_tile waits for these loads and not for the dQ atomics after them
         const int m0 = m_start + it * 64;
         const __bf16* qb = Q + (long)b * S * ld_q + (long)h * D;
         const __bf16* ob = dO + (long)b * S * ld_do + (long)h * D;
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
-            const int e = tid + NT * i, row = e / CPR, c = e % CPR;
-            const int qq = m0 + row;
-            if (e < 64 * CPR && qq < S) {
-                qreg[i] = *reinterpret_cast<const u16x8*>(qb + (long)qq * ld_q + c * 8);
-                oreg[i] = *reinterpret_cast<const u16x8*>(ob + (long)qq * ld_do + c * 8);
-            } else {
-                qreg[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-                oreg[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-            }
+            const int e = min(tid + NT * i, 64 * CPR - 1), row = e / CPR, c = e % CPR;
+            const long qq = min(m0 + row, S - 1);
+            qreg[i] = *reinterpret_cast<const u16x8*>(qb + qq * ld_q + c * 8);
+            oreg[i] = *reinterpret_cast<const u16x8*>(ob + qq * ld_do + c * 8);
         }
-        if (tid < 64) {
-            const int qq = m0 + tid;
-            const long idx = ((long)b * H + h) * S + qq;
-            lreg = qq < S ? LSE[idx] : INFINITY;
-            dreg = qq < S ? DELTA[idx] : 0.f;
+        {
+            const long idx = ((long)b * H + h) * S + min(m0 + l, S - 1);
+            lreg = LSE[idx];
+            dreg = DELTA[idx];
         }
     };
     auto write_tile = [&](int it, int buf) {
@@ -211,18 +208,21 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
         for (int i = 0; i < SPT; ++i) {
             const int e = tid + NT * i, row = e / CPR, c = e % CPR;
             if (e >= 64 * CPR) break;
-            u16x8 qv = qreg[i];
+            const bool ok = m0 + row < S;
+            u16x8 qv = ok ? qreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            const u16x8 ov = ok ? oreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
             if (ROPE_IN) {
                 const long qq = min(m0 + row, S - 1);
                 qv = rope_u16x8(qv, cosT + qq * (D / 2) + c * 4, sinT + qq * (D / 2) + c * 4, 1.f);
             }
             *reinterpret_cast<u16x8*>(Qs + buf * QT + swz<RB>(row, c)) = qv;
-            *reinterpret_cast<u16x8*>(dOs + buf * QT + swz<RB>(row, c)) = oreg[i];
+            *reinterpret_cast<u16x8*>(dOs + buf * QT + swz<RB>(row, c)) = ov;
         }
         if (tid < 64) {
             // the S / dP accumulators' starting values: -LSE2 / (scale*log2e) and -delta
-            lseS[buf * 64 + tid] = (lreg == INFINITY) ? -INFINITY : -lreg / scale_log2;
-            dltS[buf * 64 + tid] = -dreg;
+            const bool ok = m0 + tid < S;
+            lseS[buf * 64 + tid] = (!ok || lreg == INFINITY) ? -INFINITY : -lreg / scale_log2;
+            dltS[buf * 64 + tid] = ok ? -dreg : 0.f;
         }
     };
 
@@ -329,7 +329,10 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                     acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[u], 0, 0, 0);
                 }
             }
-            if (!(flags & 1)) {
+            // unconditional (no runtime skip flag): a conditional atomic block makes the wait-count pass take
+            // the count of the path WITHOUT the atomics at the join, i.e. vmcnt(1) / vmcnt(0) before the next
+            // tile's LDS writes -- which drains these atomics (~600-3000 cycles) every query tile
+            if (!(DBG & 16)) {
                 const long HD = (long)H * D;
                 const int Spad = (S + 63) & ~63;
                 float* dqp = dQacc + ((long)b * Spad + m0 + qb * 16 + 4 * (l >> 4)) * HD + (long)h * D + (l & 15);
@@ -501,10 +504,7 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
         fa_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(a.o, a.ld_o, a.dout, a.ld_do, a.delta,
                                                                                a.dq_acc, a.B, a.H, a.S, spad);
     }
-    static const int dbg = [] {
-        const char* e = getenv("BPE_FA_DEBUG");  // bit 0: skip the dQ atomics (timing diagnostics only)
-        return e ? atoi(e) : 0;
-    }();
+    constexpr int dbg = 0;
     {
         const int nkb = (a.S + Cfg::KB - 1) / Cfg::KB;
 #ifdef BPE_FA_DIAG
@@ -517,6 +517,7 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
             case 4: bwd_main<D, C, R, 4>(a, s, nkb, dbg); break;
             case 8: bwd_main<D, C, R, 8>(a, s, nkb, dbg); break;
             case 14: bwd_main<D, C, R, 14>(a, s, nkb, dbg); break;
+            case 16: bwd_main<D, C, R, 16>(a, s, nkb, dbg); break;
             default: bwd_main<D, C, R, 0>(a, s, nkb, dbg); break;
         }
 #else
