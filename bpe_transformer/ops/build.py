@@ -62,16 +62,19 @@ def lib_path(variant: str | None = None) -> Path:
 
 
 def build(verbose: bool = False, jobs: int | None = None, force: bool = False, variant: str | None = None,
-          defines: list[str] | None = None) -> Path:
+          defines: list[str] | None = None, src_dir: Path | None = None) -> Path:
     """Build the library; ``variant`` + ``defines`` build an A/B copy (``_bpe_hip_<variant>.so``, own object
-    directory) compiled with extra ``-D`` flags, selected at run time with ``BPE_HIP_VARIANT=<variant>``."""
+    directory) compiled with extra ``-D`` flags, selected at run time with ``BPE_HIP_VARIANT=<variant>``.
+    ``src_dir``: compile another copy of ``csrc`` (e.g. an older revision, ``tools/ab_build.sh``) into the
+    variant, for same-process / same-box A/B runs."""
+    csrc = Path(src_dir) if src_dir else CSRC
     build_dir = BUILD if not variant else BUILD.parent / f"hip_{variant}"
     lib = lib_path(variant)
     build_dir.mkdir(parents=True, exist_ok=True)
-    headers = sorted(CSRC.glob("*.h"))
-    hip_srcs = sorted(CSRC.glob("*.hip"))
+    headers = sorted(csrc.glob("*.h"))
+    hip_srcs = sorted(csrc.glob("*.hip"))
     inc, libdirs, abi = _torch_paths()
-    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", str(CSRC)]
+    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", str(csrc)]
     common += [f"-D{d}" for d in (defines or [])]
     jobs_list = []
     objs = []
@@ -80,12 +83,12 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False, v
         objs.append(obj)
         if force or _needs_build(obj, src, headers):
             jobs_list.append([HIPCC, *common, "-c", str(src), "-o", str(obj)])
-    bind_src = CSRC / "torch_bindings.cpp"
+    bind_src = csrc / "torch_bindings.cpp"
     bind_obj = build_dir / "torch_bindings.o"
     objs.append(bind_obj)
     if force or _needs_build(bind_obj, bind_src, headers):
         cmd = [HIPCC, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
-               "-I", str(CSRC)]
+               "-I", str(csrc)]
         for i in inc:
             cmd += ["-I", i]
         cmd += ["-I", sysconfig.get_paths()["include"], "-c", str(bind_src), "-o", str(bind_obj)]
@@ -110,8 +113,12 @@ def main() -> None:
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--variant", default=None, help="build an A/B copy _bpe_hip_<variant>.so")
     ap.add_argument("-D", dest="defines", action="append", default=[], help="extra preprocessor define")
+    ap.add_argument("--src", default=None, help="csrc directory to compile instead of the in-tree one (--variant)")
     a = ap.parse_args()
-    print(build(verbose=a.verbose, jobs=a.jobs, force=a.force, variant=a.variant, defines=a.defines))
+    if a.src and not a.variant:
+        ap.error("--src needs --variant (never overwrite the in-tree library with other sources)")
+    print(build(verbose=a.verbose, jobs=a.jobs, force=a.force, variant=a.variant, defines=a.defines,
+                src_dir=a.src))
 
 
 if __name__ == "__main__":

@@ -16,7 +16,7 @@
 
 namespace bpe {
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return fast_sigmoid(x); }
 
 __device__ __forceinline__ float gelu_f(float x) {
     const float c = 0.7978845608028654f;  // sqrt(2/pi)

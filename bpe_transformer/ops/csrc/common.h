@@ -25,6 +25,14 @@ __device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float(((unsigned
 // (keeps NaN a NaN, unlike the integer-rounding trick).
 __device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
 
+// sigmoid(x) = 1 / (1 + 2^(-x log2 e)) with the hardware v_exp_f32 / v_rcp_f32 (1 ulp): a plain `1.f / (...)`
+// compiles to the IEEE division sequence (v_div_scale x2, v_rcp, 4 fma, v_div_fmas, v_div_fixup) -- ~10 VALU
+// per element in the SwiGLU kernels, whose outputs are rounded to bf16 anyway.  Saturates to 0 / 1 (exp2 -> inf
+// gives rcp(inf) = 0), NaN stays NaN.
+__device__ __forceinline__ float fast_sigmoid(float x) {
+    return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

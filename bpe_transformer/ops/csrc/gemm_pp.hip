@@ -280,27 +280,42 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
                 const u16x4 p = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
                 *reinterpret_cast<u16x4*>(smem + i * 512 + ((((j >> 3) ^ (i & 15))) << 4) + ((j & 7) << 1)) = p;
             }
-        __syncthreads();
-#pragma unroll 4
-        for (int q = 0; q < 16; ++q) {
-            const int i = q * 16 + (tid >> 5), c = tid & 31;
-            u16x8 v = *reinterpret_cast<const u16x8*>(smem + i * 512 + ((c ^ (i & 15)) << 4));
-            if constexpr (EPI == EPI_SWIGLU_BWD) {
+        if constexpr (EPI == EPI_SWIGLU_BWD) {
+            // every g / u load of this thread's 16 row segments is issued before the barrier (the accumulators
+            // are in LDS now, their registers free): one memory round trip for the tile instead of one per
+            // unrolled group of rows, overlapped with the other waves' staging writes
+            const int c = tid & 31;
+            u16x8 gv[16], uv[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const long ro = (long)(i0 + q * 16 + (tid >> 5)) * ep.ld + j0 + c * 8;
+                gv[q] = *reinterpret_cast<const u16x8*>(ep.gu + ro);
+                uv[q] = *reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int i = q * 16 + (tid >> 5);
+                const u16x8 v = *reinterpret_cast<const u16x8*>(smem + i * 512 + ((c ^ (i & 15)) << 4));
                 const long ro = (long)(i0 + i) * ep.ld + j0 + c * 8;
-                const u16x8 gv = *reinterpret_cast<const u16x8*>(ep.gu + ro);
-                const u16x8 uv = *reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F);
                 u16x8 dg, du;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    const float gg = bf2f(gv[e]), uu = bf2f(uv[e]), d = bf2f(v[e]);
-                    const float sg = 1.f / (1.f + __expf(-gg));
+                    const float gg = bf2f(gv[q][e]), uu = bf2f(uv[q][e]), d = bf2f(v[e]);
+                    const float sg = fast_sigmoid(gg);
                     du[e] = f2bf(d * (gg * sg));
                     dg[e] = f2bf(d * uu * sg * (1.f + gg * (1.f - sg)));
                 }
                 *reinterpret_cast<u16x8*>(ep.dgu + ro) = dg;
                 *reinterpret_cast<u16x8*>(ep.dgu + ro + ep.F) = du;
-                continue;
             }
+            return;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+            const int i = q * 16 + (tid >> 5), c = tid & 31;
+            u16x8 v = *reinterpret_cast<const u16x8*>(smem + i * 512 + ((c ^ (i & 15)) << 4));
             __bf16* cp = C + (long)(i0 + i) * ldc + j0 + c * 8;
             if (beta != 0.f) {
                 const u16x8 o = *reinterpret_cast<const u16x8*>(cp);
