@@ -385,6 +385,19 @@ void cast_fp8(const at::Tensor& x, const at::Tensor& scale, at::Tensor out, at::
                     reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
 }
 
+// W [R][C] bf16 (row stride a multiple of 8) -> W^T [C][R] contiguous
+at::Tensor transpose_bf16(const at::Tensor& w) {
+    check_cuda(w, "w");
+    TORCH_CHECK(w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.stride(1) == 1 && w.stride(0) % 8 == 0,
+                "transpose_bf16: bf16 [R, C] with unit column stride and 16-byte row alignment required");
+    const int64_t R = w.size(0), C = w.size(1);
+    TORCH_CHECK(R % 64 == 0 && C % 64 == 0, "transpose_bf16: R and C must be multiples of 64");
+    DevGuard g(w.device());
+    auto out = at::empty({C, R}, w.options());
+    launch_transpose_bf16(w.data_ptr(), w.stride(0), out.data_ptr(), R, (int)R, (int)C, cur_stream());
+    return out;
+}
+
 // W [N][K] bf16 -> e4m3 copies w8 [N][K] and w8t [K][N] in one pass (amax folded into amax_bits)
 void cast_fp8_t(const at::Tensor& w, const at::Tensor& scale, at::Tensor w8, at::Tensor w8t, at::Tensor amax_bits) {
     check_cuda(w, "w");
@@ -734,6 +747,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
+    m.def("transpose_bf16(Tensor w) -> Tensor");
     m.def("cast_fp8_t(Tensor w, Tensor scale, Tensor(a!) w8, Tensor(b!) w8t, Tensor(c!) amax_bits) -> ()");
     m.def("update_scales(Tensor(a!) amax_bits, Tensor(b!) hist, Tensor(c!) scale, Tensor(d!) inv_scale, int pos, "
           "float margin, int fmt=0) -> ()");
@@ -766,6 +780,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("gemm_pp", &gemm_pp);
     m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
     m.impl("cast_fp8", &cast_fp8);
+    m.impl("transpose_bf16", &transpose_bf16);
     m.impl("cast_fp8_t", &cast_fp8_t);
     m.impl("update_scales", &update_scales);
     m.impl("softmax_fwd", &softmax_fwd);

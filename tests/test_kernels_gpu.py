@@ -299,6 +299,18 @@ def test_gemm_layouts(gpu_device, a_k, b_k, splits, tile):
     assert rel(C.cpu(), ref.cpu()) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(64, 64), (2304, 768), (768, 4096), (192, 320)])
+def test_transpose_bf16(gpu_device, shape):
+    """LDS-tiled transpose (dX in the TN layout): exact, including a row-strided (sliced) input."""
+    torch.manual_seed(3)
+    R, C = shape
+    big = torch.randn(R, C + 64, device=gpu_device, dtype=torch.bfloat16)
+    for w in (big[:, :C].contiguous(), big[:, 64:]):
+        t = torch.ops.bpe_hip.transpose_bf16(w)
+        assert t.shape == (C, R) and t.is_contiguous()
+        assert torch.equal(t.cpu(), w.t().cpu())
+
+
 def test_gemm_swiglu_bwd(gpu_device):
     """dY @ W2 with the SwiGLU backward in the epilogue vs the fp32 oracle of the same two steps."""
     torch.manual_seed(2)
