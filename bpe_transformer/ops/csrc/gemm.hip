@@ -279,14 +279,63 @@ struct Acc<16> {
 // destination; without it the compiler's wait-count pass drains the DMA (vmcnt(0)) before the first fragment read.
 // PRIO: all fragments first, then the MFMA cluster between s_setprio(1)/(0) (keeps hipcc from moving MFMAs
 // across the barriers; guide T5).
-template <int MF, bool PRIO>
+// DSPLIT (MF = 32, no PRIO): the 4 LDS-DMA instructions per wave and step spread over the step instead of one
+// burst at its start -- 1: the A tile's pair before the first 16-deep k-step, the B tile's between the two;
+// 2: one instruction after every quarter of the MFMAs.
+__device__ __forceinline__ void dma_one(const __bf16* tile0, long off, char* lds, int q, int w) {
+    __builtin_amdgcn_global_load_lds((gbl_void*)(tile0 + off), (lds_void*)(lds + (q * NT + w * 64) * 16), 16, 0, 0);
+}
+
+template <int MF, bool PRIO, int DSPLIT = 0>
 __device__ __forceinline__ void kstep(char* __restrict__ cur, char* __restrict__ nxt, const __bf16* an,
                                       const long (&oa)[2], const __bf16* bn, const long (&ob)[2], int wr, int wc,
                                       int w, int l, Acc<MF>& acc) {
+    char* Bs = cur + TILE_BYTES;
+    if constexpr (DSPLIT == 2 && MF == 32 && !PRIO) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 fb0 = frag32(Bs, wc, ks, l), fb1 = frag32(Bs, wc + 32, ks, l);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                if ((a & 1) == 0) {  // quarters: A chunk 0, A chunk 1, B chunk 0, B chunk 1
+                    const int qi = 2 * ks + (a >> 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (qi < 2)
+                        dma_one(an, oa[qi], nxt, qi, w);
+                    else
+                        dma_one(bn, ob[qi - 2], nxt + TILE_BYTES, qi - 2, w);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                bf16x8 fa = frag32(cur, wr + 32 * a, ks, l);
+                acc.v[a][0] = mfma(fa, fb0, acc.v[a][0]);
+                acc.v[a][1] = mfma(fa, fb1, acc.v[a][1]);
+            }
+        }
+        return;
+    }
+    if constexpr (DSPLIT == 1 && MF == 32 && !PRIO) {
+        dma_tile(an, oa, nxt, w);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 fb0 = frag32(Bs, wc, ks, l), fb1 = frag32(Bs, wc + 32, ks, l);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                bf16x8 fa = frag32(cur, wr + 32 * a, ks, l);
+                acc.v[a][0] = mfma(fa, fb0, acc.v[a][0]);
+                acc.v[a][1] = mfma(fa, fb1, acc.v[a][1]);
+            }
+            if (ks == 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                dma_tile(bn, ob, nxt + TILE_BYTES, w);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        return;
+    }
     dma_tile(an, oa, nxt, w);
     dma_tile(bn, ob, nxt + TILE_BYTES, w);
     __builtin_amdgcn_sched_barrier(0);  // issue the DMA first: it needs all the MFMA time to land
-    char* Bs = cur + TILE_BYTES;
     if constexpr (MF == 32) {
         if constexpr (PRIO) {
             bf16x8 fa[2][4], fb[2][2];
@@ -363,7 +412,7 @@ __device__ __forceinline__ void for_each_acc(const Acc<16>& acc, int l, F&& f) {
             for (int r = 0; r < 4; ++r) f(a * 16 + 4 * (l >> 4) + r, b * 16 + (l & 15), acc.v[a][b][r]);
 }
 
-template <int MF, bool PRIO>
+template <int MF, bool PRIO, int DSPLIT = 0>
 __global__ void __launch_bounds__(NT, 1)
 gemm256_tn_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
                   float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int Mo, int No, int R,
@@ -413,7 +462,7 @@ gemm256_tn_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restri
         // every step issues exactly one stage so the counted wait below stays exact; past the end it re-loads
         // the last stage into a buffer nobody reads again
         const int rn = min(rbeg + (kt + NSTAGE - 1) * BK, rlast);
-        kstep<MF, PRIO>(cur, nxt, A + (long)rn * lda, oa, B + (long)rn * ldb, ob, wr, wc, w, l, acc);
+        kstep<MF, PRIO, DSPLIT>(cur, nxt, A + (long)rn * lda, oa, B + (long)rn * ldb, ob, wr, wc, w, l, acc);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage kt+1 landed; kt+2, kt+3 stay in flight
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -448,27 +497,29 @@ bool gemm_shape_ok(int Mo, int No, int R, int splits, int tile) {
     return Mo % BM == 0 && No % BN == 0 && splits >= 1 && R % BK == 0 && R / BK >= splits;
 }
 
-template <int MF, bool PRIO>
+template <int MF, bool PRIO, int DSPLIT = 0>
 static void launch_g256_v(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                           float beta, int Mo, int No, int R, int splits, hipStream_t s) {
     static bool attr = false;  // > 64 KiB dynamic LDS must be opted into once per instantiation
+    auto* k = &g256::gemm256_tn_kernel<MF, PRIO, DSPLIT>;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)g256::gemm256_tn_kernel<MF, PRIO>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, g256::LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, g256::LDS_BYTES);
         attr = true;
     }
     const int grid = (Mo / 256) * (No / 256) * splits;
-    g256::gemm256_tn_kernel<MF, PRIO><<<grid, g256::NT, g256::LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, Mo,
-                                                                                No, R, splits);
+    k<<<grid, g256::NT, g256::LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits);
 }
 
-// variant (BPE_G256_VARIANT, read once): bit 0 = 16x16x32 MFMA, bit 1 = setprio'd MFMA cluster
+// variant (BPE_G256_VARIANT, read once): bit 0 = 16x16x32 MFMA, bit 1 = setprio'd MFMA cluster, bit 2 / bit 3 =
+// the DMA split over the step in 2 / 4 places (32x32x16, overrides bits 0-1)
 static void launch_g256(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                         float beta, int Mo, int No, int R, int splits, hipStream_t s) {
-    static int variant = [] {
+    static int variant = [] {  // default 4: +3-4 % over the one-burst DMA (profiles/bench/ab_dw_dma_split.log)
         const char* e = getenv("BPE_G256_VARIANT");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 4;
     }();
+    if (variant & 8) return launch_g256_v<32, false, 2>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s);
+    if (variant & 4) return launch_g256_v<32, false, 1>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s);
     switch (variant & 3) {
         case 0: launch_g256_v<32, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;
         case 1: launch_g256_v<16, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;

@@ -147,7 +147,7 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const Frags& f,
 // target (the __restrict__ parameters let the wait-count pass see that the fragment reads do not alias the
 // in-flight DMA; without it hipcc drains the DMA before the first read).
 // DIAG (timing diagnostics, numerically wrong): 1 = no DMA in the loop, 2 = fragment reads only in phase 0,
-// 3 = no MFMA, 4 = no stagger between the groups
+// 3 = no MFMA, 4 = no stagger between the groups, 5 = DMA issued but never waited for (issue cost only)
 template <bool AK, bool BKM, int DIAG>
 __device__ __forceinline__ void ktile(char* __restrict__ cur, char* __restrict__ nxt, bool dma, const __bf16* an,
                                       const __bf16* bn, const int (&oa)[4], const int (&ob)[4], int g, int wl,
@@ -179,7 +179,10 @@ __device__ __forceinline__ void ktile(char* __restrict__ cur, char* __restrict__
     bar();
     // phase 3: (m1, n0); retire this wave's DMA of the next K-tile before the barrier
     if (DIAG != 2) load_b<AK, BKM>(f, Bc, wl, 0, l);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (DIAG == 5)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // DMA issued but never waited for
+    else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     bar();
     if (DIAG != 3) mma_quadrant(acc, f, 1, 0);
     bar();
@@ -187,6 +190,106 @@ __device__ __forceinline__ void ktile(char* __restrict__ cur, char* __restrict__
 #pragma unroll
         for (int ib = 0; ib < 4; ++ib) acc[ib][0][0] += (float)f.a[ib][0][0] + (float)f.b[ib & 1][1][1];
     }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Spread DMA schedule (both operands K-major, i.e. the forward GEMM).  A diagnostic build showed where the
+// burst schedule above loses: issuing the next K-tile's 8 LDS-DMA instructions per wave in phases 0-1 only
+// (4 per load section, each ~100-185 cycles to issue beside the fragment reads) makes those load sections
+// longer than the partner wave's 256-cycle MFMA section; with the DMA removed (DIAG 1) the same loop runs
+// 1.45-1.55x faster, and issuing it without ever waiting for it (DIAG 5) is no faster than waiting for it
+// (profiles/bench/gpp_diag_b128.log) -- issue placement, not latency.  Here every load section issues 2
+// pieces, in the order the next K-tile's phases read them:
+//   phase 0: A rows [128g, +64)   (read by this group in phase 0 of kt+1)
+//   phase 1: half g of B rows {64w' + [0, 32)}   (both groups, phase 0 / 3)
+//   phase 2: half g of B rows {64w' + [32, 64)}  (both groups, phase 1)
+//   phase 3: A rows [128g + 64, +64)  (this group, phase 2)
+// and then waits vmcnt(4): the two newest issues stay in flight, the one issued three load sections ago is
+// retired before the barrier that precedes its first read (by either group: group 1 reads a piece one barrier
+// after group 0, never before the issuing wave's wait).  WAR: a region of the other buffer is refilled at
+// least one barrier after its last read of K-tile kt-1 (A rows: phases 0 / 2, B halves: phases 3 / 1).
+// Last K-tile (no issue): vmcnt(2) in phase 0 (B rows [32, 64) of this tile), vmcnt(0) afterwards.
+struct SpreadOff {
+    int a0[2], a1[2], b0[2], b1[2];  // source offsets (elements from the K-tile origin) of this thread's pieces
+    int la0, la1, lb0, lb1;          // wave-uniform LDS chunk index of each piece pair (piece j at + 64 j)
+};
+
+__device__ __forceinline__ SpreadOff spread_offsets(int g, int wl, int l, int lda, int ldb) {
+    SpreadOff o;
+    o.la0 = 1024 * g + 128 * wl;
+    o.la1 = o.la0 + 512;
+    o.lb0 = 512 * (2 * g + (wl >> 1)) + 128 * (wl & 1);
+    o.lb1 = o.lb0 + 256;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        o.a0[j] = src_off<true>(o.la0 + 64 * j + l, lda);
+        o.a1[j] = src_off<true>(o.la1 + 64 * j + l, lda);
+        o.b0[j] = src_off<true>(o.lb0 + 64 * j + l, ldb);
+        o.b1[j] = src_off<true>(o.lb1 + 64 * j + l, ldb);
+    }
+    return o;
+}
+
+__device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2], char* img, int lbase) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_global_load_lds((gbl_void*)(tile0 + off[j]), (lds_void*)(img + (lbase + 64 * j) * 16), 16,
+                                         0, 0);
+}
+
+template <int DIAG>
+__device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
+                                             const __bf16* an, const __bf16* bn, const SpreadOff& so, int g, int wl,
+                                             int l, f32x4 (&acc)[8][4]) {
+    Frags f;
+    char* Ac = cur;
+    char* Bc = cur + OPB;
+    if (DIAG == 1) dma = false;
+    // phase 0: (m0, n0)
+    load_a<true, true>(f, Ac, g, 0, l);
+    load_b<true, true>(f, Bc, wl, 0, l);
+    if (dma) {
+        dma_pair(an, so.a0, nxt, so.la0);
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    }
+    bar();
+    mma_quadrant(acc, f, 0, 0);
+    bar();
+    // phase 1: (m0, n1)
+    load_b<true, true>(f, Bc, wl, 1, l);
+    if (dma) {
+        dma_pair(bn, so.b0, nxt + OPB, so.lb0);
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    bar();
+    mma_quadrant(acc, f, 0, 1);
+    bar();
+    // phase 2: (m1, n1)
+    load_a<true, true>(f, Ac, g, 1, l);
+    if (dma) {
+        dma_pair(bn, so.b1, nxt + OPB, so.lb1);
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    bar();
+    mma_quadrant(acc, f, 1, 1);
+    bar();
+    // phase 3: (m1, n0)
+    load_b<true, true>(f, Bc, wl, 0, l);
+    if (dma) {
+        dma_pair(an, so.a1, nxt, so.la1);
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    bar();
+    mma_quadrant(acc, f, 1, 0);
+    bar();
 }
 
 // Fused epilogues of the one-tile-per-workgroup kernel.  EPI_SWIGLU_BWD: the GEMM result is da = dY W2 (the
@@ -201,7 +304,7 @@ struct Epi {
     int F;
 };
 
-template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE>
+template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, bool SPREAD = false>
 __global__ void __launch_bounds__(NT, 1)
 gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
                float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int M, int N, int R,
@@ -222,36 +325,59 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     const int kb = (int)((long)split * nkt / splits);
     const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
 
-    int oa[4], ob[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int e = g * 1024 + (wl * 4 + j) * 64 + l;
-        oa[j] = src_off<AK>(e, (int)lda);
-        ob[j] = src_off<BKM>(e, (int)ldb);
-    }
-
+    constexpr bool SPR = SPREAD && AK && BKM;
     f32x4 acc[8][4];
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // prologue: K-tile 0, both halves (each group its own), then retire + barrier
-    {
-        const long k0 = (long)kb * BK;
-        dma_half(tile_ptr<AK>(A, lda, i0, k0), oa, smem, g, wl);
-        dma_half(tile_ptr<BKM>(B, ldb, j0, k0), ob, smem + OPB, g, wl);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bar();
-    }
-    if (g == 1 && DIAG != 4) bar();  // the stagger: group 1 runs one barrier interval behind group 0
-    for (int kt = 0; kt < nk; ++kt) {
-        char* cur = smem + (kt & 1) * STAGE;
-        char* nxt = smem + ((kt + 1) & 1) * STAGE;
-        const bool dma = kt + 1 < nk;
-        const long k1 = (long)(kb + kt + 1) * BK;
-        ktile<AK, BKM, DIAG>(cur, nxt, dma, tile_ptr<AK>(A, lda, i0, k1), tile_ptr<BKM>(B, ldb, j0, k1), oa, ob, g, wl, l,
-                       acc);
+    if constexpr (SPR) {
+        const SpreadOff so = spread_offsets(g, wl, l, (int)lda, (int)ldb);
+        {  // prologue: all of K-tile 0 (this wave's 8 pieces of the schedule), retired before the first read
+            const long k0 = (long)kb * BK;
+            const __bf16* a0 = tile_ptr<true>(A, lda, i0, k0);
+            const __bf16* b0 = tile_ptr<true>(B, ldb, j0, k0);
+            dma_pair(a0, so.a0, smem, so.la0);
+            dma_pair(b0, so.b0, smem + OPB, so.lb0);
+            dma_pair(b0, so.b1, smem + OPB, so.lb1);
+            dma_pair(a0, so.a1, smem, so.la1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();
+        }
+        if (g == 1) bar();  // the stagger
+        for (int kt = 0; kt < nk; ++kt) {
+            char* cur = smem + (kt & 1) * STAGE;
+            char* nxt = smem + ((kt + 1) & 1) * STAGE;
+            const long k1 = (long)(kb + kt + 1) * BK;
+            ktile_spread<DIAG>(cur, nxt, kt + 1 < nk, tile_ptr<true>(A, lda, i0, k1), tile_ptr<true>(B, ldb, j0, k1),
+                               so, g, wl, l, acc);
+        }
+    } else {
+        int oa[4], ob[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = g * 1024 + (wl * 4 + j) * 64 + l;
+            oa[j] = src_off<AK>(e, (int)lda);
+            ob[j] = src_off<BKM>(e, (int)ldb);
+        }
+        // prologue: K-tile 0, both halves (each group its own), then retire + barrier
+        {
+            const long k0 = (long)kb * BK;
+            dma_half(tile_ptr<AK>(A, lda, i0, k0), oa, smem, g, wl);
+            dma_half(tile_ptr<BKM>(B, ldb, j0, k0), ob, smem + OPB, g, wl);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();
+        }
+        if (g == 1 && DIAG != 4) bar();  // the stagger: group 1 runs one barrier interval behind group 0
+        for (int kt = 0; kt < nk; ++kt) {
+            char* cur = smem + (kt & 1) * STAGE;
+            char* nxt = smem + ((kt + 1) & 1) * STAGE;
+            const bool dma = kt + 1 < nk;
+            const long k1 = (long)(kb + kt + 1) * BK;
+            ktile<AK, BKM, DIAG>(cur, nxt, dma, tile_ptr<AK>(A, lda, i0, k1), tile_ptr<BKM>(B, ldb, j0, k1), oa, ob, g,
+                                 wl, l, acc);
+        }
     }
     if (g == 0 && DIAG != 4) bar();
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -559,17 +685,36 @@ bool gemm_pp_shape_ok(int M, int N, int R, int splits) {
     return M % BT == 0 && N % BT == 0 && R % BK == 0 && splits >= 1 && R / BK >= splits;
 }
 
-template <bool AK, bool BKM, bool SLAB, int DIAG>
-static void launch_pp1(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
-                      float beta, int M, int N, int R, int splits, hipStream_t s) {
+// BPE_GPP_SPREAD (read once, default 1): the spread DMA schedule where it applies (both operands K-major)
+static bool spread_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("BPE_GPP_SPREAD");
+        return !e || e[0] != '0';
+    }();
+    return on;
+}
+
+template <bool AK, bool BKM, bool SLAB, int DIAG, bool SPREAD>
+static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
+                        float beta, int M, int N, int R, int splits, hipStream_t s) {
     static bool attr = false;  // > 64 KiB dynamic LDS must be opted into once per instantiation
+    auto* k = &gemm_pp_kernel<AK, BKM, SLAB, DIAG, EPI_NONE, SPREAD>;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<AK, BKM, SLAB, DIAG>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr = true;
     }
     const int grid = (M / BT) * (N / BT) * splits;
-    gemm_pp_kernel<AK, BKM, SLAB, DIAG><<<grid, NT, LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits);
+    k<<<grid, NT, LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, Epi{});
+}
+
+template <bool AK, bool BKM, bool SLAB, int DIAG>
+static void launch_pp1(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
+                      float beta, int M, int N, int R, int splits, hipStream_t s) {
+    if constexpr (AK && BKM) {
+        if (spread_enabled())
+            return launch_pp1s<AK, BKM, SLAB, DIAG, true>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
+    }
+    launch_pp1s<AK, BKM, SLAB, DIAG, false>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
 }
 
 template <bool AK, bool BKM, bool SLAB>
@@ -614,6 +759,7 @@ static void launch_pp(const __bf16* a, long lda, const __bf16* b, long ldb, floa
         case 2: launch_pp1<AK, BKM, SLAB, 2>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
         case 3: launch_pp1<AK, BKM, SLAB, 3>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
         case 4: launch_pp1<AK, BKM, SLAB, 4>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
+        case 5: launch_pp1<AK, BKM, SLAB, 5>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
 #endif
         default: launch_pp1<AK, BKM, SLAB, 0>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
     }
