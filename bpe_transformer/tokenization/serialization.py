@@ -3,9 +3,10 @@
 Byte-compatible with the reference (``bpe_trainer.py:447-472``,
 ``bpe_tokenizer.py:292-337``): ``vocab.pkl`` is a pickled
 ``dict[int, bytes]`` and ``merges.pkl`` a pickled ``list[tuple[bytes, bytes]]``
-(protocol 4).  Loading goes through a RESTRICTED unpickler that refuses every
-global/class lookup, so a tampered file cannot execute code -- these two
-artifacts only ever contain builtin containers, ints and bytes.
+(protocol 4).  Loading never runs an unpickler: :mod:`.safe_pickle` interprets
+the opcode stream itself and accepts only builtin data (ints, bytes, lists,
+tuples, dicts), so a tampered file cannot execute code -- these two artifacts
+only ever contain builtin containers, ints and bytes.
 
 Also reads/writes the GPT-2 text formats (``vocab.json`` + ``merges.txt`` with
 the byte-to-unicode remapping).
@@ -13,23 +14,19 @@ the byte-to-unicode remapping).
 
 from __future__ import annotations
 
-import io
 import json
 import pickle
 from functools import lru_cache
 from pathlib import Path
 
+from . import safe_pickle
+
 PICKLE_PROTOCOL = 4
 
 
-class _NoGlobalsUnpickler(pickle.Unpickler):
-    def find_class(self, module, name):  # noqa: D401
-        raise pickle.UnpicklingError(f"refusing to load global {module}.{name} from a tokenizer artifact")
-
-
 def safe_pickle_load(path: str | Path):
-    with open(path, "rb") as f:
-        return _NoGlobalsUnpickler(io.BytesIO(f.read())).load()
+    """Builtin data from a pickle file, without unpickling (:func:`.safe_pickle.load`)."""
+    return safe_pickle.load(path)
 
 
 def save_vocab(vocab: dict[int, bytes], path: str | Path) -> None:

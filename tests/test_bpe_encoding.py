@@ -146,8 +146,45 @@ def test_restricted_unpickler_refuses_code(tmp_path):
     p = tmp_path / "vocab.pkl"
     with open(p, "wb") as f:
         pickle.dump({0: Evil()}, f)
-    with pytest.raises(pickle.UnpicklingError):
+    from bpe_transformer.tokenization.safe_pickle import UnsafePickleError
+
+    with pytest.raises(UnsafePickleError):
         BPETokenizer.load_vocab(p)
+
+
+def test_safe_pickle_reads_what_pickle_writes(tmp_path):
+    """The opcode-level reader decodes builtin data in protocols 3-5 (the reference's artifacts are protocol 4).
+    Protocol 2 has no bytes opcode -- it pickles bytes as a call to ``_codecs.encode`` -- and is refused."""
+    from bpe_transformer.tokenization import safe_pickle
+
+    obj = {0: b"a", 300: b"\xff" * 300, 70000: b"", 2**40: [(b"x", b"y"), (b"x", b"y")]}
+    for proto in (3, 4, 5):
+        data = pickle.dumps(obj, protocol=proto)
+        assert safe_pickle.loads(data) == obj
+    with pytest.raises(safe_pickle.UnsafePickleError):
+        safe_pickle.loads(pickle.dumps(obj, protocol=2))
+    shared = [b"ab", b"cd"]
+    merges = [(shared[0], shared[1]), (shared[1], shared[0])]  # memoised bytes referenced twice
+    assert safe_pickle.loads(pickle.dumps(merges, protocol=4)) == merges
+
+
+SAMPLE = FIXTURES / "sample_tokenizer"  # the reference's notebooks/sample_data/bpe_tokenizer/{vocab,merges}.pkl
+
+
+def test_reference_sample_tokenizer_parity():
+    """The reference's shipped TinyStories tokenizer (10 000 vocab, 9 743 merges) loads through the
+    non-executing reader and reproduces the reference notebook's outputs
+    (``notebooks/3_bpe_tokenization_encode_decode.ipynb`` cells 11, 16, 18)."""
+    t = BPETokenizer.from_files(SAMPLE / "vocab.pkl", SAMPLE / "merges.pkl")
+    assert len(t.vocab) == 10000 and len(t.merges) == 9743
+    text = "Hello, I am encoding my text. How are you?"
+    ids = t.encode(text)
+    assert ids == [1183, 44, 338, 740, 835, 1262, 5686, 622, 799, 983, 46, 2687, 483, 349, 63]
+    assert t.decode(ids) == text
+    with open(FIXTURES / "tinystories_sample.txt", encoding="utf-8") as f:
+        stream = list(t.encode_iterable(f))
+    assert len(stream) == 927
+    assert stream[-10:] == [10, 60, 124, 353, 111, 791, 3279, 124, 62, 10]
 
 
 def test_trained_tokenizer_end_to_end(tmp_path):
