@@ -87,13 +87,37 @@ __device__ __forceinline__ void dma_half(const __bf16* tile0, const int (&off)[4
                                          (lds_void*)(img + (g * 1024 + (wl * 4 + j) * 64) * 16), 16, 0, 0);
 }
 
+// MN-major image of the spread schedule: eight [64 k][32 col] sub-images of 4 KiB (64-byte rows), so that
+// every set of columns the phases read (a 64-column A block, the 32-column halves of the B blocks) is a whole
+// number of 1-KiB DMA pieces.  The 32-byte halves of a row are swapped on odd 8-row groups, which keeps the
+// ds_read_b64_tr_b16 reads conflict-free (the 8 rows a 32-lane group reads, r0..r0+3 and r0+8..r0+11, land
+// on 8 distinct 32-byte bank groups).
+__device__ __forceinline__ int sub_off(int r, int c) {
+    return (c >> 5) * 4096 + r * 64 + ((((c >> 4) & 1) ^ ((r >> 3) & 1)) << 5) + ((c & 15) << 1);
+}
+
+// Source offset (elements, from the tile origin) of 16-byte chunk e (0..2047) of a sub-image MN-major image:
+// sub-image e >> 8, piece (16 k-rows) ((e >> 6) & 3), lane e & 63 -> k-row 16 piece + lane / 4, physical
+// 16-byte chunk lane & 3 of the 64-byte row, which holds logical chunk (lane & 3) ^ (2 * bit 3 of the row).
+__device__ __forceinline__ int src_off_sub(int e, int ld) {
+    const int s = e >> 8, q = (e >> 6) & 3, ln = e & 63;
+    const int row = 16 * q + (ln >> 2);
+    const int ql = (ln & 3) ^ (((row >> 3) & 1) << 1);
+    return row * ld + 32 * s + 8 * ql;
+}
+
 // MFMA operand fragment of 16-row/col block tb, k-step ks: lane l gets X[t = 16 tb + (l & 15)][k = 32 ks + 8 (l >> 4) + j].
-template <bool KM>
+// SUB: MN-major operands use the sub-image layout above (spread schedule) instead of [64][256] 512-byte rows.
+template <bool KM, bool SUB = false>
 __device__ __forceinline__ bf16x8 frag(char* img, int tb, int ks, int l) {
     if constexpr (KM) {
         const int row = tb * 16 + (l & 15);
         const int ch = (4 * ks + (l >> 4)) ^ fk(l & 15);
         return fa::lds_row16(img, row * 128 + (ch << 4));
+    } else if constexpr (SUB) {
+        const int r = 32 * ks + 8 * (l >> 4) + ((l & 15) >> 2);
+        const int c = tb * 16 + 4 * (l & 3);
+        return fa::lds_tr_pair(img, sub_off(r, c), sub_off(r + 4, c));
     } else {
         const int r = 32 * ks + 8 * (l >> 4) + ((l & 15) >> 2);
         const int c = tb * 16 + 4 * (l & 3);
@@ -118,19 +142,19 @@ __device__ __forceinline__ void bar() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, bool SUB = false>
 __device__ __forceinline__ void load_a(Frags& f, char* img, int g, int m, int l) {
 #pragma unroll
     for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) f.a[ib][ks] = frag<AK>(img, 8 * g + 4 * m + ib, ks, l);
+        for (int ks = 0; ks < 2; ++ks) f.a[ib][ks] = frag<AK, SUB>(img, 8 * g + 4 * m + ib, ks, l);
 }
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, bool SUB = false>
 __device__ __forceinline__ void load_b(Frags& f, char* img, int wl, int n, int l) {
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) f.b[jb][ks] = frag<BKM>(img, 4 * wl + 2 * n + jb, ks, l);
+        for (int ks = 0; ks < 2; ++ks) f.b[jb][ks] = frag<BKM, SUB>(img, 4 * wl + 2 * n + jb, ks, l);
 }
 
 __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const Frags& f, int m, int n) {
@@ -214,6 +238,16 @@ struct SpreadOff {
     int la0, la1, lb0, lb1;          // wave-uniform LDS chunk index of each piece pair (piece j at + 64 j)
 };
 
+// Chunk e of either image kind: K-major [256][64] (A rows / B rows = output index) or the MN-major sub-image
+// layout.  The piece sets line up in both: chunks [1024 g + 512 m, +512) are output rows / columns
+// [128 g + 64 m, +64) and chunks {512 w' + 256 h + [0, 256)} the 32-wide half h of block w'.
+template <bool KM>
+__device__ __forceinline__ int spread_src(int e, int ld) {
+    if constexpr (KM) return src_off<true>(e, ld);
+    else return src_off_sub(e, ld);
+}
+
+template <bool AK, bool BKM>
 __device__ __forceinline__ SpreadOff spread_offsets(int g, int wl, int l, int lda, int ldb) {
     SpreadOff o;
     o.la0 = 1024 * g + 128 * wl;
@@ -222,10 +256,10 @@ __device__ __forceinline__ SpreadOff spread_offsets(int g, int wl, int l, int ld
     o.lb1 = o.lb0 + 256;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        o.a0[j] = src_off<true>(o.la0 + 64 * j + l, lda);
-        o.a1[j] = src_off<true>(o.la1 + 64 * j + l, lda);
-        o.b0[j] = src_off<true>(o.lb0 + 64 * j + l, ldb);
-        o.b1[j] = src_off<true>(o.lb1 + 64 * j + l, ldb);
+        o.a0[j] = spread_src<AK>(o.la0 + 64 * j + l, lda);
+        o.a1[j] = spread_src<AK>(o.la1 + 64 * j + l, lda);
+        o.b0[j] = spread_src<BKM>(o.lb0 + 64 * j + l, ldb);
+        o.b1[j] = spread_src<BKM>(o.lb1 + 64 * j + l, ldb);
     }
     return o;
 }
@@ -237,7 +271,7 @@ __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2
                                          0, 0);
 }
 
-template <int DIAG>
+template <bool AK, bool BKM, int DIAG>
 __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
                                              const __bf16* an, const __bf16* bn, const SpreadOff& so, int g, int wl,
                                              int l, f32x4 (&acc)[8][4]) {
@@ -246,8 +280,8 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     char* Bc = cur + OPB;
     if (DIAG == 1) dma = false;
     // phase 0: (m0, n0)
-    load_a<true, true>(f, Ac, g, 0, l);
-    load_b<true, true>(f, Bc, wl, 0, l);
+    load_a<AK, BKM, true>(f, Ac, g, 0, l);
+    load_b<AK, BKM, true>(f, Bc, wl, 0, l);
     if (dma) {
         dma_pair(an, so.a0, nxt, so.la0);
         asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
@@ -258,7 +292,7 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     mma_quadrant(acc, f, 0, 0);
     bar();
     // phase 1: (m0, n1)
-    load_b<true, true>(f, Bc, wl, 1, l);
+    load_b<AK, BKM, true>(f, Bc, wl, 1, l);
     if (dma) {
         dma_pair(bn, so.b0, nxt + OPB, so.lb0);
         asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
@@ -269,7 +303,7 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     mma_quadrant(acc, f, 0, 1);
     bar();
     // phase 2: (m1, n1)
-    load_a<true, true>(f, Ac, g, 1, l);
+    load_a<AK, BKM, true>(f, Ac, g, 1, l);
     if (dma) {
         dma_pair(bn, so.b1, nxt + OPB, so.lb1);
         asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
@@ -280,7 +314,7 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     mma_quadrant(acc, f, 1, 1);
     bar();
     // phase 3: (m1, n0)
-    load_b<true, true>(f, Bc, wl, 0, l);
+    load_b<AK, BKM, true>(f, Bc, wl, 0, l);
     if (dma) {
         dma_pair(an, so.a1, nxt, so.la1);
         asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
@@ -325,7 +359,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     const int kb = (int)((long)split * nkt / splits);
     const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
 
-    constexpr bool SPR = SPREAD && AK && BKM;
+    constexpr bool SPR = SPREAD;
     f32x4 acc[8][4];
 #pragma unroll
     for (int a = 0; a < 8; ++a)
@@ -333,11 +367,11 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
         for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if constexpr (SPR) {
-        const SpreadOff so = spread_offsets(g, wl, l, (int)lda, (int)ldb);
+        const SpreadOff so = spread_offsets<AK, BKM>(g, wl, l, (int)lda, (int)ldb);
         {  // prologue: all of K-tile 0 (this wave's 8 pieces of the schedule), retired before the first read
             const long k0 = (long)kb * BK;
-            const __bf16* a0 = tile_ptr<true>(A, lda, i0, k0);
-            const __bf16* b0 = tile_ptr<true>(B, ldb, j0, k0);
+            const __bf16* a0 = tile_ptr<AK>(A, lda, i0, k0);
+            const __bf16* b0 = tile_ptr<BKM>(B, ldb, j0, k0);
             dma_pair(a0, so.a0, smem, so.la0);
             dma_pair(b0, so.b0, smem + OPB, so.lb0);
             dma_pair(b0, so.b1, smem + OPB, so.lb1);
@@ -350,8 +384,8 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
             char* cur = smem + (kt & 1) * STAGE;
             char* nxt = smem + ((kt + 1) & 1) * STAGE;
             const long k1 = (long)(kb + kt + 1) * BK;
-            ktile_spread<DIAG>(cur, nxt, kt + 1 < nk, tile_ptr<true>(A, lda, i0, k1), tile_ptr<true>(B, ldb, j0, k1),
-                               so, g, wl, l, acc);
+            ktile_spread<AK, BKM, DIAG>(cur, nxt, kt + 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
+                                        tile_ptr<BKM>(B, ldb, j0, k1), so, g, wl, l, acc);
         }
     } else {
         int oa[4], ob[4];
@@ -666,11 +700,21 @@ gemm_pp_pers_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __rest
 
 using namespace bpe::gpp;
 
+// BPE_GPP_SPREAD (read once, default 1): the spread DMA schedule (0: the burst schedule of ktile)
+static bool spread_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("BPE_GPP_SPREAD");
+        return !e || e[0] != '0';
+    }();
+    return on;
+}
+
 // dgu = swiglu_bwd(dY . W2, gu): A = dY [M][R] (K-major), B = W2 [R][F] (MN-major)
 void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,
                                long ldg, int M, int F, int R, hipStream_t s) {
     static bool attr = false;
-    auto* k = &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD>;
+    auto* k = spread_enabled() ? &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, true>
+                               : &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, false>;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr = true;
@@ -685,14 +729,6 @@ bool gemm_pp_shape_ok(int M, int N, int R, int splits) {
     return M % BT == 0 && N % BT == 0 && R % BK == 0 && splits >= 1 && R / BK >= splits;
 }
 
-// BPE_GPP_SPREAD (read once, default 1): the spread DMA schedule where it applies (both operands K-major)
-static bool spread_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("BPE_GPP_SPREAD");
-        return !e || e[0] != '0';
-    }();
-    return on;
-}
 
 template <bool AK, bool BKM, bool SLAB, int DIAG, bool SPREAD>
 static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
@@ -710,10 +746,8 @@ static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, fl
 template <bool AK, bool BKM, bool SLAB, int DIAG>
 static void launch_pp1(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                       float beta, int M, int N, int R, int splits, hipStream_t s) {
-    if constexpr (AK && BKM) {
-        if (spread_enabled())
-            return launch_pp1s<AK, BKM, SLAB, DIAG, true>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
-    }
+    if (DIAG != 5 && spread_enabled())
+        return launch_pp1s<AK, BKM, SLAB, DIAG, true>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
     launch_pp1s<AK, BKM, SLAB, DIAG, false>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
 }
 
