@@ -1,5 +1,6 @@
-"""SwiGLU kernels at GPT-2-small training shapes (bf16): the gate forward, the standalone backward, the dY.W2 GEMM
-with the SwiGLU backward in its epilogue, and the unfused pair it replaces (hipBLASLt dY.W2 + swiglu_bwd).
+"""SwiGLU kernels at GPT-2-small training shapes (bf16): the gate forward, the X.W13 GEMM with the gate in its
+epilogue and the unfused pair it replaces (hipBLASLt X.W13^T + swiglu_fwd), the standalone backward, the dY.W2
+GEMM with the SwiGLU backward in its epilogue, and the unfused pair it replaces (hipBLASLt dY.W2 + swiglu_bwd).
 
     python benchmarks/swiglu_bench.py [--tokens 131072] [--dim 768] [--ff 2048]
 
@@ -42,9 +43,15 @@ def main():
     dy = torch.randn(M, d, device="cuda", dtype=torch.bfloat16)
     w2 = (0.05 * torch.randn(d, F, device="cuda")).to(torch.bfloat16)
     da = torch.randn(M, F, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(M, d, device="cuda", dtype=torch.bfloat16)
+    w13 = (0.05 * torch.randn(2 * F, d, device="cuda")).to(torch.bfloat16)
     gemm_flops = 2.0 * M * d * F
     rows = {
         "swiglu_fwd": (lambda: h.swiglu_fwd(gu), 3 * M * F * 2, 0.0),
+        "gemm_swiglu_fwd(fused)": (lambda: h.gemm_swiglu_fwd(x, w13), 3 * M * F * 2, 2 * gemm_flops),
+        "X@W13 (hipBLASLt)": (lambda: torch.matmul(x, w13.t()), 2 * M * F * 2, 2 * gemm_flops),
+        "X@W13 + swiglu_fwd (unfused)": (lambda: h.swiglu_fwd(torch.matmul(x, w13.t())), 5 * M * F * 2,
+                                         2 * gemm_flops),
         "swiglu_bwd": (lambda: h.swiglu_bwd(da, gu), 5 * M * F * 2, 0.0),
         "gemm_swiglu_bwd(fused)": (lambda: h.gemm_swiglu_bwd(dy, w2, gu), 4 * M * F * 2, gemm_flops),
         "dY@W2 (hipBLASLt)": (lambda: torch.matmul(dy, w2), M * F * 2, gemm_flops),

@@ -76,6 +76,16 @@ def _fuse_swiglu_bwd(dy: Tensor, w2: Tensor, gu: Tensor) -> bool:
             and gu.is_contiguous() and dy.stride(1) == 1 and w2.stride(1) == 1)
 
 
+_FUSE_SWIGLU_FWD = os.environ.get("BPE_FUSE_SWIGLU_FWD", "1") == "1"
+
+
+def _fuse_swiglu_fwd(x: Tensor, w13: Tensor) -> bool:
+    """The W13 GEMM with a = silu(g) * u in its epilogue (csrc/gemm_pp.hip EPI_SWIGLU_FWD): tokens in multiples
+    of 256, d_ff of 128, d_model of 64."""
+    return (_FUSE_SWIGLU_FWD and x.dtype == torch.bfloat16 and x.shape[0] % 256 == 0 and x.shape[1] % 64 == 0
+            and w13.shape[0] % 256 == 0 and x.stride(1) == 1 and w13.stride(1) == 1)
+
+
 _DX_TN = os.environ.get("BPE_DX_TN", "1") == "1"
 
 
@@ -134,8 +144,11 @@ class FusedBlockFn(torch.autograd.Function):
         o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, pre)
         g1 = mm(o, wo.detach(), 1) if fp8 is not None else torch.matmul(o, wo.t())
         xm, h2, r2 = hip().add_rmsnorm_fwd(x2, g1, ln2, eps)
-        gu = mm(h2, w_13, 2) if fp8 is not None else torch.matmul(h2, w_13.t())
-        a = hip().swiglu_fwd(gu)
+        if fp8 is None and _fuse_swiglu_fwd(h2, w_13):
+            gu, a = hip().gemm_swiglu_fwd(h2, w_13)  # the gate in the GEMM epilogue: no second pass over gu
+        else:
+            gu = mm(h2, w_13, 2) if fp8 is not None else torch.matmul(h2, w_13.t())
+            a = hip().swiglu_fwd(gu)
         g2 = mm(a, w2.detach(), 3) if fp8 is not None else torch.matmul(a, w2.t())
         ctx.w8s = w8s if w8s else None
         ctx.has_xd = xd is not None

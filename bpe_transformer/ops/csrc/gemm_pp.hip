@@ -330,12 +330,18 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
 // gradient of a = silu(g) * u); instead of storing da the epilogue reads g and u from gu = [g | u] ([M][2F])
 // and writes dgu = [dg | du] -- the SwiGLU backward without the da round trip through HBM.  Same math and
 // rounding as swiglu_bwd_kernel (da rounded to bf16 first).
-enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1 };
+// EPI_SWIGLU_FWD: the forward gu = X [W1; W3]^T with a = silu(g) * u in the epilogue.  A workgroup's 256 output
+// columns are 128 columns of g and the SAME 128 columns of u (B rows [128 t, +128) and [F + 128 t, +128) of
+// [W1; W3]), so the epilogue writes both halves of gu and the gate a from one tile -- the separate swiglu_fwd
+// pass over gu (read 2F, write F per token) disappears.  Same rounding as swiglu_fwd_kernel (a from bf16 g, u).
+enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2 };
 struct Epi {
     const __bf16* gu;
-    __bf16* dgu;
-    long ld;  // row stride of gu / dgu (elements)
+    __bf16* dgu;  // EPI_SWIGLU_BWD: dgu out; EPI_SWIGLU_FWD: gu out
+    long ld;      // row stride of gu / dgu (elements)
     int F;
+    __bf16* act = nullptr;  // EPI_SWIGLU_FWD: a = silu(g) * u, [M][F]
+    long ld_act = 0;
 };
 
 template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, bool SPREAD = false>
@@ -355,6 +361,8 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     const int ntiles = (M / BT) * tiles_n;
     const int split = wid / ntiles, tile = wid % ntiles;
     const int i0 = (tile / tiles_n) * BT, j0 = (tile % tiles_n) * BT;
+    // B tile origin: EPI_SWIGLU_FWD tiles 128 g columns (+ the matching u columns, offset F rows in B)
+    const int jb = EPI == EPI_SWIGLU_FWD ? (tile % tiles_n) * (BT / 2) : j0;
     const int nkt = R / BK;
     const int kb = (int)((long)split * nkt / splits);
     const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
@@ -367,11 +375,23 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
         for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if constexpr (SPR) {
-        const SpreadOff so = spread_offsets<AK, BKM>(g, wl, l, (int)lda, (int)ldb);
+        SpreadOff so = spread_offsets<AK, BKM>(g, wl, l, (int)lda, (int)ldb);
+        if constexpr (EPI == EPI_SWIGLU_FWD) {
+            // group g DMAs B rows [128 g, +128) of the tile: group 1's are the u rows, F - 128 rows further on
+            static_assert(BKM, "SwiGLU forward: B = [W1; W3] is K-major");
+            if (g == 1) {
+                const int du = (ep.F - BT / 2) * (int)ldb;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    so.b0[j] += du;
+                    so.b1[j] += du;
+                }
+            }
+        }
         {  // prologue: all of K-tile 0 (this wave's 8 pieces of the schedule), retired before the first read
             const long k0 = (long)kb * BK;
             const __bf16* a0 = tile_ptr<AK>(A, lda, i0, k0);
-            const __bf16* b0 = tile_ptr<BKM>(B, ldb, j0, k0);
+            const __bf16* b0 = tile_ptr<BKM>(B, ldb, jb, k0);
             dma_pair(a0, so.a0, smem, so.la0);
             dma_pair(b0, so.b0, smem + OPB, so.lb0);
             dma_pair(b0, so.b1, smem + OPB, so.lb1);
@@ -385,7 +405,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
             char* nxt = smem + ((kt + 1) & 1) * STAGE;
             const long k1 = (long)(kb + kt + 1) * BK;
             ktile_spread<AK, BKM, DIAG>(cur, nxt, kt + 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
-                                        tile_ptr<BKM>(B, ldb, j0, k1), so, g, wl, l, acc);
+                                        tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc);
         }
     } else {
         int oa[4], ob[4];
@@ -468,6 +488,28 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
                 }
                 *reinterpret_cast<u16x8*>(ep.dgu + ro) = dg;
                 *reinterpret_cast<u16x8*>(ep.dgu + ro + ep.F) = du;
+            }
+            return;
+        }
+        if constexpr (EPI == EPI_SWIGLU_FWD) {
+            // row i: g = staged columns [0, 128), u = [128, 256); 16 threads x 16 bytes per 256-byte segment
+            __syncthreads();
+            const int c = tid & 15;
+#pragma unroll 4
+            for (int q = 0; q < 8; ++q) {
+                const int i = q * 32 + (tid >> 4);
+                const u16x8 gv = *reinterpret_cast<const u16x8*>(smem + i * 512 + ((c ^ (i & 15)) << 4));
+                const u16x8 uv = *reinterpret_cast<const u16x8*>(smem + i * 512 + (((16 + c) ^ (i & 15)) << 4));
+                u16x8 av;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float gg = bf2f(gv[e]);
+                    av[e] = f2bf(gg * fast_sigmoid(gg) * bf2f(uv[e]));
+                }
+                const long r = i0 + i;
+                *reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + jb + c * 8) = gv;
+                *reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + ep.F + jb + c * 8) = uv;
+                *reinterpret_cast<u16x8*>(ep.act + r * ep.ld_act + jb + c * 8) = av;
             }
             return;
         }
@@ -723,6 +765,21 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
     Epi ep{(const __bf16*)gu, (__bf16*)dgu, ldg, F};
     k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)dY, ldy, (const __bf16*)W2, ldw, nullptr, nullptr, 0, 0.f, M, F, R,
                                   1, ep);
+}
+
+// gu = X . [W1; W3]^T and a = silu(g) * u (EPI_SWIGLU_FWD): X [M][R], W13 [2F][R] (both K-major)
+void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ldw, void* gu, long ldg, void* act,
+                               long lda_, int M, int F, int R, hipStream_t s) {
+    static bool attr = false;
+    auto* k = &gemm_pp_kernel<true, true, false, 0, EPI_SWIGLU_FWD, true>;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        attr = true;
+    }
+    const int grid = (M / BT) * (F / (BT / 2));
+    Epi ep{nullptr, (__bf16*)gu, ldg, F, (__bf16*)act, lda_};
+    k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)X, ldx, (const __bf16*)W13, ldw, nullptr, nullptr, 0, 0.f, M, 2 * F,
+                                  R, 1, ep);
 }
 
 bool gemm_pp_shape_ok(int M, int N, int R, int splits) {

@@ -70,6 +70,8 @@ bool gemm_pp_shape_ok(int M, int N, int R, int splits);
 void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                     float beta, int M, int N, int R, int splits, float* slab, hipStream_t s);
 
+void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ldw, void* gu, long ldg, void* act,
+                               long lda_, int M, int F, int R, hipStream_t s);
 void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,
                                long ldg, int M, int F, int R, hipStream_t s);
 

@@ -369,6 +369,27 @@ at::Tensor gemm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& w2, const at:
     return dgu;
 }
 
+// (gu, a): gu = x @ w13^T with a = silu(g) * u in the GEMM epilogue (no separate pass over gu)
+std::tuple<at::Tensor, at::Tensor> gemm_swiglu_fwd(const at::Tensor& x, const at::Tensor& w13) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w13.scalar_type() == at::kBFloat16,
+                "gemm_swiglu_fwd: bf16 tensors required");
+    TORCH_CHECK(x.dim() == 2 && w13.dim() == 2 && x.stride(1) == 1 && w13.stride(1) == 1,
+                "gemm_swiglu_fwd: row-major 2-D tensors required");
+    const int M = (int)x.size(0), R = (int)x.size(1), F = (int)(w13.size(0) / 2);
+    TORCH_CHECK(w13.size(1) == R && w13.size(0) == 2 * F, "gemm_swiglu_fwd: shape mismatch");
+    TORCH_CHECK(M % 256 == 0 && F % 128 == 0 && R % 64 == 0, "gemm_swiglu_fwd: M multiple of 256, F of 128, d of 64");
+    TORCH_CHECK(x.stride(0) % 8 == 0 && w13.stride(0) % 8 == 0, "gemm_swiglu_fwd: 16-byte row alignment");
+    TORCH_CHECK(2L * F * w13.stride(0) < (1L << 31) && 256L * x.stride(0) < (1L << 31),
+                "gemm_swiglu_fwd: operand offsets exceed 32 bits");
+    DevGuard g(x.device());
+    auto gu = at::empty({M, 2 * F}, x.options());
+    auto a = at::empty({M, F}, x.options());
+    launch_gemm_pp_swiglu_fwd(x.data_ptr(), x.stride(0), w13.data_ptr(), w13.stride(0), gu.data_ptr(), 2 * (long)F,
+                              a.data_ptr(), F, M, F, R, cur_stream());
+    return {gu, a};
+}
+
 // ---------------------------------------------------------------- FP8 quantisation (delayed scaling)
 void cast_fp8(const at::Tensor& x, const at::Tensor& scale, at::Tensor out, at::Tensor amax_bits) {
     check_cuda(x, "x");
@@ -744,6 +765,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("grad_norm(Tensor[] tensors, float max_norm) -> (Tensor, Tensor)");
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
     m.def("gemm_swiglu_bwd(Tensor dy, Tensor w2, Tensor gu) -> Tensor");
+    m.def("gemm_swiglu_fwd(Tensor x, Tensor w13) -> (Tensor, Tensor)");
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
@@ -779,6 +801,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("gemm", &gemm);
     m.impl("gemm_pp", &gemm_pp);
     m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
+    m.impl("gemm_swiglu_fwd", &gemm_swiglu_fwd);
     m.impl("cast_fp8", &cast_fp8);
     m.impl("transpose_bf16", &transpose_bf16);
     m.impl("cast_fp8_t", &cast_fp8_t);
