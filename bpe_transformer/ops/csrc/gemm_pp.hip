@@ -167,6 +167,17 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const Frags& f,
                 acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
 }
 
+// Half of a quadrant (i-blocks 2h, 2h+1): the MFMA section can then issue one DMA piece between its halves.
+__device__ __forceinline__ void mma_half(f32x4 (&acc)[8][4], const Frags& f, int m, int n, int h) {
+#pragma unroll
+    for (int ib = 2 * h; ib < 2 * h + 2; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+                acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
+}
+
 // One K-tile: four (load section, barrier, MFMA section, barrier) phases.  `cur` is read, `nxt` is the DMA
 // target (the __restrict__ parameters let the wait-count pass see that the fragment reads do not alias the
 // in-flight DMA; without it hipcc drains the DMA before the first read).
@@ -264,6 +275,10 @@ __device__ __forceinline__ SpreadOff spread_offsets(int g, int wl, int l, int ld
     return o;
 }
 
+__device__ __forceinline__ void dma_one(const __bf16* tile0, int off, char* img, int lbase) {
+    __builtin_amdgcn_global_load_lds((gbl_void*)(tile0 + off), (lds_void*)(img + lbase * 16), 16, 0, 0);
+}
+
 __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2], char* img, int lbase) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -271,7 +286,9 @@ __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2
                                          0, 0);
 }
 
-template <bool AK, bool BKM, int DIAG>
+// SPLIT (BPE_GPP_DMA_SPLIT=1): the second piece of each pair is issued by the same wave in its MFMA section,
+// between the two halves of the quadrant, so a load section carries one piece; the waits become vmcnt(3).
+template <bool AK, bool BKM, int DIAG, bool SPLIT = false>
 __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
                                              const __bf16* an, const __bf16* bn, const SpreadOff& so, int g, int wl,
                                              int l, f32x4 (&acc)[8][4]) {
@@ -279,51 +296,48 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     char* Ac = cur;
     char* Bc = cur + OPB;
     if (DIAG == 1) dma = false;
+    // one phase: fragment reads (done by the caller), pieces of (tile, off, img, lbase), wait, barrier, MFMAs
+    auto phase = [&](const __bf16* t0, const int (&off)[2], char* img, int lb, int m, int n, bool last_nodma_wait2) {
+        if (dma) {
+            if constexpr (SPLIT) {
+                dma_one(t0, off[0], img, lb);
+                asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+            } else {
+                dma_pair(t0, off, img, lb);
+                asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+            }
+        } else if (last_nodma_wait2) {
+            asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        }
+        bar();
+        if constexpr (SPLIT) {
+            mma_half(acc, f, m, n, 0);
+            if (dma) {
+                __builtin_amdgcn_sched_barrier(0);
+                dma_one(t0, off[1], img, lb + 64);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            mma_half(acc, f, m, n, 1);
+        } else {
+            mma_quadrant(acc, f, m, n);
+        }
+        bar();
+    };
     // phase 0: (m0, n0)
     load_a<AK, BKM, true>(f, Ac, g, 0, l);
     load_b<AK, BKM, true>(f, Bc, wl, 0, l);
-    if (dma) {
-        dma_pair(an, so.a0, nxt, so.la0);
-        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-    }
-    bar();
-    mma_quadrant(acc, f, 0, 0);
-    bar();
+    phase(an, so.a0, nxt, so.la0, 0, 0, true);
     // phase 1: (m0, n1)
     load_b<AK, BKM, true>(f, Bc, wl, 1, l);
-    if (dma) {
-        dma_pair(bn, so.b0, nxt + OPB, so.lb0);
-        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-    bar();
-    mma_quadrant(acc, f, 0, 1);
-    bar();
+    phase(bn, so.b0, nxt + OPB, so.lb0, 0, 1, false);
     // phase 2: (m1, n1)
     load_a<AK, BKM, true>(f, Ac, g, 1, l);
-    if (dma) {
-        dma_pair(bn, so.b1, nxt + OPB, so.lb1);
-        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-    bar();
-    mma_quadrant(acc, f, 1, 1);
-    bar();
+    phase(bn, so.b1, nxt + OPB, so.lb1, 1, 1, false);
     // phase 3: (m1, n0)
     load_b<AK, BKM, true>(f, Bc, wl, 0, l);
-    if (dma) {
-        dma_pair(an, so.a1, nxt, so.la1);
-        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-    bar();
-    mma_quadrant(acc, f, 1, 0);
-    bar();
+    phase(an, so.a1, nxt, so.la1, 1, 0, false);
 }
 
 // Fused epilogues of the one-tile-per-workgroup kernel.  EPI_SWIGLU_BWD: the GEMM result is da = dY W2 (the
@@ -344,7 +358,7 @@ struct Epi {
     long ld_act = 0;
 };
 
-template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, bool SPREAD = false>
+template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, int SPREAD = 0>
 __global__ void __launch_bounds__(NT, 1)
 gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
                float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int M, int N, int R,
@@ -367,7 +381,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     const int kb = (int)((long)split * nkt / splits);
     const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
 
-    constexpr bool SPR = SPREAD;
+    constexpr bool SPR = SPREAD != 0;
     f32x4 acc[8][4];
 #pragma unroll
     for (int a = 0; a < 8; ++a)
@@ -404,8 +418,8 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
             char* cur = smem + (kt & 1) * STAGE;
             char* nxt = smem + ((kt + 1) & 1) * STAGE;
             const long k1 = (long)(kb + kt + 1) * BK;
-            ktile_spread<AK, BKM, DIAG>(cur, nxt, kt + 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
-                                        tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc);
+            ktile_spread<AK, BKM, DIAG, SPREAD == 2>(cur, nxt, kt + 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
+                                                     tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc);
         }
     } else {
         int oa[4], ob[4];
@@ -742,21 +756,25 @@ gemm_pp_pers_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __rest
 
 using namespace bpe::gpp;
 
-// BPE_GPP_SPREAD (read once, default 1): the spread DMA schedule (0: the burst schedule of ktile)
-static bool spread_enabled() {
-    static const bool on = [] {
+// BPE_GPP_SPREAD (read once): 1 = the spread DMA schedule, 2 = spread with one piece per section moved into
+// the MFMA section, 0 = the burst schedule of ktile.  Unset: 2 for the weight gradient (both operands MN-major:
+// +1-3 %), 1 for the rest (2 is 3 % slower there; profiles/bench/ab_gpp_dma_split.log).
+static int spread_mode(bool weight_grad = false) {
+    static const int m = [] {
         const char* e = getenv("BPE_GPP_SPREAD");
-        return !e || e[0] != '0';
+        return e ? atoi(e) : -1;
     }();
-    return on;
+    return m >= 0 ? m : (weight_grad ? 2 : 1);
 }
 
 // dgu = swiglu_bwd(dY . W2, gu): A = dY [M][R] (K-major), B = W2 [R][F] (MN-major)
 void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,
                                long ldg, int M, int F, int R, hipStream_t s) {
     static bool attr = false;
-    auto* k = spread_enabled() ? &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, true>
-                               : &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, false>;
+    const int sm = spread_mode();
+    auto* k = sm == 2   ? &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, 2>
+              : sm == 1 ? &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, 1>
+                        : &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, 0>;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr = true;
@@ -771,7 +789,8 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
 void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ldw, void* gu, long ldg, void* act,
                                long lda_, int M, int F, int R, hipStream_t s) {
     static bool attr = false;
-    auto* k = &gemm_pp_kernel<true, true, false, 0, EPI_SWIGLU_FWD, true>;
+    auto* k = spread_mode() == 2 ? &gemm_pp_kernel<true, true, false, 0, EPI_SWIGLU_FWD, 2>
+                                 : &gemm_pp_kernel<true, true, false, 0, EPI_SWIGLU_FWD, 1>;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr = true;
@@ -787,7 +806,7 @@ bool gemm_pp_shape_ok(int M, int N, int R, int splits) {
 }
 
 
-template <bool AK, bool BKM, bool SLAB, int DIAG, bool SPREAD>
+template <bool AK, bool BKM, bool SLAB, int DIAG, int SPREAD>
 static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                         float beta, int M, int N, int R, int splits, hipStream_t s) {
     static bool attr = false;  // > 64 KiB dynamic LDS must be opted into once per instantiation
@@ -803,9 +822,10 @@ static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, fl
 template <bool AK, bool BKM, bool SLAB, int DIAG>
 static void launch_pp1(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                       float beta, int M, int N, int R, int splits, hipStream_t s) {
-    if (DIAG != 5 && spread_enabled())
-        return launch_pp1s<AK, BKM, SLAB, DIAG, true>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
-    launch_pp1s<AK, BKM, SLAB, DIAG, false>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
+    const int sm = DIAG == 5 ? 0 : spread_mode(!AK && !BKM);
+    if (sm == 2) return launch_pp1s<AK, BKM, SLAB, DIAG, 2>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
+    if (sm == 1) return launch_pp1s<AK, BKM, SLAB, DIAG, 1>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
+    launch_pp1s<AK, BKM, SLAB, DIAG, 0>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
 }
 
 template <bool AK, bool BKM, bool SLAB>
