@@ -29,6 +29,19 @@ def default_lmhead_chunk() -> int:
     return int(os.environ.get("BPE_LMHEAD_CHUNK", "0"))
 
 
+_HEAD_DX_TN = os.environ.get("BPE_HEAD_DX_TN", "1") == "1"
+
+
+def _head_dx(dlogits: Tensor, w: Tensor) -> Tensor:
+    """dh = dlogits @ W in hipBLASLt's TN layout through a transposed copy of W (``ops.transpose_bf16``, as the
+    blocks' input gradients do: models/fused_block.py ``_dx_tn``): 7.24 vs 8.27 ms at GPT-2 B 128 with tuned
+    solutions (profiles/bench/head_dx_layouts_b128.log), +0.65 % end to end.  ``BPE_HEAD_DX_TN=0`` keeps NN."""
+    if (_HEAD_DX_TN and w.dtype == torch.bfloat16 and dlogits.is_cuda and w.stride(1) == 1
+            and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0):
+        return torch.matmul(dlogits, ops().transpose_bf16(w).t())
+    return torch.matmul(dlogits, w)
+
+
 class _LMHeadCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h: Tensor, w: Tensor, targets: Tensor, ignore_index: int, chunk: int):
@@ -66,7 +79,7 @@ class _LMHeadCEFn(torch.autograd.Function):
     def backward(ctx, g: Tensor):
         h, w, dlogits = ctx.saved_tensors
         gg = g.to(h.dtype)
-        dh = torch.matmul(dlogits, w) * gg  # the upstream scale goes on the small operands, never on the logits
+        dh = _head_dx(dlogits, w) * gg  # the upstream scale goes on the small operands, never on the logits
         hs = h * gg
         mg = getattr(ctx.w_param, "_bpe_padded_grad" if ctx.padded else "main_grad", None)
         if ctx.padded and mg is None:
