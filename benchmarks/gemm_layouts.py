@@ -2,6 +2,7 @@
 at the model's real shapes, in each operand layout the library / our kernel can run it in.
 
   fwd : Y  = X  @ W^T        X [T,K], W [N,K]            (both operands K-contiguous)
+  fwdN: Y  = X  @ Wt         Wt = W^T materialised [K,N] (the copy the TN input gradient makes)
   dX  : dX = dY @ W          dY [T,N], W [N,K]           (B is N-contiguous: the "NN" layout)
   dXt : dX = dY @ (W^T)^T    with W^T materialised once  (back to the K-contiguous layout; the
                                                           transpose copy is timed separately)
@@ -58,12 +59,13 @@ def main():
         dx = torch.empty(T, k, device="cuda", dtype=bf)
         wt = w.t().contiguous()
         g = torch.zeros(n, k, device="cuda", dtype=bf)
-        r = {k_: [] for k_ in ("fwd", "dX", "dXt", "tr", "dW_blas", "dW_ours", "dW_256")}
+        r = {k_: [] for k_ in ("fwd", "fwdN", "dX", "dXt", "tr", "dW_blas", "dW_ours", "dW_256")}
         ours_ok = n % 128 == 0 and k % 128 == 0
         s128 = choose_splits(n, k, T)
         s256 = choose_splits_256(n, k, T) if use_tile256(n, k, T) else None
         for _ in range(a.rounds):
             r["fwd"].append(bench(lambda: torch.matmul(x, w.t(), out=y)))
+            r["fwdN"].append(bench(lambda: torch.matmul(x, wt, out=y)))
             r["dX"].append(bench(lambda: torch.matmul(dy, w, out=dx)))
             r["dXt"].append(bench(lambda: torch.matmul(dy, wt.t(), out=dx)))
             r["tr"].append(bench(lambda: wt.copy_(w.t())))

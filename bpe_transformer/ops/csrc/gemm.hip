@@ -416,9 +416,10 @@ template <int MF, bool PRIO, int DSPLIT = 0>
 __global__ void __launch_bounds__(NT, 1)
 gemm256_tn_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
                   float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int Mo, int No, int R,
-                  int splits) {
+                  int splits, int prio) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+    if (prio && w >= 4) __builtin_amdgcn_s_setprio(1);  // static form of guide T5: the younger wave half
     // XCD-aware bijective remap: consecutive work ids (same split, neighbouring tiles sharing token rows)
     // run on one XCD and its L2 (guide §5 "XCD swizzle must be bijective").
     const int nwg = gridDim.x, orig = blockIdx.x;
@@ -499,7 +500,7 @@ bool gemm_shape_ok(int Mo, int No, int R, int splits, int tile) {
 
 template <int MF, bool PRIO, int DSPLIT = 0>
 static void launch_g256_v(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
-                          float beta, int Mo, int No, int R, int splits, hipStream_t s) {
+                          float beta, int Mo, int No, int R, int splits, hipStream_t s, int prio) {
     static bool attr = false;  // > 64 KiB dynamic LDS must be opted into once per instantiation
     auto* k = &g256::gemm256_tn_kernel<MF, PRIO, DSPLIT>;
     if (!attr) {
@@ -507,24 +508,26 @@ static void launch_g256_v(const __bf16* a, long lda, const __bf16* b, long ldb, 
         attr = true;
     }
     const int grid = (Mo / 256) * (No / 256) * splits;
-    k<<<grid, g256::NT, g256::LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits);
+    k<<<grid, g256::NT, g256::LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, prio);
 }
 
 // variant (BPE_G256_VARIANT, read once): bit 0 = 16x16x32 MFMA, bit 1 = setprio'd MFMA cluster, bit 2 / bit 3 =
-// the DMA split over the step in 2 / 4 places (32x32x16, overrides bits 0-1)
+// the DMA split over the step in 2 / 4 places (32x32x16, overrides bits 0-1), bit 4 = static s_setprio 1 for
+// waves 4-7
 static void launch_g256(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                         float beta, int Mo, int No, int R, int splits, hipStream_t s) {
     static int variant = [] {  // default 4: +3-4 % over the one-burst DMA (profiles/bench/ab_dw_dma_split.log)
         const char* e = getenv("BPE_G256_VARIANT");
         return e ? atoi(e) : 4;
     }();
-    if (variant & 8) return launch_g256_v<32, false, 2>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s);
-    if (variant & 4) return launch_g256_v<32, false, 1>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s);
+    const int pr = (variant >> 4) & 1;
+    if (variant & 8) return launch_g256_v<32, false, 2>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr);
+    if (variant & 4) return launch_g256_v<32, false, 1>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr);
     switch (variant & 3) {
-        case 0: launch_g256_v<32, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;
-        case 1: launch_g256_v<16, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;
-        case 2: launch_g256_v<32, true>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;
-        default: launch_g256_v<16, true>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s); break;
+        case 0: launch_g256_v<32, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;
+        case 1: launch_g256_v<16, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;
+        case 2: launch_g256_v<32, true>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;
+        default: launch_g256_v<16, true>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;
     }
 }
 

@@ -356,6 +356,7 @@ struct Epi {
     int F;
     __bf16* act = nullptr;  // EPI_SWIGLU_FWD: a = silu(g) * u, [M][F]
     long ld_act = 0;
+    int prio = 0;  // 1: group 1 (the younger waves 4-7) runs at s_setprio 1 (guide T5, static form)
 };
 
 template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, int SPREAD = 0>
@@ -382,6 +383,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
 
     constexpr bool SPR = SPREAD != 0;
+    if (ep.prio && g == 1) __builtin_amdgcn_s_setprio(1);  // g is wave-uniform (readfirstlane): a scalar branch
     f32x4 acc[8][4];
 #pragma unroll
     for (int a = 0; a < 8; ++a)
@@ -756,6 +758,16 @@ gemm_pp_pers_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __rest
 
 using namespace bpe::gpp;
 
+// BPE_GPP_PRIO (read once, default 1): static s_setprio 1 for the younger wave group (end to end +0.1-0.6 %,
+// profiles/bench/ab_e2e_gpp_prio.log)
+static int prio_mode() {
+    static const int m = [] {
+        const char* e = getenv("BPE_GPP_PRIO");
+        return e ? atoi(e) : 1;
+    }();
+    return m;
+}
+
 // BPE_GPP_SPREAD (read once): 1 = the spread DMA schedule, 2 = spread with one piece per section moved into
 // the MFMA section, 0 = the burst schedule of ktile.  Unset: 2 for the weight gradient (both operands MN-major:
 // +1-3 %), 1 for the rest (2 is 3 % slower there; profiles/bench/ab_gpp_dma_split.log).
@@ -781,6 +793,7 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
     }
     const int grid = (M / BT) * (F / BT);
     Epi ep{(const __bf16*)gu, (__bf16*)dgu, ldg, F};
+    ep.prio = prio_mode();
     k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)dY, ldy, (const __bf16*)W2, ldw, nullptr, nullptr, 0, 0.f, M, F, R,
                                   1, ep);
 }
@@ -797,6 +810,7 @@ void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ld
     }
     const int grid = (M / BT) * (F / (BT / 2));
     Epi ep{nullptr, (__bf16*)gu, ldg, F, (__bf16*)act, lda_};
+    ep.prio = prio_mode();
     k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)X, ldx, (const __bf16*)W13, ldw, nullptr, nullptr, 0, 0.f, M, 2 * F,
                                   R, 1, ep);
 }
@@ -816,7 +830,9 @@ static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, fl
         attr = true;
     }
     const int grid = (M / BT) * (N / BT) * splits;
-    k<<<grid, NT, LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, Epi{});
+    Epi ep{};
+    ep.prio = prio_mode();
+    k<<<grid, NT, LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, ep);
 }
 
 template <bool AK, bool BKM, bool SLAB, int DIAG>
