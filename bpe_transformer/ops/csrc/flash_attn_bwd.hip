@@ -140,6 +140,8 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     float* dltS = lseS + 128;                                              // [2][64]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    // flags bit 0: static s_setprio 1 for the younger half of the waves (guide T5 static form; wave-uniform test)
+    if ((flags & 1) && __builtin_amdgcn_readfirstlane(tid >> 6) >= NW / 2) __builtin_amdgcn_s_setprio(1);
     // one workgroup per (key block, batch, QUERY head): with GQA the G query heads of a kv head run in
     // parallel (their dK / dV partials are summed by fa_dkv_reduce_kernel) instead of one workgroup sweeping
     // all G heads -- with causal masking that serial sweep left most CUs idle behind the key-block-0 groups.
@@ -472,6 +474,15 @@ using namespace bpe::fa;
 
 size_t fa_bwd_lds_bytes(int D) { return D == 64 ? BwdCfg<64>::LDS : BwdCfg<128>::LDS; }
 
+// BPE_FA_BWD_PRIO (read once, default 0): static s_setprio 1 for waves NW/2.. of the backward kernel
+static int bwd_prio() {
+    static const int p = [] {
+        const char* e = getenv("BPE_FA_BWD_PRIO");
+        return e ? atoi(e) : 0;
+    }();
+    return p;
+}
+
 template <int D, bool C, bool R, int DBG, bool RIN>
 static void bwd_main_k(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
     using Cfg = BwdCfg<D>;
@@ -483,7 +494,8 @@ static void bwd_main_k(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
     }
     fa_bwd_kernel<D, C, R, DBG, RIN><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv,
-        a.dkv_part, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, dbg, fa_group(a.B * a.H));
+        a.dkv_part, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, (dbg << 1) | (bwd_prio() & 1),
+        fa_group(a.B * a.H));
 }
 
 template <int D, bool C, bool R, int DBG>
