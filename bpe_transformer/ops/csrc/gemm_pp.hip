@@ -182,6 +182,7 @@ __device__ __forceinline__ void mma_half(f32x4 (&acc)[8][4], const Frags& f, int
 // target (the __restrict__ parameters let the wait-count pass see that the fragment reads do not alias the
 // in-flight DMA; without it hipcc drains the DMA before the first read).
 // DIAG (timing diagnostics, numerically wrong): 1 = no DMA in the loop, 2 = fragment reads only in phase 0,
+// 6 = no epilogue global stores (gemm_pp_kernel),
 // 3 = no MFMA, 4 = no stagger between the groups, 5 = DMA issued but never waited for (issue cost only)
 template <bool AK, bool BKM, int DIAG>
 __device__ __forceinline__ void ktile(char* __restrict__ cur, char* __restrict__ nxt, bool dma, const __bf16* an,
@@ -453,6 +454,9 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     bar();  // every fragment read done: the LDS is free for the epilogue
 
+    // DIAG 6 (timing only): the epilogue's global stores are skipped (kept in the code behind a runtime test
+    // that is never true, so the MFMAs and the LDS staging stay): prices the store burst at the end of each tile
+    const bool st_on = DIAG != 6 || ep.prio == 77;
     // accumulator (ib, jb) register r of lane l: row i = 128 g + 16 ib + (l & 15), col j = 64 wl + 16 jb + 4 (l >> 4) + r
     if constexpr (SLAB) {
         float* sp = slab + (long)split * M * N;
@@ -462,7 +466,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
             for (int jb = 0; jb < 4; ++jb) {
                 const long i = i0 + 128 * g + 16 * ib + (l & 15);
                 const long j = j0 + 64 * wl + 16 * jb + 4 * (l >> 4);
-                *reinterpret_cast<f32x4*>(sp + i * N + j) = acc[ib][jb];
+                if (st_on) *reinterpret_cast<f32x4*>(sp + i * N + j) = acc[ib][jb];
             }
     } else {
         // stage bf16 tile as [256][512 B], 16-byte chunk c of row i at c ^ (i & 15)
@@ -540,7 +544,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
 #pragma unroll
                 for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + beta * bf2f(o[e]));
             }
-            *reinterpret_cast<u16x8*>(cp) = v;
+            if (st_on) *reinterpret_cast<u16x8*>(cp) = v;
         }
     }
 }
@@ -887,6 +891,7 @@ static void launch_pp(const __bf16* a, long lda, const __bf16* b, long ldb, floa
         case 3: launch_pp1<AK, BKM, SLAB, 3>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
         case 4: launch_pp1<AK, BKM, SLAB, 4>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
         case 5: launch_pp1<AK, BKM, SLAB, 5>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
+        case 6: launch_pp1<AK, BKM, SLAB, 6>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
 #endif
         default: launch_pp1<AK, BKM, SLAB, 0>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
     }
