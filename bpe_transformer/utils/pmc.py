@@ -19,6 +19,9 @@ Derived values:
 * ``valu_per_mfma``, ``lds_per_mfma``: instruction ratios.
 * ``lds_conflict``: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE.
 * ``wait_frac``: SQ_WAIT_ANY / SQ_WAVE_CYCLES.
+* ``hbm_rd_TBps`` / ``hbm_wr_TBps``: FETCH_SIZE / WRITE_SIZE (KiB) over the kernel's mean duration from the
+  same directories' ``*kernel_trace.csv``.  FETCH_SIZE is doubled: on gfx950 it reports exactly half the bytes
+  of wide coalesced streaming reads (``MI355X_MICROARCH.md``, FETCH_SIZE note).
 """
 
 from __future__ import annotations
@@ -55,9 +58,29 @@ def load(dirs: list[str | Path], match: list[str] | None = None) -> dict[str, di
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
-def derive(c: dict[str, float], cus: int = MI355X_CUS, xcds: int = MI355X_XCDS) -> dict[str, float]:
+def load_durations(dirs: list[str | Path], match: list[str] | None = None) -> dict[str, float]:
+    """Mean dispatch duration (ns) per kernel from the runs' kernel traces."""
+    acc: dict[str, list[float]] = defaultdict(list)
+    for d in dirs:
+        for f in Path(d).glob("*kernel_trace.csv"):
+            for r in csv.DictReader(open(f)):
+                n = r["Kernel_Name"]
+                if match and not any(m in n for m in match):
+                    continue
+                acc[short_name(n)].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def derive(c: dict[str, float], cus: int = MI355X_CUS, xcds: int = MI355X_XCDS,
+           dur_ns: float | None = None) -> dict[str, float]:
     out: dict[str, float] = {}
     g = lambda k: c.get(k)  # noqa: E731
+    if dur_ns:
+        out["dur_us"] = dur_ns / 1e3
+        if g("FETCH_SIZE") is not None:
+            out["hbm_rd_TBps"] = 2 * g("FETCH_SIZE") * 1024 / dur_ns / 1e3
+        if g("WRITE_SIZE") is not None:
+            out["hbm_wr_TBps"] = g("WRITE_SIZE") * 1024 / dur_ns / 1e3
     if g("SQ_VALU_MFMA_BUSY_CYCLES") and g("GRBM_GUI_ACTIVE"):
         out["mfma_util"] = g("SQ_VALU_MFMA_BUSY_CYCLES") / (g("GRBM_GUI_ACTIVE") / xcds * cus * 4)
     if g("SQ_INSTS_MFMA"):
@@ -77,9 +100,10 @@ def derive(c: dict[str, float], cus: int = MI355X_CUS, xcds: int = MI355X_XCDS) 
 
 def report(dirs: list[str | Path], match: list[str] | None = None) -> str:
     data = load(dirs, match)
+    durs = load_durations(dirs, match)
     lines = []
     for k in sorted(data):
-        d = derive(data[k])
+        d = derive(data[k], dur_ns=durs.get(k))
         lines.append(f"## {k}")
         if d:
             lines.append("derived: " + ", ".join(f"{n}={v:.3g}" for n, v in d.items()))
