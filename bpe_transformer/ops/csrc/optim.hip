@@ -108,13 +108,26 @@ __global__ void __launch_bounds__(256) sumsq_partial_kernel(const T* __restrict_
     __shared__ float red[16];
     constexpr int V = Vec<T>::N;
     const size_t nv = n / V;
-    float acc = 0.f;
-    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < nv; i += (size_t)gridDim.x * 256) {
+    float acc = 0.f, acc2 = 0.f;
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = blockIdx.x * (size_t)256 + threadIdx.x;
+    for (; i + stride < nv; i += 2 * stride) {  // two independent 16-byte loads in flight per thread
+        Vec<T> a, b;
+        a.load(x + i * V);
+        b.load(x + (i + stride) * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            acc += a.v[j] * a.v[j];
+            acc2 += b.v[j] * b.v[j];
+        }
+    }
+    if (i < nv) {
         Vec<T> a;
         a.load(x + i * V);
 #pragma unroll
         for (int j = 0; j < V; ++j) acc += a.v[j] * a.v[j];
     }
+    acc += acc2;
     const size_t t = nv * V + blockIdx.x * (size_t)256 + threadIdx.x;
     if (blockIdx.x == 0 && t < n) {
         const float e = ld1<T>(x + t);

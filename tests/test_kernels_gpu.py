@@ -262,6 +262,16 @@ def test_flat_adamw_skip_keeps_bias_correction(gpu_device):
     torch.testing.assert_close(flat.data.cpu(), fcpu.data, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("dtype,n", [(torch.float32, 9_000_003), (torch.bfloat16, 20_000_001)])
+def test_grad_norm_large(gpu_device, dtype, n):
+    """Sizes past two grid strides (2048 blocks x 256 threads x one vector each), with a ragged tail."""
+    torch.manual_seed(1)
+    ts = [torch.randn(n, device=gpu_device).to(dtype), torch.randn(77, device=gpu_device).to(dtype)]
+    norm, _ = ops.grad_norm(ts, 1.0)
+    exp = torch.sqrt(sum((t.double() ** 2).sum() for t in ts)).item()
+    assert abs(norm.item() - exp) / exp < 1e-4
+
+
 def test_grad_norm_clip(gpu_device):
     torch.manual_seed(0)
     ts = [torch.randn(n, device=gpu_device) for n in (5, 1000, 3333)]
