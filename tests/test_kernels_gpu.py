@@ -163,6 +163,28 @@ def test_lm_head_ce_chunked_matches_one_pass(gpu_device):
     assert rel(g1[: V * d].view(V, d).cpu(), wr.grad) < 3e-2
 
 
+def test_lm_head_dx_tn_matches_nn(gpu_device, monkeypatch):
+    """The LM-head input gradient through the transposed weight copy (hipBLASLt TN layout, the default) equals
+    the NN call on the stored weight up to GEMM rounding, and both match the fp32 oracle."""
+    from bpe_transformer.ops import loss as L
+
+    V, d, M = 4096, 256, 512  # V, d multiples of 64: the TN path applies
+    torch.manual_seed(3)
+    w = (0.05 * torch.randn(V, d, device=gpu_device)).to(torch.bfloat16)
+    h0 = torch.randn(M, d, device=gpu_device, dtype=torch.bfloat16)
+    t = torch.randint(0, V, (M,), device=gpu_device)
+    dh = {}
+    for tn in (False, True):
+        monkeypatch.setattr(L, "_HEAD_DX_TN", tn)
+        h = h0.clone().requires_grad_(True)
+        ops.lm_head_cross_entropy(h, w, t).backward()
+        dh[tn] = h.grad.float()
+    assert rel(dh[True], dh[False]) < 1e-2
+    hr = h0.float().cpu().requires_grad_(True)
+    torch.nn.functional.cross_entropy(hr @ w.float().cpu().t(), t.cpu()).backward()
+    assert rel(dh[True].cpu(), hr.grad) < 3e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_embedding(gpu_device, dtype):
     torch.manual_seed(0)
