@@ -287,7 +287,8 @@ __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2
                                          0, 0);
 }
 
-// SPLIT (BPE_GPP_DMA_SPLIT=1): the second piece of each pair is issued by the same wave in its MFMA section,
+// SPLIT (spread mode 2, BPE_GPP_SPREAD; the default for the weight-gradient layout): the second piece of each
+// pair is issued by the same wave in its MFMA section,
 // between the two halves of the quadrant, so a load section carries one piece; the waits become vmcnt(3).
 template <bool AK, bool BKM, int DIAG, bool SPLIT = false>
 __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
