@@ -44,6 +44,29 @@ def test_loss_and_grads_match_oracle(gpu_device):
         assert e < 0.08, (n, float(e))
 
 
+@pytest.mark.parametrize("fuse", [False, True])
+def test_swiglu_forward_paths_match_oracle(gpu_device, monkeypatch, fuse):
+    """Both SwiGLU forward paths of the fused block -- the gate in the [W1;W3] GEMM epilogue (gemm_swiglu_fwd,
+    d_model <= 1024) and hipBLASLt + swiglu_fwd (wider models) -- against the fp32 oracle, with a batch whose
+    token count (2 x 128) meets the fused kernel's 256-row tiles."""
+    from bpe_transformer.models import fused_block
+
+    monkeypatch.setattr(fused_block, "_FUSE_SWIGLU_FWD", fuse)
+    probe = torch.empty(256, 256, device=gpu_device, dtype=torch.bfloat16)
+    assert fused_block._fuse_swiglu_fwd(probe, torch.empty(1024, 256, device=gpu_device, dtype=torch.bfloat16)) == fuse
+    ref, gpu = _pair(gpu_device)
+    ids = torch.randint(0, 1000, (2, 128))
+    tgt = torch.randint(0, 1000, (2, 128))
+    l_ref = ref.loss(ids, tgt)
+    l_ref.backward()
+    l_gpu = gpu.loss(ids.to(gpu_device), tgt.to(gpu_device))
+    l_gpu.backward()
+    assert abs(l_gpu.item() - l_ref.item()) < 3e-2
+    for (n, pr), (_, pg) in zip(ref.named_parameters(), gpu.named_parameters()):
+        e = (pg.grad.float().cpu() - pr.grad).norm() / pr.grad.norm().clamp_min(1e-12)
+        assert e < 0.08, (n, float(e))
+
+
 def test_main_grad_path_matches_autograd(gpu_device):
     """Fused blocks accumulating into the flat buffer (main_grad) == per-parameter autograd grads."""
     from bpe_transformer.optim.flat import FlatParameters
