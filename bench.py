@@ -70,6 +70,9 @@ def main() -> int:
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--zero", type=int, choices=[0, 1], default=0,
+                    help="1 = sharded data parallelism (reduce-scatter gradients, AdamW on 1/N of the parameters, "
+                         "weight all-gather overlapped with the next forward; parallel/zero.py); N>1 only")
     ap.add_argument("--gemm-tuning", default="auto",
                     help="hipBLASLt/rocBLAS solution table (TunableOp CSV) for the library GEMMs; 'auto' = the "
                          "shipped table for this model/batch if present, 'off' = library heuristics")
@@ -100,7 +103,8 @@ def main() -> int:
     model = TransformerLM.from_config(cfg, device=dev, dtype=dtype)
     if args.precision == "fp8":
         model.enable_fp8()
-    engine = TrainEngine(model, info, lr=3e-4, weight_decay=0.1, max_grad_norm=1.0, bucket_mb=args.bucket_mb)
+    engine = TrainEngine(model, info, lr=3e-4, weight_decay=0.1, max_grad_norm=1.0, bucket_mb=args.bucket_mb,
+                         zero=args.zero)
 
     # synthetic token stream, different per rank; batches staged on the device up front
     data = synthetic_tokens(cfg.vocab_size, args.batch * (args.seq + 1) * 8, seed=1000 + info.rank)
@@ -151,7 +155,7 @@ def main() -> int:
                      f"vocab {cfg.vocab_size})",
             "global_batch": args.batch * n,
             "seq_len": args.seq,
-            "parallelism": f"dp{n}",
+            "parallelism": f"dp{n}" + ("-zero1" if engine.zero else ""),
             "micro_batch_per_gpu": args.batch,
         },
         "mfu_bf16_dense_2.5PF": round(value / n * flops_tok / 2.5e15, 4),

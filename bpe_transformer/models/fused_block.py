@@ -295,10 +295,15 @@ def fused_block_forward(block, x: Tensor) -> Tensor:
     return (xm + g2).view(B, S, d)
 
 
-def fused_stack_forward(layers, ln_final, x: Tensor) -> Tensor:
-    """All blocks + the final RMSNorm with every residual add fused into the following norm."""
+def fused_stack_forward(layers, ln_final, x: Tensor, fence=None) -> Tensor:
+    """All blocks + the final RMSNorm with every residual add fused into the following norm.  ``fence``
+    (optional callable(module)) runs before each module's weights are read (sharded DP weight all-gathers)."""
     B, S, d = x.shape
     xr, xd = x.reshape(B * S, d).contiguous(), None
     for layer in layers:
+        if fence is not None:
+            fence(layer)
         xr, xd = fused_block_pair(layer, xr, xd, B, S)
+    if fence is not None:
+        fence(ln_final)
     return AddRMSNormFn.apply(xr, xd, ln_final.weight, ln_final.eps).view(B, S, d)

@@ -28,6 +28,15 @@ _VOCAB_PAD = int(os.environ.get("BPE_VOCAB_PAD", "256"))
 
 
 class TransformerLM(nn.Module):
+    # sharded data parallelism (parallel/zero.py) sets this to a callable(module) that waits for the in-flight
+    # all-gather of that module's weights; the forward calls it right before each module's weights are read
+    _bpe_param_fence = None
+
+    def _fence(self, module: nn.Module) -> None:
+        f = self._bpe_param_fence
+        if f is not None:
+            f(module)
+
     def __init__(
         self,
         vocab_size: int,
@@ -102,22 +111,32 @@ class TransformerLM(nn.Module):
 
     def hidden_states(self, in_indices: Tensor) -> Tensor:
         assert in_indices.shape[-1] <= self.context_length, "sequence longer than context_length"
+        fence = self._bpe_param_fence
+        if fence is not None:
+            fence(self.token_embeddings)
         x = self.token_embeddings(in_indices)
         if (_FUSED_STACK and len(self.layers) and x.dim() == 3
                 and all(layer._fused_ok(x) for layer in self.layers)):
             from .fused_block import fused_stack_forward
 
-            return fused_stack_forward(self.layers, self.ln_final, x)
+            return fused_stack_forward(self.layers, self.ln_final, x, fence)
         for layer in self.layers:
+            if fence is not None:
+                fence(layer)
             x = layer(x)
+        if fence is not None:
+            fence(self.ln_final)
         return self.ln_final(x)
 
     def forward(self, in_indices: Tensor) -> Tensor:
-        return self.lm_head(self.hidden_states(in_indices))
+        h = self.hidden_states(in_indices)
+        self._fence(self.lm_head)
+        return self.lm_head(h)
 
     def loss(self, in_indices: Tensor, targets: Tensor, ignore_index: int = ops.IGNORE_INDEX) -> Tensor:
         """Mean next-token cross-entropy; fused LM head + CE on the GPU."""
         h = self.hidden_states(in_indices)
+        self._fence(self.lm_head)
         return ops.lm_head_cross_entropy(h, self.lm_head.weight, targets, ignore_index)
 
     def load_reference_state_dict(self, state_dict: dict, strict: bool = True):
@@ -145,6 +164,7 @@ class TransformerLM(nn.Module):
         """
         squeeze = prompt.dim() == 1
         ids = prompt.unsqueeze(0) if squeeze else prompt
+        self._fence(self)  # the decode session packs / reads every weight up front
         if use_cache and ids.shape[1] + max_new_tokens <= self.context_length and max_new_tokens > 0:
             from .generation import DecodeSession
 

@@ -46,7 +46,10 @@ class Slot:
 
 
 class FlatParameters:
-    def __init__(self, named_params: list[tuple[str, nn.Parameter]], grad_dtype: torch.dtype | None = None):
+    def __init__(self, named_params: list[tuple[str, nn.Parameter]], grad_dtype: torch.dtype | None = None,
+                 pad_to: int = ALIGN):
+        """``pad_to``: the total length is rounded up to a multiple of it (zero tail; sharded data parallelism
+        needs buckets that split evenly over the ranks, ``parallel/zero.py``)."""
         assert named_params, "no parameters"
         dtypes = {p.dtype for _, p in named_params}
         devices = {p.device for _, p in named_params}
@@ -63,6 +66,7 @@ class FlatParameters:
             self.slots.append(Slot(name, p, off, n))
             reserve.append(r)
             off += (r + ALIGN - 1) // ALIGN * ALIGN
+        off = (off + pad_to - 1) // pad_to * pad_to
         self.numel = off
         self.data = torch.zeros(off, dtype=self.dtype, device=self.device)
         self.grad = torch.zeros(off, dtype=grad_dtype or self.dtype, device=self.device)
@@ -78,12 +82,13 @@ class FlatParameters:
                     s.param._bpe_padded_grad = self.grad[s.offset : s.offset + r].view(r // cols, cols)
 
     @classmethod
-    def from_module(cls, module: nn.Module, grad_dtype: torch.dtype | None = None) -> "FlatParameters":
+    def from_module(cls, module: nn.Module, grad_dtype: torch.dtype | None = None,
+                    pad_to: int = ALIGN) -> "FlatParameters":
         for m in module.modules():  # row padding requested on the module (survives deepcopy / .to())
             rows = getattr(m, "pad_rows", None)
             if rows and isinstance(getattr(m, "weight", None), nn.Parameter):
                 m.weight._bpe_pad_rows = rows
-        return cls([(n, p) for n, p in module.named_parameters() if p.requires_grad], grad_dtype)
+        return cls([(n, p) for n, p in module.named_parameters() if p.requires_grad], grad_dtype, pad_to)
 
     def zero_grad(self) -> None:
         self.grad.zero_()
@@ -121,6 +126,15 @@ class FlatAdamW:
         self.exp_avg = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
         self.exp_avg_sq = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
         self.weight_decay = weight_decay
+        self.shard: list[tuple[int, int]] | None = None  # element ranges this rank updates (ZeRO-1), None = all
+        self._build_segments()
+
+    def set_shard(self, ranges: list[tuple[int, int]] | None) -> None:
+        """Restrict :meth:`step` to the element ranges ``[s, e)`` this rank owns (sharded data parallelism,
+        ``parallel/zero.py``).  The moments and master weights stay full-size buffers -- at 288 GB of HBM the
+        point of sharding is the optimizer's time and HBM traffic, not capacity -- but only the owned ranges are
+        current; ``ShardedDataParallel.gather_optimizer_state`` makes all of them current on every rank (checkpoints)."""
+        self.shard = sorted(ranges) if ranges is not None else None
         self._build_segments()
 
     def _build_segments(self) -> None:
@@ -134,6 +148,9 @@ class FlatAdamW:
                 self.segments[-1] = (self.segments[-1][0], end, wd)
             else:
                 self.segments.append((s.offset, end, wd))
+        if self.shard is not None:  # intersect with the owned ranges: one launch per (segment, range) overlap
+            self.segments = [(max(a, s), min(b, e), wd) for a, b, wd in self.segments for s, e in self.shard
+                             if max(a, s) < min(b, e)]
 
     @property
     def step_count(self) -> int:
@@ -159,7 +176,8 @@ class FlatAdamW:
                 out[s:e] if out is not None else None, self.lr, b1, b2, self.eps, wd, 0, grad_scale, self.nstep,
             )
         if out is None and self.master is not self.flat.data:
-            self.flat.data.copy_(self.master)
+            for s, e in (self.shard or [(0, self.flat.numel)]):
+                self.flat.data[s:e].copy_(self.master[s:e])
 
     def state_dict(self) -> dict:
         return {

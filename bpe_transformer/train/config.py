@@ -60,6 +60,7 @@ class TrainConfig:
     phase_timing: bool = False  # log fwd / bwd / exposed-comm / optimizer ms (device events) at each log step
     nan_guard: bool = True
     ddp_check_every: int = 0  # >0: every N steps assert bit-identical grads / weights across DP ranks
+    zero: int = 0  # 1: sharded data parallelism (reduce-scatter + 1/N AdamW + all-gather, parallel/zero.py)
 
     def to_dict(self) -> dict:
         d = dataclasses.asdict(self)

@@ -19,8 +19,10 @@ from torch import Tensor, nn
 
 from ..ops import streams
 from ..optim.flat import FlatAdamW, FlatParameters
+from ..optim.flat import ALIGN
 from ..parallel.ddp import BucketedAllReduce
 from ..parallel.dist import DistInfo
+from ..parallel.zero import ShardedDataParallel
 
 
 class TrainEngine:
@@ -36,18 +38,34 @@ class TrainEngine:
         bucket_mb: float = 64.0,
         time_phases: bool = False,
         ddp_check_every: int = 0,
+        zero: int = 0,
     ):
         self.model = model
         self.dist = dist_info or DistInfo()
-        self.flat = FlatParameters.from_module(model)
+        # zero=1: sharded data parallelism (parallel/zero.py) -- reduce-scatter, 1/N of the AdamW work,
+        # all-gather of the weights overlapped with the next forward
+        self.zero = int(zero) if self.dist.world_size > 1 else 0
+        pad = self.dist.world_size * ALIGN if self.zero else ALIGN
+        self.flat = FlatParameters.from_module(model, pad_to=pad)
         for slot in self.flat.slots:  # fused blocks accumulate weight grads straight into the flat buffer
             slot.param.main_grad = self.flat.grad_view(slot).view_as(slot.param)
         self.opt = FlatAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         self.max_grad_norm = max_grad_norm
-        self.ddp = BucketedAllReduce(self.flat, bucket_mb=bucket_mb) if self.dist.world_size > 1 else None
+        self.ddp = None
+        if self.dist.world_size > 1:
+            self.ddp = (ShardedDataParallel(self.flat, bucket_mb=bucket_mb) if self.zero
+                        else BucketedAllReduce(self.flat, bucket_mb=bucket_mb))
         if self.ddp is not None:
             self.ddp.broadcast_parameters(0)
             self.opt.master.copy_(self.flat.data)  # keep fp32 master == broadcast weights
+        self._fenced = False
+        if self.zero:
+            self.opt.set_shard(self.ddp.shard_ranges())
+            # the model waits for each module's weight all-gather right before reading it; a model without
+            # that hook waits for all of them at the start of the next step instead
+            if hasattr(model, "_bpe_param_fence"):
+                model._bpe_param_fence = self.ddp.wait_params
+                self._fenced = True
         self.last_grad_norm: Tensor | None = None
         # DP race / divergence detector: every N steps compare per-bucket gradient and weight checksums across
         # ranks (parallel/ddp.py check_consistency; raises on mismatch)
@@ -85,6 +103,8 @@ class TrainEngine:
         """
         self.model.train()
         self._mark("start")
+        if self.zero and not self._fenced:
+            self.ddp.wait_all_params()
         self.flat.grad.zero_()
         n = len(batches)
         total = None
@@ -110,9 +130,14 @@ class TrainEngine:
         self._mark("comm")
         coef = None
         if self.max_grad_norm is not None and self.max_grad_norm > 0:
-            norm, coef = self.opt.clip_grad_norm(self.max_grad_norm)
+            if self.zero:
+                norm, coef = self.ddp.clip_coef(self.max_grad_norm)
+            else:
+                norm, coef = self.opt.clip_grad_norm(self.max_grad_norm)
             self.last_grad_norm = norm
         self.opt.step(lr, coef)
+        if self.zero:
+            self.ddp.gather_params()  # waited per module by the next forward (or sync_params)
         if check:
             self.ddp.check_consistency("data")
         self.steps_done += 1
@@ -124,6 +149,18 @@ class TrainEngine:
                 torch.distributed.all_reduce(fp8.amax, op=torch.distributed.ReduceOp.MAX)
             fp8.update()
         return total / n if n > 1 else total
+
+    def sync_params(self) -> None:
+        """Wait for in-flight weight all-gathers (sharded DP); call before reading the weights outside a
+        forward (evaluation through other code paths, checkpoints, comparisons).  No-op otherwise."""
+        if self.zero:
+            self.ddp.wait_all_params()
+
+    def gather_optimizer_state(self) -> None:
+        """Collective on every rank (sharded DP): make the full optimizer state current before a checkpoint.
+        No-op otherwise."""
+        if self.zero:
+            self.ddp.gather_optimizer_state(self.opt)
 
     def state_dict(self) -> dict:
         return self.opt.state_dict()

@@ -65,7 +65,7 @@ class Trainer:
         self.engine = TrainEngine(self.model, self.info, lr=o.lr, betas=o.betas, eps=o.eps,
                                   weight_decay=o.weight_decay, max_grad_norm=o.max_grad_norm,
                                   bucket_mb=cfg.bucket_mb, time_phases=cfg.phase_timing,
-                                  ddp_check_every=cfg.ddp_check_every)
+                                  ddp_check_every=cfg.ddp_check_every, zero=cfg.zero)
         self.schedule = CosineSchedule(o.lr, o.min_lr, o.warmup_iters, o.cosine_cycle_iters or cfg.max_iters)
         ctx = cfg.model.context_length
         if cfg.data.train_path:
@@ -87,6 +87,10 @@ class Trainer:
         return Path(self.cfg.ckpt_dir) / f"ckpt_{it:08d}.pt"
 
     def save(self, it: int) -> None:
+        # sharded DP: every rank joins the collectives that make the weights and the full optimizer state
+        # current on rank 0 (no-ops otherwise)
+        self.engine.sync_params()
+        self.engine.gather_optimizer_state()
         extra = {"rng": {"torch": torch.get_rng_state(),
                          "cuda": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else []}}
         if self.model.fp8_state is not None:
@@ -130,6 +134,7 @@ class Trainer:
         from ..data import get_batch
 
         tot = torch.zeros((), device=self.info.device)
+        self.engine.sync_params()
         for _ in range(self.cfg.eval_iters):
             x, y = get_batch(data, self.cfg.batch_size, self.cfg.model.context_length, self.info.device, rng)
             tot += self.model.loss(x, y).float()

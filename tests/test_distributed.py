@@ -164,7 +164,8 @@ def test_ddp_consistency_check_detects_divergence():
 
 
 
-def test_bench_contract_two_ranks_cpu(tmp_path):
+@pytest.mark.parametrize("zero", [0, 1])
+def test_bench_contract_two_ranks_cpu(tmp_path, zero):
     """bench.py under torch.distributed.run with 2 ranks (gloo, CPU plumbing config) prints exactly one JSON line,
     from rank 0, with the whole-job numbers the driver's scaling run reads (n_gpus, dp2, global batch)."""
     import json
@@ -180,7 +181,7 @@ def test_bench_contract_two_ranks_cpu(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
            "--gpus", "2", "--device", "cpu", "--model", "tinystories-17m", "--seq", "32", "--batch", "2",
-           "--steps", "2", "--warmup", "1"]
+           "--steps", "2", "--warmup", "1", "--zero", str(zero)]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -188,5 +189,5 @@ def test_bench_contract_two_ranks_cpu(tmp_path):
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1 and out["scaling"] == "weak"
-    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    assert out["config"]["parallelism"] == ("dp2-zero1" if zero else "dp2") and out["config"]["global_batch"] == 4
     assert out["value"] > 0 and abs(out["value"] - 2 * 2 * 2 * 32 / (out["ms_per_step"] * 2 / 1000)) < 0.02 * out["value"]
