@@ -44,7 +44,9 @@ class TrainEngine:
         self.dist = dist_info or DistInfo()
         # zero=1: sharded data parallelism (parallel/zero.py) -- reduce-scatter, 1/N of the AdamW work,
         # all-gather of the weights overlapped with the next forward
-        self.zero = int(zero) if self.dist.world_size > 1 else 0
+        # (a one-rank job gets the sharded path only inside an explicitly initialised process group: tests of
+        # the RCCL calls on one GPU)
+        self.zero = int(zero) if (self.dist.world_size > 1 or (zero and torch.distributed.is_initialized())) else 0
         pad = self.dist.world_size * ALIGN if self.zero else ALIGN
         self.flat = FlatParameters.from_module(model, pad_to=pad)
         for slot in self.flat.slots:  # fused blocks accumulate weight grads straight into the flat buffer
@@ -52,7 +54,7 @@ class TrainEngine:
         self.opt = FlatAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         self.max_grad_norm = max_grad_norm
         self.ddp = None
-        if self.dist.world_size > 1:
+        if self.dist.world_size > 1 or self.zero:
             self.ddp = (ShardedDataParallel(self.flat, bucket_mb=bucket_mb) if self.zero
                         else BucketedAllReduce(self.flat, bucket_mb=bucket_mb))
         if self.ddp is not None:

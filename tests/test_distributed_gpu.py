@@ -54,7 +54,8 @@ def _worker(rank, world, port, bucket_mb, side, out_q):
     g1 = eng.flat.grad.float().cpu()
     eng.train_step([_batch(rank, info.device)])
     torch.cuda.synchronize()
-    out_q.put((rank, g1, eng.flat.data.float().cpu(), len(eng.ddp.buckets)))
+    # numpy copies travel by value; torch tensors go through fd sharing whose listener dies with this process
+    out_q.put((rank, g1.numpy().copy(), eng.flat.data.float().cpu().numpy().copy(), len(eng.ddp.buckets)))
     cleanup()
 
 
@@ -67,7 +68,7 @@ def test_dp2_gpu(gpu_device, bucket_mb, side):
     procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, side, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = {r: (g, d, nb) for r, g, d, nb in (q.get(timeout=240) for _ in range(world))}
+    res = {r: (torch.from_numpy(g), torch.from_numpy(d), nb) for r, g, d, nb in (q.get(timeout=240) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -102,7 +103,7 @@ def _zero_worker(rank, world, port, side, out_q):
             eng.train_step([_batch(rank, info.device)])
         eng.sync_params()
         torch.cuda.synchronize()
-        out.append((eng.flat.data.float().cpu(), float(eng.last_grad_norm), len(eng.ddp.buckets)))
+        out.append((eng.flat.data.float().cpu().numpy().copy(), float(eng.last_grad_norm), len(eng.ddp.buckets)))
         eng.ddp.remove_hooks()
     out_q.put((rank, out))
     cleanup()
@@ -124,10 +125,55 @@ def test_zero1_gpu(gpu_device, side):
         p.join(timeout=60)
         assert p.exitcode == 0
     (d0, n0, _), (z0, nz, nb) = res[0]
+    d0, z0 = torch.from_numpy(d0), torch.from_numpy(z0)
     assert nb > 2
-    assert torch.equal(res[0][1][0], res[1][1][0]), "sharded ranks diverged"
+    assert (res[0][1][0] == res[1][1][0]).all(), "sharded ranks diverged"
     assert abs(n0 - nz) <= 1e-3 * n0
     m = min(d0.numel(), z0.numel())
     err = float((z0[:m] - d0[:m]).abs().max())
     assert err < 2e-2, err
     assert float((z0[:m] != d0[:m]).float().mean()) < 0.01
+
+
+def _nccl_zero_worker(port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from bpe_transformer.parallel.dist import DistInfo
+    from bpe_transformer.train.engine import TrainEngine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    info = DistInfo(0, 1, 0, dev, "nccl")
+    out = []
+    for zero in (0, 1):
+        eng = TrainEngine(_model(dev), info if zero else None, lr=1e-3, weight_decay=0.1, max_grad_norm=1.0,
+                          bucket_mb=0.25, zero=zero)
+        for _ in range(2):
+            eng.train_step([_batch(0, dev)])
+        eng.sync_params()
+        torch.cuda.synchronize()
+        out.append((eng.flat.data.float().cpu().numpy().copy(), float(eng.last_grad_norm),
+                    len(eng.ddp.buckets) if eng.ddp is not None else 0))
+    dist.destroy_process_group()
+    out_q.put(out)
+
+
+def test_zero1_rccl_calls_one_rank(gpu_device):
+    """The RCCL side of sharded DP on one GPU (a one-rank nccl group): the in-place reduce_scatter_tensor /
+    all_gather_into_tensor on flat-buffer views and the scalar norm all-reduce are accepted by the backend and
+    the engine trains exactly like the single-process one (the 8-GPU data movement is the driver's run)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_zero_worker, args=(_free_port(), q))
+    p.start()
+    (d0, n0, _), (z0, nz, nb) = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert nb > 2
+    assert abs(n0 - nz) <= 1e-3 * n0
+    m = min(d0.shape[0], z0.shape[0])
+    d0, z0 = torch.from_numpy(d0[:m]), torch.from_numpy(z0[:m])
+    assert float((z0 - d0).abs().max()) < 2e-2
+    assert float((z0 != d0).float().mean()) < 0.01
