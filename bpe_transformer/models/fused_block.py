@@ -90,6 +90,10 @@ def _fuse_swiglu_fwd(x: Tensor, w13: Tensor) -> bool:
 
 _DX_TN = os.environ.get("BPE_DX_TN", "1") == "1"
 
+# the attention forward zeroes the backward's fp32 dQ accumulator in its epilogue instead of the backward
+# pre-pass doing it (``BPE_FA_DQ_FWD_ZERO=0`` restores the pre-pass; docs/performance.md, attention)
+_DQ_FWD_ZERO = os.environ.get("BPE_FA_DQ_FWD_ZERO", "1") == "1"
+
 
 def _dx_tn(w: Tensor) -> bool:
     """Run dX = dY . W as dY . (W^T)^T with W^T materialised (``ops.transpose_bf16``): hipBLASLt's TN layout
@@ -143,7 +147,12 @@ class FusedBlockFn(torch.autograd.Function):
         if pre:  # RoPE once, in place on Q / K of the QKV activation (saved rotated for the backward)
             hip().rope_qk_(qkv, cos, sin, B, S, H, Hkv, D)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
-        o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, pre)
+        # training: the forward kernel zeroes the backward's fp32 dQ accumulator in its epilogue (hidden under
+        # its compute; the backward pre-pass then only reads O / dO)
+        dq_acc = (torch.empty(B * ((S + 63) // 64 * 64), H * D, device=q.device, dtype=torch.float32)
+                  if _DQ_FWD_ZERO and any(ctx.needs_input_grad) else None)
+        o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, pre, dq_acc)
+        ctx.dq_acc = dq_acc
         g1 = mm(o, wo.detach(), 1) if fp8 is not None else torch.matmul(o, wo.t())
         xm, h2, r2 = hip().add_rmsnorm_fwd(x2, g1, ln2, eps)
         if fp8 is None and _fuse_swiglu_fwd(h2, w_13):
@@ -231,7 +240,9 @@ class FusedBlockFn(torch.autograd.Function):
         acc_weight([wo], dxm, o)
         do = dx(dxm, [wo], 1)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
-        dqkv = hip().fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, ctx.prerotated)
+        dqkv = hip().fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, ctx.prerotated,
+                            ctx.dq_acc)
+        ctx.dq_acc = None
         acc_weight([wq, wk, wv], dqkv, h1)
         dh1 = dx(dqkv, [wq, wk, wv], 0)
         dx2, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm)

@@ -55,8 +55,8 @@ __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const __bf16* __restric
                                                          const __bf16* __restrict__ dO, long ld_do,
                                                          float* __restrict__ delta, float* __restrict__ dq_acc,
                                                          int B, int H, int S, int spad) {
-    // one row per (b, s < spad, h): delta = rowsum(O * dO) for s < S, and the row's fp32 dQ accumulator
-    // zeroed (replaces a separate memset; pad rows s >= S only get the zeros)
+    // one row per (b, s < spad, h): delta = rowsum(O * dO) for s < S, and -- unless the forward already did
+    // (dq_acc == nullptr) -- the row's fp32 dQ accumulator zeroed (pad rows s >= S only get the zeros)
     constexpr int LPR = D / 8;
     const long row = ((long)blockIdx.x * 256 + threadIdx.x) / LPR;
     const int sub = threadIdx.x % LPR;
@@ -70,9 +70,11 @@ __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const __bf16* __restric
         h = (int)(row % H);
         b = bsp / spad;
         s = (int)(bsp % spad);
-        float4* z = reinterpret_cast<float4*>(dq_acc + row * D + sub * 8);
-        z[0] = float4{0.f, 0.f, 0.f, 0.f};
-        z[1] = float4{0.f, 0.f, 0.f, 0.f};
+        if (dq_acc != nullptr) {
+            float4* z = reinterpret_cast<float4*>(dq_acc + row * D + sub * 8);
+            z[0] = float4{0.f, 0.f, 0.f, 0.f};
+            z[1] = float4{0.f, 0.f, 0.f, 0.f};
+        }
     }
     const bool ok = in && s < S;
     if (ok) {
@@ -513,8 +515,8 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
         const int spad = (a.S + 63) & ~63;  // dq_acc is [B][spad][H][D] fp32
         const long rows = (long)a.B * spad * a.H;
         const long threads = rows * (D / 8);
-        fa_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(a.o, a.ld_o, a.dout, a.ld_do, a.delta,
-                                                                               a.dq_acc, a.B, a.H, a.S, spad);
+        fa_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
+            a.o, a.ld_o, a.dout, a.ld_do, a.delta, a.dq_zeroed ? nullptr : a.dq_acc, a.B, a.H, a.S, spad);
     }
     constexpr int dbg = 0;
     {

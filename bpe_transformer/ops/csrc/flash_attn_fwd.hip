@@ -49,7 +49,8 @@ template <int D, bool CAUSAL, bool ROPE>
 __global__ void __launch_bounds__(256, 2)
 fa_fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv, long ld_q,
               long ld_kv, __bf16* __restrict__ O, long ld_o, float* __restrict__ LSE, const float* __restrict__ cosT,
-              const float* __restrict__ sinT, int B, int H, int Hkv, int S, float scale_log2, int group) {
+              const float* __restrict__ sinT, int B, int H, int Hkv, int S, float scale_log2, int group,
+              float* __restrict__ DQZ) {
     constexpr int RB = D * 2;            // bytes per LDS row
     constexpr int CPR = D / 8;           // 16-byte chunks per row
     constexpr int TILE = 64 * RB;        // bytes per 64-row tile
@@ -245,6 +246,19 @@ fa_fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                 *reinterpret_cast<u16x4*>(op + dt * 32 + 8 * i + 4 * hh) = t;
             }
         if (hh == 0) LSE[((long)b * H + h) * S + qrow] = (l_run > 0.f) ? m_run + __log2f(l_run) : INFINITY;
+    }
+    // training: zero this block's rows of the backward's fp32 dQ accumulator ([B][Spad][H][D], rows padded to
+    // 64), after every other store -- fire-and-forget stores under a compute-bound kernel replace the zeroing
+    // pass of fa_bwd_pre_kernel (one 4 x [tokens, H*D]-byte HBM write per layer).  Blocks cover [0, Spad).
+    if (DQZ != nullptr) {
+        constexpr int C4 = D / 4;
+        const int spad = (S + 63) & ~63;
+        const int rows = min(128, spad - q0);
+        float* zb = DQZ + ((long)b * spad + q0) * ((long)H * D) + (long)h * D;
+        for (int e = tid; e < rows * C4; e += 256) {
+            const int r = e / C4, c = e % C4;
+            *reinterpret_cast<float4*>(zb + (long)r * H * D + 4 * c) = float4{0.f, 0.f, 0.f, 0.f};
+        }
     }
 }
 
@@ -496,7 +510,8 @@ template <int D, bool C, bool R>
 static void fwd_launch(const FaArgs& a, hipStream_t s) {
     const int nqb = (a.S + 127) / 128;
     fa_fwd_kernel<D, C, R><<<nqb * a.B * a.H, 256, fa_fwd_lds_bytes(D), s>>>(
-        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.lse, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, fa_group(a.B * a.H));
+        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.lse, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, fa_group(a.B * a.H),
+        a.dq_acc);
 }
 
 template <bool C>
@@ -520,6 +535,8 @@ void launch_fa_fwd(const FaArgs& a, hipStream_t s) {
     // rope 2 = Q / K already rotated: no RoPE inside the kernel
     if (a.D == 64 && a.rope != 1 && fwd_v3_enabled()) {
         if (a.causal) fwd_v3_launch<true>(a, s); else fwd_v3_launch<false>(a, s);
+        if (a.dq_acc != nullptr)  // v3 has no zeroing epilogue
+            (void)hipMemsetAsync(a.dq_acc, 0, (size_t)a.B * ((a.S + 63) & ~63) * a.H * a.D * sizeof(float), s);
         return;
     }
     const bool r = a.rope == 1;

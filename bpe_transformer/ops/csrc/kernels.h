@@ -99,7 +99,8 @@ struct FaArgs {
     const __bf16* dout;
     long ld_do;
     float* delta;   // [B, H, S] scratch
-    float* dq_acc;  // [B, S, H, D] fp32 scratch
+    float* dq_acc;  // [B, Spad, H, D] fp32 scratch (forward: zeroed there when non-null)
+    int dq_zeroed;  // backward: dq_acc arrives zeroed (by the forward), the pre-kernel skips it
     __bf16* dq;
     long ld_dq;
     __bf16* dk;

@@ -491,10 +491,18 @@ void rope_qk_(at::Tensor qkv, const at::Tensor& cos, const at::Tensor& sin, int6
                    (int)H, (int)Hkv, (int)D, cur_stream());
 }
 
+// the fp32 dQ accumulator shared by fa_fwd (zeroes it) and fa_bwd: [B * Spad, H * D], Spad = S rounded up to 64
+void check_dq_acc(const at::Tensor& t, const at::Tensor& q, int64_t B, int64_t S, int64_t H, int64_t D) {
+    check_cuda(t, "dq_acc");
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous() && t.dim() == 2 &&
+                    t.size(0) == B * ((S + 63) / 64 * 64) && t.size(1) == H * D && t.device() == q.device(),
+                "flash attention: dq_acc must be a contiguous fp32 [B * round_up(S, 64), H * D] tensor on q's device");
+}
+
 std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                           const at::Tensor& cos, const at::Tensor& sin, int64_t B, int64_t S, int64_t H,
                                           int64_t Hkv, int64_t D, bool causal, bool use_rope, double scale,
-                                          bool prerotated) {
+                                          bool prerotated, const c10::optional<at::Tensor>& dq_acc) {
     TORCH_CHECK(D == 64 || D == 128, "flash attention: head dim must be 64 or 128");
     TORCH_CHECK(H % Hkv == 0, "flash attention: H must be a multiple of Hkv");
     check_qkv(q, B * S, H * D, "q");
@@ -515,6 +523,10 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
     a.cos = fused_rope ? cos.data_ptr<float>() : nullptr; a.sin = fused_rope ? sin.data_ptr<float>() : nullptr;
     a.B = (int)B; a.H = (int)H; a.Hkv = (int)Hkv; a.S = (int)S; a.D = (int)D;
     a.causal = causal; a.rope = use_rope ? (prerotated ? 2 : 1) : 0; a.scale = (float)scale;
+    if (dq_acc.has_value() && dq_acc->defined()) {  // training: the forward zeroes the backward's dQ accumulator
+        check_dq_acc(*dq_acc, q, B, S, H, D);
+        a.dq_acc = dq_acc->data_ptr<float>();
+    }
     launch_fa_fwd(a, cur_stream());
     return {o, lse};
 }
@@ -523,7 +535,7 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
 at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                   const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cos, const at::Tensor& sin, int64_t B,
                   int64_t S, int64_t H, int64_t Hkv, int64_t D, bool causal, bool use_rope, double scale,
-                  bool prerotated) {
+                  bool prerotated, const c10::optional<at::Tensor>& dq_acc_in) {
     TORCH_CHECK(D == 64 || D == 128, "flash attention: head dim must be 64 or 128");
     TORCH_CHECK(Hkv > 0 && H % Hkv == 0, "flash attention: H must be a multiple of Hkv");
     if (use_rope)
@@ -539,7 +551,10 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     const int64_t W = (H + 2 * Hkv) * D;
     auto dqkv = at::empty({B * S, W}, q.options());
     auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-    auto dq_acc = at::empty({B * ((S + 63) / 64 * 64), H * D}, q.options().dtype(at::kFloat));  // rows padded
+    // rows padded to 64 per batch; zeroed by the forward when it was handed this buffer (fa_fwd dq_acc)
+    const bool pre_zeroed = dq_acc_in.has_value() && dq_acc_in->defined();
+    if (pre_zeroed) check_dq_acc(*dq_acc_in, q, B, S, H, D);
+    auto dq_acc = pre_zeroed ? *dq_acc_in : at::empty({B * ((S + 63) / 64 * 64), H * D}, q.options().dtype(at::kFloat));
     at::Tensor dkv_part;
     if (Hkv < H) dkv_part = at::empty({B * S, H * 2 * D}, q.options().dtype(at::kFloat));
     FaArgs a{};
@@ -550,7 +565,7 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     a.B = (int)B; a.H = (int)H; a.Hkv = (int)Hkv; a.S = (int)S; a.D = (int)D;
     a.causal = causal; a.rope = use_rope ? (prerotated ? 2 : 1) : 0; a.scale = (float)scale;
     a.dout = (const __bf16*)d.data_ptr(); a.ld_do = d.stride(0);
-    a.delta = delta.data_ptr<float>(); a.dq_acc = dq_acc.data_ptr<float>();
+    a.delta = delta.data_ptr<float>(); a.dq_acc = dq_acc.data_ptr<float>(); a.dq_zeroed = pre_zeroed ? 1 : 0;
     __bf16* base = (__bf16*)dqkv.data_ptr();
     a.dq = base; a.ld_dq = W;
     a.dk = base + H * D; a.dv = base + (H + Hkv) * D; a.ld_dkv = W;
@@ -777,9 +792,10 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("softmax_bwd(Tensor dy, Tensor y) -> Tensor");
     m.def("rope(Tensor x, Tensor pos, Tensor cos, Tensor sin, bool inverse) -> Tensor");
     m.def("fa_fwd(Tensor q, Tensor k, Tensor v, Tensor cos, Tensor sin, int B, int S, int H, int Hkv, int D, "
-          "bool causal, bool rope, float scale, bool prerotated=False) -> (Tensor, Tensor)");
+          "bool causal, bool rope, float scale, bool prerotated=False, Tensor? dq_acc=None) -> (Tensor, Tensor)");
     m.def("fa_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor cos, Tensor sin, int B, "
-          "int S, int H, int Hkv, int D, bool causal, bool rope, float scale, bool prerotated=False) -> Tensor");
+          "int S, int H, int Hkv, int D, bool causal, bool rope, float scale, bool prerotated=False, "
+          "Tensor? dq_acc=None) -> Tensor");
     m.def("rope_qk_(Tensor(a!) qkv, Tensor cos, Tensor sin, int B, int S, int H, int Hkv, int D) -> ()");
 }
 

@@ -485,6 +485,32 @@ def test_flash_attention_gpt2_shape(gpu_device):
     assert rel(g.cpu(), gr) < 3e-2
 
 
+@pytest.mark.parametrize("S,D,H,Hkv,fused", [(1000, 64, 4, 4, False), (192, 128, 8, 4, True), (64, 64, 4, 2, True),
+                                              (320, 64, 4, 4, True)])
+def test_flash_dq_acc_zeroed_by_forward(gpu_device, S, D, H, Hkv, fused):
+    """fa_fwd handed the backward's fp32 dQ accumulator (filled with NaN here) zeroes every row of it,
+    padding included, and fa_bwd then skips its own zeroing: the gradients equal those of the path where the
+    backward pre-pass zeroes (the fused blocks use this form) -- dK / dV bitwise, dQ up to the order of its fp32
+    atomics."""
+    torch.manual_seed(5)
+    B = 2
+    h = torch.ops.bpe_hip
+    qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device=gpu_device, dtype=torch.bfloat16)
+    cos, sin = R.rope_tables(D, S + 3, 10000.0, device=gpu_device)
+    q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
+    scale = D ** -0.5
+    acc = torch.full((B * ((S + 63) // 64 * 64), H * D), float("nan"), device=gpu_device)
+    o, lse = h.fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, True, scale, not fused, acc)
+    assert bool((acc == 0).all()), "forward left rows of the dQ accumulator unzeroed"
+    o2, lse2 = h.fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, True, scale, not fused)
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+    do = torch.randn_like(o)
+    ref = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, True, scale, not fused)
+    got = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, True, scale, not fused, acc)
+    assert torch.equal(got[:, H * D :], ref[:, H * D :])  # dK / dV: no atomics, bitwise
+    assert rel(got[:, : H * D].cpu(), ref[:, : H * D].float().cpu()) < 1e-3  # dQ: fp32 atomics, order varies
+
+
 def test_rope_qk_inplace(gpu_device):
     """rope_qk_ rotates exactly the Q and K heads of the fused activation (positions restart per sequence)."""
     torch.manual_seed(4)
