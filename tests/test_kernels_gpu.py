@@ -250,6 +250,28 @@ def test_adamw_matches_torch(gpu_device):
     assert rel(p1.detach(), p2.detach()) < 1e-5
 
 
+@pytest.mark.parametrize("n,gdtype", [(1_000_005, torch.bfloat16), (4099, torch.float32), (7, torch.bfloat16)])
+def test_fused_adamw_kernel_vs_cpu(gpu_device, n, gdtype):
+    """The 8-wide AdamW kernel (ragged tail < 8, bf16 or fp32 gradients, clip coefficient, bf16 copy-out) vs
+    the same update computed by the CPU path of ops.fused_adamw_step."""
+    from bpe_transformer.ops.optim import fused_adamw_step
+
+    torch.manual_seed(2)
+    p = torch.randn(n)
+    m = 0.1 * torch.randn(n)
+    v = 0.01 * torch.rand(n)
+    g = torch.randn(n).to(gdtype)
+    scale = torch.tensor(0.5)
+    ref = [t.clone() for t in (p, m, v)]
+    fused_adamw_step(*ref, g, None, 1e-3, 0.9, 0.95, 1e-8, 0.1, 3, scale)
+    gp, gm, gv = (t.to(gpu_device) for t in (p, m, v))
+    out = torch.empty(n, device=gpu_device, dtype=torch.bfloat16)
+    fused_adamw_step(gp, gm, gv, g.to(gpu_device), out, 1e-3, 0.9, 0.95, 1e-8, 0.1, 3, scale.to(gpu_device))
+    for a, b in zip((gp, gm, gv), ref):
+        torch.testing.assert_close(a.cpu(), b, rtol=1e-5, atol=1e-7)
+    assert torch.equal(out.cpu(), gp.cpu().to(torch.bfloat16))
+
+
 def test_flat_adamw_bf16_master(gpu_device):
     from bpe_transformer.optim import FlatAdamW, FlatParameters
 
