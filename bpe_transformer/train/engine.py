@@ -61,6 +61,7 @@ class TrainEngine:
             self.ddp.broadcast_parameters(0)
             self.opt.master.copy_(self.flat.data)  # keep fp32 master == broadcast weights
         self._fenced = False
+        self._opt_state_current = True  # sharded DP: False from a step until gather_optimizer_state()
         if self.zero:
             self.opt.set_shard(self.ddp.shard_ranges())
             # the model waits for each module's weight all-gather right before reading it; a model without
@@ -140,6 +141,7 @@ class TrainEngine:
         self.opt.step(lr, coef)
         if self.zero:
             self.ddp.gather_params()  # waited per module by the next forward (or sync_params)
+            self._opt_state_current = False
         if check:
             self.ddp.check_consistency("data")
         self.steps_done += 1
@@ -163,8 +165,12 @@ class TrainEngine:
         No-op otherwise."""
         if self.zero:
             self.ddp.gather_optimizer_state(self.opt)
+            self._opt_state_current = True
 
     def state_dict(self) -> dict:
+        if not self._opt_state_current:
+            raise RuntimeError("sharded data parallelism: only this rank's pieces of the optimizer state are "
+                               "current; call gather_optimizer_state() on every rank before state_dict()")
         return self.opt.state_dict()
 
     def load_state_dict(self, sd: dict) -> None:

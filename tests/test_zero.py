@@ -53,6 +53,12 @@ def _worker(rank, world, port, zero, accum, bucket_mb, out_q):
         eng.train_step([_batch(rank, step, m) for m in range(accum)])
         norms.append(float(eng.last_grad_norm))
     eng.sync_params()
+    if zero:
+        try:
+            eng.state_dict()
+            raise AssertionError("state_dict() must refuse stale sharded optimizer state")
+        except RuntimeError:
+            pass
     eng.gather_optimizer_state()
     sd = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in eng.state_dict().items()}
     nb = len(eng.ddp.buckets)
