@@ -103,8 +103,10 @@ def main() -> int:
     model = TransformerLM.from_config(cfg, device=dev, dtype=dtype)
     if args.precision == "fp8":
         model.enable_fp8()
+    # phase timing: device events around forward / backward / exposed collective wait / clip + AdamW, read once
+    # after the timed loop (stderr; the driver's scaling run then shows how much all-reduce stays exposed)
     engine = TrainEngine(model, info, lr=3e-4, weight_decay=0.1, max_grad_norm=1.0, bucket_mb=args.bucket_mb,
-                         zero=args.zero)
+                         zero=args.zero, time_phases=on_gpu)
 
     # synthetic token stream, different per rank; batches staged on the device up front
     data = synthetic_tokens(cfg.vocab_size, args.batch * (args.seq + 1) * 8, seed=1000 + info.rank)
@@ -119,6 +121,7 @@ def main() -> int:
     for i in range(args.warmup):
         engine.train_step(batch(i))
     sync()
+    engine.phase_times()  # drop the warmup steps' events
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -130,6 +133,7 @@ def main() -> int:
     sync()
     dt = time.perf_counter() - t0
     dt = all_reduce_max(dt, dev)
+    phases = {k: round(all_reduce_max(v, dev), 3) for k, v in sorted(engine.phase_times().items())}
     loss_v = float(loss.item()) if loss is not None else float("nan")
 
     n = info.world_size
@@ -167,6 +171,8 @@ def main() -> int:
 
         out["dw_gemm_routes"] = _gemm.routes_summary()  # weight-gradient kernel per shape (ops/tuning/dw_routes.json)
     if info.is_main:
+        if phases:  # max over ranks of each phase's mean ms per step (comm_ms = exposed collective wait)
+            print(json.dumps({"phases_ms_per_step_max_over_ranks": phases}), file=sys.stderr, flush=True)
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:
