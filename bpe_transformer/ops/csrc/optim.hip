@@ -73,9 +73,11 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float
     const size_t n4 = n / 4;
     const size_t stride = (size_t)gridDim.x * 256;
     for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += stride) {
-        f32x4 pv = *reinterpret_cast<f32x4*>(p + 4 * i);
-        f32x4 mv = *reinterpret_cast<f32x4*>(m + 4 * i);
-        f32x4 vv = *reinterpret_cast<f32x4*>(v + 4 * i);
+        // every optimizer stream is touched once per step: non-temporal accesses keep them from allocating in
+        // (and later evicting through) the L2
+        f32x4 pv = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(p + 4 * i));
+        f32x4 mv = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(m + 4 * i));
+        f32x4 vv = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(v + 4 * i));
         float gv[4];
         G4<GT>::load(g + 4 * i, gv);
 #pragma unroll
@@ -84,9 +86,9 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float
             adam_one(pj, mj, vj, gv[j] * sc, a);
             pv[j] = pj; mv[j] = mj; vv[j] = vj;
         }
-        *reinterpret_cast<f32x4*>(p + 4 * i) = pv;
-        *reinterpret_cast<f32x4*>(m + 4 * i) = mv;
-        *reinterpret_cast<f32x4*>(v + 4 * i) = vv;
+        __builtin_nontemporal_store(pv, reinterpret_cast<f32x4*>(p + 4 * i));
+        __builtin_nontemporal_store(mv, reinterpret_cast<f32x4*>(m + 4 * i));
+        __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v + 4 * i));
         if (pout) {
             u16x4 o = {f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3])};
             *reinterpret_cast<u16x4*>(pout + 4 * i) = o;
