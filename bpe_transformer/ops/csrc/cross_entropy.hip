@@ -111,6 +111,10 @@ template <typename T>
 __device__ __forceinline__ float raw_get(const typename RawVec<T>::type& r, int j);
 template <> __device__ __forceinline__ float raw_get<__bf16>(const u16x8& r, int j) { return bf2f(r[j]); }
 template <> __device__ __forceinline__ float raw_get<float>(const f32x4& r, int j) { return r[j]; }
+template <typename T>
+__device__ __forceinline__ void raw_set(typename RawVec<T>::type& r, int j, float v);
+template <> __device__ __forceinline__ void raw_set<__bf16>(u16x8& r, int j, float v) { r[j] = f2bf(v); }
+template <> __device__ __forceinline__ void raw_set<float>(f32x4& r, int j, float v) { r[j] = v; }
 
 template <typename T, int MAXV>
 __global__ void __launch_bounds__(512) ce_fwd_bwd_reg_kernel(T* __restrict__ logits, long ld,
@@ -137,7 +141,7 @@ __global__ void __launch_bounds__(512) ce_fwd_bwd_reg_kernel(T* __restrict__ log
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
         const int i = tid + k * NTH;
-        if (i < nv) r[k] = *reinterpret_cast<const R*>(x + head + (long)i * VN);
+        if (i < nv) r[k] = __builtin_nontemporal_load(reinterpret_cast<const R*>(x + head + (long)i * VN));
     }
     // one scalar per thread covers the unaligned head (< VN elements) and the tail (< VN elements)
     const int si = tid < head ? tid : (tid >= 64 && tid - 64 < ntail ? body_end + tid - 64 : -1);
@@ -186,7 +190,11 @@ __global__ void __launch_bounds__(512) ce_fwd_bwd_reg_kernel(T* __restrict__ log
             Vec<T> o;
 #pragma unroll
             for (int j = 0; j < VN; ++j) o.v[j] = (__expf(raw_get<T>(r[k], j) - lse) - ((long)(base + j) == t ? 1.f : 0.f)) * sc;
-            o.store(x + base);
+            // streamed once in, once out: non-temporal on both sides (the row is not re-read by this kernel)
+            R ov;
+#pragma unroll
+            for (int j = 0; j < VN; ++j) raw_set<T>(ov, j, o.v[j]);
+            __builtin_nontemporal_store(ov, reinterpret_cast<R*>(x + base));
         }
     }
 }
