@@ -44,6 +44,28 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// ---- streaming (non-temporal) vector access ---------------------------------
+// Activations that a memory-bound kernel reads or writes exactly once (hundreds of MB per tensor, never cached
+// usefully) go through these: the nt hint keeps them from displacing reusable lines.  Measured on the
+// softmax-CE kernel: 5.1 -> 5.5 TB/s (docs/performance.md).  -DBPE_STREAM_NT=0 builds the plain form (A/B).
+#ifndef BPE_STREAM_NT
+#define BPE_STREAM_NT 1
+#endif
+template <typename V> __device__ __forceinline__ V ld_stream(const V* p) {
+#if BPE_STREAM_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <typename V> __device__ __forceinline__ void st_stream(V* p, V v) {
+#if BPE_STREAM_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // ---- typed 16-byte vector load/store, converting to/from fp32 -------------
 // T = float (4 elems / 16 B) or __bf16 (8 elems / 16 B).
 template <typename T> struct Vec;
@@ -54,6 +76,11 @@ template <> struct Vec<float> {
         f32x4 t = *reinterpret_cast<const f32x4*>(p);
         v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
     }
+    __device__ __forceinline__ void load_s(const float* p) {  // streaming (see ld_stream)
+        f32x4 t = ld_stream(reinterpret_cast<const f32x4*>(p));
+        v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    }
+    __device__ __forceinline__ void store_s(float* p) const { st_stream(reinterpret_cast<f32x4*>(p), f32x4{v[0], v[1], v[2], v[3]}); }
     __device__ __forceinline__ void store(float* p) const {
         f32x4 t = {v[0], v[1], v[2], v[3]};
         *reinterpret_cast<f32x4*>(p) = t;
@@ -72,6 +99,17 @@ template <> struct Vec<__bf16> {
 #pragma unroll
         for (int i = 0; i < 8; ++i) t[i] = f2bf(v[i]);
         *reinterpret_cast<u16x8*>(p) = t;
+    }
+    __device__ __forceinline__ void load_s(const __bf16* p) {  // streaming (see ld_stream)
+        u16x8 t = ld_stream(reinterpret_cast<const u16x8*>(p));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = bf2f(t[i]);
+    }
+    __device__ __forceinline__ void store_s(__bf16* p) const {
+        u16x8 t;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = f2bf(v[i]);
+        st_stream(reinterpret_cast<u16x8*>(p), t);
     }
 };
 

@@ -50,7 +50,7 @@ template <int D> struct BwdCfg {
 };
 
 // delta = rowsum(dO * O) per (b, h, s)
-template <int D>
+template <int D, bool NT>
 __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const __bf16* __restrict__ O, long ld_o,
                                                          const __bf16* __restrict__ dO, long ld_do,
                                                          float* __restrict__ delta, float* __restrict__ dq_acc,
@@ -79,7 +79,8 @@ __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const __bf16* __restric
     const bool ok = in && s < S;
     if (ok) {
         const long bs = b * S + s;
-        u16x8 a = *reinterpret_cast<const u16x8*>(O + bs * ld_o + (long)h * D + sub * 8);
+        const u16x8* op = reinterpret_cast<const u16x8*>(O + bs * ld_o + (long)h * D + sub * 8);
+        u16x8 a = NT ? ld_stream(op) : *op;  // O is read once
         u16x8 g = *reinterpret_cast<const u16x8*>(dO + bs * ld_do + (long)h * D + sub * 8);
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc += bf2f(a[i]) * bf2f(g[i]);
@@ -438,7 +439,7 @@ __global__ void __launch_bounds__(256) fa_dkv_reduce_kernel(const float* __restr
 }
 
 // dQ (fp32, roped space, unscaled) -> bf16 output slice: dq = scale * R(-pos) dQacc
-template <int D, bool ROPE>
+template <int D, bool ROPE, bool NT>
 __global__ void __launch_bounds__(256) fa_dq_convert_kernel(const float* __restrict__ dQacc, __bf16* __restrict__ dq,
                                                             long ld_dq, const float* __restrict__ cosT,
                                                             const float* __restrict__ sinT, int B, int H, int S,
@@ -451,7 +452,8 @@ __global__ void __launch_bounds__(256) fa_dq_convert_kernel(const float* __restr
         const int h = (int)(row % H);
         const long s = bs % S;
         const long src = ((bs / S) * ((S + 63) & ~63) + s) * H + h;  // padded dQacc row
-        f32x4 v = *reinterpret_cast<const f32x4*>(dQacc + src * D + d0);
+        const f32x4* vp = reinterpret_cast<const f32x4*>(dQacc + src * D + d0);
+        f32x4 v = NT ? ld_stream(vp) : *vp;  // read once
         float x[4] = {v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale};
         if (ROPE) {
 #pragma unroll
@@ -508,6 +510,9 @@ static void bwd_main(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
         bwd_main_k<D, C, R, DBG, R>(a, s, nkb, dbg);
 }
 
+// a [tokens, H * D] bf16 activation larger than the 256 MB Infinity Cache: stream it non-temporally
+static bool big_stream(const FaArgs& a) { return (size_t)a.B * a.S * a.H * a.D * 2 > ((size_t)256 << 20); }
+
 template <int D, bool C, bool R>
 static void bwd_launch(const FaArgs& a, hipStream_t s) {
     using Cfg = BwdCfg<D>;
@@ -515,7 +520,10 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
         const int spad = (a.S + 63) & ~63;  // dq_acc is [B][spad][H][D] fp32
         const long rows = (long)a.B * spad * a.H;
         const long threads = rows * (D / 8);
-        fa_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
+        // non-temporal loads only for tensors past the 256 MB Infinity Cache (GPT-2 B 128: 3-5 % faster
+        // pre / convert kernels; Llama B 8, 67 MB O: 3-4 % slower with them)
+        auto* pre = big_stream(a) ? &fa_bwd_pre_kernel<D, true> : &fa_bwd_pre_kernel<D, false>;
+        pre<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
             a.o, a.ld_o, a.dout, a.ld_do, a.delta, a.dq_zeroed ? nullptr : a.dq_acc, a.B, a.H, a.S, spad);
     }
     constexpr int dbg = 0;
@@ -546,7 +554,8 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
     }
     const long total = (long)a.B * a.S * a.H * (D / 4);
     const int grid = (int)std::min<long>((total + 255) / 256, 4096);
-    fa_dq_convert_kernel<D, R><<<grid, 256, 0, s>>>(a.dq_acc, a.dq, a.ld_dq, a.cos, a.sin, a.B, a.H, a.S, a.scale);
+    auto* conv = big_stream(a) ? &fa_dq_convert_kernel<D, R, true> : &fa_dq_convert_kernel<D, R, false>;
+    conv<<<grid, 256, 0, s>>>(a.dq_acc, a.dq, a.ld_dq, a.cos, a.sin, a.B, a.H, a.S, a.scale);
 }
 
 void launch_fa_bwd(const FaArgs& a, hipStream_t s) {

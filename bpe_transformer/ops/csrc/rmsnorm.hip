@@ -133,7 +133,10 @@ __global__ void __launch_bounds__(256) add_rmsnorm_fwd_kernel(const T* __restric
     }
 }
 
-// C = number of 16-byte column chunks each lane owns (ceil(N / V / 64)).
+// C = number of 16-byte column chunks each lane owns (ceil(N / V / 64)).  Activations go through the
+// streaming (non-temporal) accessors: 140.3 -> 138.3 us at 131072 x 768, where each tensor is ~200 MB.  The
+// forward kernels, and the wide kernel below at Llama's 67 MB tensors (which fit the 256 MB Infinity Cache),
+// measured slower with them (docs/performance.md).
 template <typename T, int C>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const T* __restrict__ w,
@@ -171,9 +174,9 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ 
         for (int c = 0; c < C; ++c) {
             const int i = c * 64 + lane;
             const bool ok = i < nvec;
-            xo[c] = ok ? *reinterpret_cast<const R*>(x + (size_t)row * N + i * V) : zero;
-            go[c] = ok ? *reinterpret_cast<const R*>(dy + (size_t)row * N + i * V) : zero;
-            ro[c] = (ok && dres) ? *reinterpret_cast<const R*>(dres + (size_t)row * N + i * V) : zero;
+            xo[c] = ok ? ld_stream(reinterpret_cast<const R*>(x + (size_t)row * N + i * V)) : zero;
+            go[c] = ok ? ld_stream(reinterpret_cast<const R*>(dy + (size_t)row * N + i * V)) : zero;
+            ro[c] = (ok && dres) ? ld_stream(reinterpret_cast<const R*>(dres + (size_t)row * N + i * V)) : zero;
         }
     };
     const int stride = gridDim.x * 4;
@@ -205,7 +208,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ 
                     o.v[j] = r * (g * wv[c][j] - xh * dot) + RawV<T>::get(ra[c], j);
                     dwacc[c][j] += g * xh;
                 }
-                o.store(dxr + i * V);
+                o.store_s(dxr + i * V);
             }
         }
 #pragma unroll
