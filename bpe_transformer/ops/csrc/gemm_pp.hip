@@ -490,8 +490,8 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const long ro = (long)(i0 + q * 16 + (tid >> 5)) * ep.ld + j0 + c * 8;
-                gv[q] = *reinterpret_cast<const u16x8*>(ep.gu + ro);
-                uv[q] = *reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F);
+                gv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro));  // read once
+                uv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F));
             }
             __syncthreads();
 #pragma unroll
@@ -528,8 +528,9 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
                     av[e] = f2bf(gg * fast_sigmoid(gg) * bf2f(uv[e]));
                 }
                 const long r = i0 + i;
-                *reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + jb + c * 8) = gv;
-                *reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + ep.F + jb + c * 8) = uv;
+                // gu is next read by the backward, long after this step's forward: streaming stores
+                st_stream(reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + jb + c * 8), gv);
+                st_stream(reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + ep.F + jb + c * 8), uv);
                 *reinterpret_cast<u16x8*>(ep.act + r * ep.ld_act + jb + c * 8) = av;
             }
             return;
