@@ -510,8 +510,9 @@ static void bwd_main(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
         bwd_main_k<D, C, R, DBG, R>(a, s, nkb, dbg);
 }
 
-// a [tokens, H * D] bf16 activation larger than the 256 MB Infinity Cache: stream it non-temporally
-static bool big_stream(const FaArgs& a) { return (size_t)a.B * a.S * a.H * a.D * 2 > ((size_t)256 << 20); }
+// stream non-temporally when a [tokens, H * D] bf16 activation is past 128 MB: GPT-2 B 128 (201 MB; its fp32 dQ
+// accumulator 402 MB) gains, Llama-1.1B B 8 s2048 (67 MB, fits the 256 MB Infinity Cache with room) loses
+static bool big_stream(const FaArgs& a) { return (size_t)a.B * a.S * a.H * a.D * 2 > ((size_t)128 << 20); }
 
 template <int D, bool C, bool R>
 static void bwd_launch(const FaArgs& a, hipStream_t s) {
@@ -520,8 +521,8 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
         const int spad = (a.S + 63) & ~63;  // dq_acc is [B][spad][H][D] fp32
         const long rows = (long)a.B * spad * a.H;
         const long threads = rows * (D / 8);
-        // non-temporal loads only for tensors past the 256 MB Infinity Cache (GPT-2 B 128: 3-5 % faster
-        // pre / convert kernels; Llama B 8, 67 MB O: 3-4 % slower with them)
+        // non-temporal loads only for large activations (big_stream: GPT-2 B 128 3-5 % faster pre / convert
+        // kernels; Llama B 8, 67 MB O: 3-4 % slower with them)
         auto* pre = big_stream(a) ? &fa_bwd_pre_kernel<D, true> : &fa_bwd_pre_kernel<D, false>;
         pre<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
             a.o, a.ld_o, a.dout, a.ld_do, a.delta, a.dq_zeroed ? nullptr : a.dq_acc, a.B, a.H, a.S, spad);

@@ -533,6 +533,30 @@ def test_flash_dq_acc_zeroed_by_forward(gpu_device, S, D, H, Hkv, fused):
     assert rel(got[:, : H * D].cpu(), ref[:, : H * D].float().cpu()) < 1e-3  # dQ: fp32 atomics, order varies
 
 
+def test_flash_bwd_streaming_path_matches(gpu_device):
+    """Past 128 MB of bf16 activation the backward's pre-pass / dQ-convert kernels switch to non-temporal loads
+    (csrc/flash_attn_bwd.hip big_stream).  Batch 96 at the GPT-2 shape takes that path; its gradients must
+    equal those of two 48-sequence halves, which take the plain path: dK / dV bitwise, dQ up to atomic order."""
+    torch.manual_seed(6)
+    B, S, H, D = 96, 1024, 12, 64
+    assert B * S * H * D * 2 > (128 << 20) and B // 2 * S * H * D * 2 <= (128 << 20)
+    h = torch.ops.bpe_hip
+    qkv = torch.randn(B * S, 3 * H * D, device=gpu_device, dtype=torch.bfloat16)
+    cos, sin = R.rope_tables(D, S, 10000.0, device=gpu_device)
+    scale = D ** -0.5
+
+    def run(x, b):
+        q, k, v = x[:, : H * D], x[:, H * D : 2 * H * D], x[:, 2 * H * D :]
+        o, lse = h.fa_fwd(q, k, v, cos, sin, b, S, H, H, D, True, True, scale, True)
+        do = torch.ones_like(o) * 0.01 + (o * 0.5)
+        return h.fa_bwd(do, q, k, v, o, lse, cos, sin, b, S, H, H, D, True, True, scale, True)
+
+    full = run(qkv, B)
+    half = torch.cat([run(qkv[: B // 2 * S], B // 2), run(qkv[B // 2 * S :], B // 2)])
+    assert torch.equal(full[:, H * D :], half[:, H * D :])
+    assert rel(full[:, : H * D], half[:, : H * D]) < 1e-3
+
+
 def test_rope_qk_inplace(gpu_device):
     """rope_qk_ rotates exactly the Q and K heads of the fused activation (positions restart per sequence)."""
     torch.manual_seed(4)
