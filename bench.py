@@ -78,6 +78,12 @@ def main() -> int:
                          "shipped table for this model/batch if present, 'off' = library heuristics")
     ap.add_argument("--precision", choices=["bf16", "fp8"], default="bf16",
                     help="fp8 = block projections' forward GEMMs in e4m3fn with delayed scaling (bf16 backward)")
+    ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16",
+                    help="flat gradient buffer dtype (fp32: weight gradients written unrounded through the dW "
+                         "kernels' fp32 slab; the default bf16 is the measured-faster form for one micro-batch)")
+    ap.add_argument("--comm-dtype", choices=["auto", "bf16", "fp32"], default="auto",
+                    help="data-parallel all-reduce dtype (auto = the gradient dtype; fp32 with bf16 gradients "
+                         "sums across ranks without a bf16 rounding per ring hop)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = the plumbing config path (fp32, no HIP kernels), e.g. --model tinystories-17m --seq 256")
     ap.add_argument("--json-out", default=None)
@@ -105,8 +111,10 @@ def main() -> int:
         model.enable_fp8()
     # phase timing: device events around forward / backward / exposed collective wait / clip + AdamW, read once
     # after the timed loop (stderr; the driver's scaling run then shows how much all-reduce stays exposed)
+    gdt = {"bf16": torch.bfloat16, "fp32": torch.float32}[args.grad_dtype] if on_gpu else None
+    cdt = None if args.comm_dtype == "auto" else {"bf16": torch.bfloat16, "fp32": torch.float32}[args.comm_dtype]
     engine = TrainEngine(model, info, lr=3e-4, weight_decay=0.1, max_grad_norm=1.0, bucket_mb=args.bucket_mb,
-                         zero=args.zero, time_phases=on_gpu)
+                         zero=args.zero, time_phases=on_gpu, grad_dtype=gdt, comm_dtype=cdt)
 
     # synthetic token stream, different per rank; batches staged on the device up front
     data = synthetic_tokens(cfg.vocab_size, args.batch * (args.seq + 1) * 8, seed=1000 + info.rank)
@@ -122,6 +130,8 @@ def main() -> int:
         engine.train_step(batch(i))
     sync()
     engine.phase_times()  # drop the warmup steps' events
+    if on_gpu:
+        torch.cuda.reset_peak_memory_stats(dev)
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -165,8 +175,14 @@ def main() -> int:
         "mfu_bf16_dense_2.5PF": round(value / n * flops_tok / 2.5e15, 4),
         "final_loss": round(loss_v, 4),
         "gemm_tuning": tuning,
+        "grad_dtype": str(engine.flat.grad.dtype).replace("torch.", ""),
+        "allreduce_dtype": (str(engine.ddp.comm_dtype if hasattr(engine.ddp, "comm_dtype") else
+                                engine.flat.grad.dtype).replace("torch.", "") if engine.ddp is not None else None),
     }
     if on_gpu:
+        # peak HBM allocated by PyTorch's caching allocator over the timed steps (max over ranks), and reserved
+        out["peak_mem_gb"] = round(all_reduce_max(torch.cuda.max_memory_allocated(dev) / 1e9, dev), 2)
+        out["peak_reserved_gb"] = round(all_reduce_max(torch.cuda.max_memory_reserved(dev) / 1e9, dev), 2)
         from bpe_transformer.ops import gemm as _gemm
 
         out["dw_gemm_routes"] = _gemm.routes_summary()  # weight-gradient kernel per shape (ops/tuning/dw_routes.json)

@@ -21,6 +21,10 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-rope", action="store_true", help="plain attention (isolates the fused-RoPE cost)")
+    ap.add_argument("--bwd-ab", action="store_true",
+                    help="interleaved same-process A/B of the backward forms: fused (atomics) and split at 4/8 "
+                         "waves per workgroup (ops.fa_bwd_config)")
+    ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--mode", choices=["block", "fused"], default="block",
                     help="block = the training path (rope_qk_ in place, then pre-rotated kernels; rope time reported "
                          "separately and included in fwd_ms); fused = RoPE inside the attention kernels")
@@ -53,6 +57,29 @@ def main():
         o, lse = fwd()
         bwd(o, lse)
     torch.cuda.synchronize()
+    fl = 4.0 * B * H * S * S * D / 2
+    if a.bwd_ab:
+        arms = {"fused": (1, 0, 0), "split4x4": (0, 4, 4), "split8x8": (0, 8, 8), "split4x8": (0, 4, 8),
+                "split8x4": (0, 8, 4)}
+        prev = hip.fa_bwd_config(-1, 0, 0)
+        times = {k: [] for k in arms}
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for _ in range(a.rounds):
+            for name, cfg in arms.items():
+                hip.fa_bwd_config(*cfg)
+                bwd(o, lse)
+                ev[0].record()
+                for _ in range(a.iters):
+                    bwd(o, lse)
+                ev[1].record()
+                torch.cuda.synchronize()
+                times[name].append(ev[0].elapsed_time(ev[1]) / a.iters)
+        hip.fa_bwd_config(prev, 4, 4)
+        for name, t in times.items():
+            t = sorted(t)
+            print(json.dumps({"shape": [B, S, H, Hkv, D], "arm": name, "bwd_ms_median": round(t[len(t) // 2], 4),
+                              "bwd_ms_min": round(t[0], 4), "bwd_tflops": round(2.5 * fl / t[len(t) // 2] / 1e9, 1)}))
+        return
     e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     tf, tb, tr = 0.0, 0.0, 0.0
     for _ in range(a.iters):
@@ -72,7 +99,6 @@ def main():
     tf /= a.iters
     tb /= a.iters
     tr /= a.iters
-    fl = 4.0 * B * H * S * S * D / 2
     print(json.dumps({"shape": [B, S, H, Hkv, D], "rope": rope, "mode": a.mode, "rope_ms": round(tr, 4),
                       "fwd_ms": round(tf, 4), "bwd_ms": round(tb, 4),
                       "fwd_tflops": round(fl / tf / 1e9, 1), "bwd_tflops": round(2.5 * fl / tb / 1e9, 1)}))

@@ -149,8 +149,11 @@ class FusedBlockFn(torch.autograd.Function):
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         # training: the forward kernel zeroes the backward's fp32 dQ accumulator in its epilogue (hidden under
         # its compute; the backward pre-pass then only reads O / dO)
+        # (only the fused atomics backward has that accumulator: D != 64 or BPE_FA_BWD=fused), and only when a
+        # backward will run
         dq_acc = (torch.empty(B * ((S + 63) // 64 * 64), H * D, device=q.device, dtype=torch.float32)
-                  if _DQ_FWD_ZERO and any(ctx.needs_input_grad) else None)
+                  if _DQ_FWD_ZERO and torch.is_grad_enabled() and any(ctx.needs_input_grad)
+                  and hip().fa_bwd_needs_dq_acc(D) else None)
         o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, pre, dq_acc)
         ctx.dq_acc = dq_acc
         g1 = mm(o, wo.detach(), 1) if fp8 is not None else torch.matmul(o, wo.t())

@@ -36,8 +36,9 @@ def load() -> None:
     with _lock:
         if _loaded:
             return
+        autobuild = os.environ.get("BPE_AUTOBUILD", "0") == "1" and not _VARIANT
         if not LIB_PATH.exists():
-            if os.environ.get("BPE_AUTOBUILD", "0") == "1" and not _VARIANT:
+            if autobuild:
                 from .build import build
 
                 build()
@@ -46,8 +47,28 @@ def load() -> None:
                     f"bpe_transformer HIP kernels are not built ({LIB_PATH} missing). "
                     "Run `python -m bpe_transformer.ops.build` (hipcc --offload-arch=gfx950)."
                 )
+        if not _VARIANT:  # A/B variants are built from other sources / defines: their stamps name those
+            check_fresh(autobuild)
         torch.ops.load_library(str(LIB_PATH))
         _loaded = True
+
+
+def check_fresh(rebuild: bool = False) -> None:
+    """Refuse a library whose content stamp does not match the kernel sources next to it (ops/build.py): it was
+    built from other sources, so its kernels are not the ones in the tree.  ``rebuild``: rebuild instead."""
+    from .build import read_stamp, source_digest
+
+    if read_stamp(LIB_PATH) == source_digest():
+        return
+    if rebuild:
+        from .build import build
+
+        build()
+        if read_stamp(LIB_PATH) == source_digest():
+            return
+    raise RuntimeError(
+        f"{LIB_PATH.name} is stale: its content stamp does not match bpe_transformer/ops/csrc (sources changed "
+        "since it was built). Run `python -m bpe_transformer.ops.build`, or set BPE_AUTOBUILD=1.")
 
 
 def ops():

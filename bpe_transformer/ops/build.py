@@ -4,8 +4,15 @@
 ``hipcc --offload-arch=gfx950`` (device code, no torch headers: seconds per
 file), the single torch-binding translation unit, and links
 ``bpe_transformer/ops/_bpe_hip.so`` next to this file, so the library travels
-with the source tree (no JIT cache, no site-packages install).  Rebuilds are
-incremental (mtime of each source and every header).
+with the source tree (no JIT cache, no site-packages install).
+
+Staleness is decided by CONTENT, not mtimes: every object records the sha256 of
+its compile command, its source and every header (``<obj>.sha``), and the linked
+library carries a stamp (``_bpe_hip.so.stamp``) with the digest of all sources,
+headers and flags.  ``_ext.load()`` recomputes that digest and refuses a library
+whose stamp does not match the tree (or rebuilds it with ``BPE_AUTOBUILD=1``), so a
+newer-but-stale ``.so`` shipped with a snapshot can never run in place of the
+sources next to it.
 
 No hipify step and no CUDA sources: the kernels are written for CDNA4 directly.
 """
@@ -14,6 +21,8 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -39,11 +48,41 @@ def _torch_paths():
     return inc, lib, abi
 
 
-def _needs_build(obj: Path, src: Path, headers: list[Path]) -> bool:
-    if not obj.exists():
-        return True
-    t = obj.stat().st_mtime
-    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
+COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17"]
+
+
+def _digest(paths: list[Path], extra: list[str]) -> str:
+    h = hashlib.sha256()
+    for x in extra:
+        h.update(x.encode() + b"\0")
+    for p in paths:
+        h.update(p.name.encode() + b"\0")
+        h.update(p.read_bytes())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def source_digest(csrc: Path = CSRC, defines: list[str] | None = None) -> str:
+    """sha256 over every kernel source, header and the binding unit plus the arch and flags: the library stamp."""
+    files = sorted(csrc.glob("*.h")) + sorted(csrc.glob("*.hip")) + [csrc / "torch_bindings.cpp"]
+    return _digest(files, [ARCH, *COMMON_FLAGS, *[f"-D{d}" for d in (defines or [])]])
+
+
+def stamp_path(lib: Path) -> Path:
+    return lib.with_name(lib.name + ".stamp")
+
+
+def read_stamp(lib: Path) -> str | None:
+    try:
+        return json.loads(stamp_path(lib).read_text())["digest"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def _needs_build(obj: Path, key: str) -> bool:
+    """Rebuild unless the object exists and was compiled from exactly this command + source + headers."""
+    sha = obj.with_name(obj.name + ".sha")
+    return not obj.exists() or not sha.exists() or sha.read_text().strip() != key
 
 
 def _run(cmd: list[str], verbose: bool) -> None:
@@ -74,35 +113,49 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False, v
     headers = sorted(csrc.glob("*.h"))
     hip_srcs = sorted(csrc.glob("*.hip"))
     inc, libdirs, abi = _torch_paths()
-    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", str(csrc)]
+    common = [*COMMON_FLAGS, f"--offload-arch={ARCH}", "-I", str(csrc)]
     common += [f"-D{d}" for d in (defines or [])]
-    jobs_list = []
+    jobs_list = []  # (command, object, content key)
     objs = []
     for src in hip_srcs:
         obj = build_dir / (src.stem + ".o")
         objs.append(obj)
-        if force or _needs_build(obj, src, headers):
-            jobs_list.append([HIPCC, *common, "-c", str(src), "-o", str(obj)])
+        cmd = [HIPCC, *common, "-c", str(src), "-o", str(obj)]
+        key = _digest([src, *headers], cmd)
+        if force or _needs_build(obj, key):
+            jobs_list.append((cmd, obj, key))
     bind_src = csrc / "torch_bindings.cpp"
     bind_obj = build_dir / "torch_bindings.o"
     objs.append(bind_obj)
-    if force or _needs_build(bind_obj, bind_src, headers):
-        cmd = [HIPCC, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
-               "-I", str(csrc)]
-        for i in inc:
-            cmd += ["-I", i]
-        cmd += ["-I", sysconfig.get_paths()["include"], "-c", str(bind_src), "-o", str(bind_obj)]
-        jobs_list.append(cmd)
+    cmd = [HIPCC, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
+           "-I", str(csrc)]
+    for i in inc:
+        cmd += ["-I", i]
+    cmd += ["-I", sysconfig.get_paths()["include"], "-c", str(bind_src), "-o", str(bind_obj)]
+    key = _digest([bind_src, *headers], cmd)
+    if force or _needs_build(bind_obj, key):
+        jobs_list.append((cmd, bind_obj, key))
+
+    def compile_one(job):
+        cmd, obj, key = job
+        obj.with_name(obj.name + ".sha").unlink(missing_ok=True)
+        _run(cmd, verbose)
+        obj.with_name(obj.name + ".sha").write_text(key + "\n")
+
     if jobs_list:
         n = jobs or min(8, os.cpu_count() or 4)
         with cf.ThreadPoolExecutor(n) as ex:
-            list(ex.map(lambda c: _run(c, verbose), jobs_list))
-    if force or jobs_list or not lib.exists():
+            list(ex.map(compile_one, jobs_list))
+    digest = source_digest(csrc, defines)
+    if force or jobs_list or not lib.exists() or read_stamp(lib) != digest:
+        stamp_path(lib).unlink(missing_ok=True)
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(lib), *map(str, objs)]
         for d in libdirs:
             link += ["-L", d, f"-Wl,-rpath,{d}"]
         link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip"]
         _run(link, verbose)
+        stamp_path(lib).write_text(json.dumps({"digest": digest, "arch": ARCH, "defines": defines or [],
+                                               "src": str(csrc)}) + "\n")
     return lib
 
 

@@ -559,7 +559,22 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
     conv<<<grid, 256, 0, s>>>(a.dq_acc, a.dq, a.ld_dq, a.cos, a.sin, a.B, a.H, a.S, a.scale);
 }
 
+void launch_fa_dkv_reduce(const FaArgs& a, hipStream_t s) {
+    const long tkv = (long)a.B * a.S * a.Hkv * (a.D / 4);
+    const int g2 = (int)std::min<long>((tkv + 255) / 256, 4096);
+    if (a.D != 64) return;
+    if (a.rope)
+        fa_dkv_reduce_kernel<64, true><<<g2, 256, 0, s>>>(a.dkv_part, a.dk, a.dv, a.ld_dkv, a.cos, a.sin, a.B, a.H,
+                                                            a.Hkv, a.S, a.scale);
+    else
+        fa_dkv_reduce_kernel<64, false><<<g2, 256, 0, s>>>(a.dkv_part, a.dk, a.dv, a.ld_dkv, a.cos, a.sin, a.B, a.H,
+                                                             a.Hkv, a.S, a.scale);
+}
+
+bool launch_fa_bwd_split(const FaArgs& a, hipStream_t s);  // flash_attn_bwd_split.hip
+
 void launch_fa_bwd(const FaArgs& a, hipStream_t s) {
+    if (launch_fa_bwd_split(a, s)) return;  // D = 64: the split (dQ kernel + dK/dV kernel) form
     // a.rope: 0 none, 1 rotate Q / K on load and dQ / dK on output, 2 outputs only (Q / K pre-rotated)
 #define BWD_CASE(DD)                                                                                        \
     if (a.D == DD) {                                                                                        \

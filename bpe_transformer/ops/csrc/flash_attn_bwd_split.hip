@@ -1,0 +1,489 @@
+// Flash attention backward, split form (D = 64), gfx950 (MI355X).
+//
+// Parity target: the gradient of reference contracts K7/K10 (`tests/adapters.py:92-184`); checked against
+// autograd of the fp32 oracle (tests/test_kernels_gpu.py).
+//
+// Why split: the fused backward (flash_attn_bwd.hip) owns 256 keys per workgroup and adds dQ = dS.K into an fp32
+// buffer with float atomics.  At GPT-2 B 128 that is 983 MB of atomics per layer, whose chip-wide rate (1.3 TB/s,
+// MI355X_MICROARCH 'Global float atomics') floors the kernel at 0.76 ms; it also needs a zeroed 402 MB fp32
+// accumulator per layer, a delta pre-pass and a dQ convert pass.  Here the five products are computed by two
+// kernels that each own their output, so nothing is summed across workgroups:
+//
+//   fa_bwd_dq_kernel   (query-major, first):  delta = rowsum(dO * O) for its queries (written for the second
+//       kernel), then per 64-key tile  S^T = K.Q^T,  dP^T = V.dO^T - delta,  P^T = exp2(S^T * c - lse),
+//       dS^T = P^T * dP^T,  dQ^T += K^T.dS^T.   Q and dO are the lane-resident B operands (query on the lane),
+//       pinned in registers for the whole key sweep; K / V tiles are staged in LDS (register staging, guide
+//       T14: loads of tile t+1 issued before tile t's MFMAs, written after them; one barrier per tile).  dS^T
+//       is the B operand of the dQ^T product straight from its accumulator (guide §3).  dQ is scaled,
+//       un-rotated (RoPE) and written as bf16 in the epilogue.
+//   fa_bwd_dkv_kernel  (key-major):  per 64-query tile  S = Q.K^T - lse/c,  dP = dO.V^T - delta (row constants
+//       as the initial accumulators), P = exp2(c S), dS = P dP,  dV^T += dO^T.P,  dK^T += Q^T.dS.  K and V are
+//       the pinned B operands (key on the lane); Q / dO rows and their transposed reads come from one LDS image
+//       (fa_common.h).  No dS LDS round trip, no second barrier, no atomics.
+//
+// The price is the recomputation of S and dP in the dQ kernel (7 MFMA products instead of 5); in exchange the
+// atomics floor, the 402 MB/layer accumulator (4.8 GB at GPT-2 B 128), the zeroing and the two side passes go.
+// GQA: the dK / dV kernel runs per query head and writes fp32 partials summed by fa_dkv_reduce_kernel.
+#include "fa_common.h"
+#include "kernels.h"
+
+#include <cstdlib>
+
+namespace bpe {
+namespace fa {
+namespace split {
+
+constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4;
+
+// staged 16-byte chunks per thread and tensor for one 64-row tile (512 chunks)
+template <int NW> constexpr int cpt() { return 512 / (NW * 64); }
+
+template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW>
+__global__ void __launch_bounds__(NW * 64, 2)
+fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
+                 long ld_q, long ld_kv, const __bf16* __restrict__ O, long ld_o, const __bf16* __restrict__ dO,
+                 long ld_do, const float* __restrict__ LSE, float* __restrict__ DELTA, __bf16* __restrict__ dQ,
+                 long ld_dq, const float* __restrict__ cosT, const float* __restrict__ sinT, int B, int H, int Hkv,
+                 int S, float scale_log2, float scale, int group) {
+    constexpr int NT = NW * 64, QB = 32 * NW, CPT = cpt<NW>();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Ks = smem;             // [2][64 keys][128 B]  (roped K)
+    char* Vs = smem + 2 * TILE;  // [2][64 keys][128 B]
+
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    const int nqb = (S + QB - 1) / QB;
+    int rank, bh;
+    grouped_order((int)blockIdx.x, nqb, B * H, group, rank, bh);
+    const int qblk = CAUSAL ? nqb - 1 - rank : rank;  // causal: the last (heaviest) query blocks first
+    const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+    const int q0 = qblk * QB, qw = q0 + 32 * w, q = qw + l31;
+    const bool q_ok = q < S;
+    const long qc = q_ok ? q : S - 1;
+    const long qrow = (long)b * S + qc;
+
+    // ---- pinned B operands (query on the lane, d = 16 ks + 8 hh + j) and delta = rowsum(dO * O)
+    bf16x8 qf[KS], of[KS];
+    float dsum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int d0 = 16 * ks + 8 * hh;
+        u16x8 tq = *reinterpret_cast<const u16x8*>(Q + qrow * ld_q + (long)h * D + d0);
+        if (ROPE_IN) tq = rope_u16x8(tq, cosT + qc * (D / 2) + d0 / 2, sinT + qc * (D / 2) + d0 / 2, 1.f);
+        qf[ks] = __builtin_bit_cast(bf16x8, tq);
+        const u16x8 tg = *reinterpret_cast<const u16x8*>(dO + qrow * ld_do + (long)h * D + d0);
+        const u16x8 to = *reinterpret_cast<const u16x8*>(O + qrow * ld_o + (long)h * D + d0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dsum += bf2f(tg[i]) * bf2f(to[i]);
+        of[ks] = __builtin_bit_cast(bf16x8, tg);
+    }
+    dsum += __shfl_xor(dsum, 32, 64);
+    if (q_ok && hh == 0) DELTA[((long)b * H + h) * S + q] = dsum;
+    const float lse = LSE[((long)b * H + h) * S + qc];
+    const float nl = (q_ok && lse < INFINITY) ? -lse : -INFINITY;  // P = exp2(S c - lse); 0 for empty / pad rows
+    f32x16 nd;                                                       // dP^T starts at -delta (row constant)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) nd[r] = -dsum;
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
+
+    const int kend = CAUSAL ? min(S, q0 + QB) : S;
+    const int nkt = (kend + 63) / 64;
+    const __bf16* kb = K + (long)b * S * ld_kv + (long)hk * D;
+    const __bf16* vb = Vv + (long)b * S * ld_kv + (long)hk * D;
+    u16x8 kreg[CPT], vreg[CPT];
+    auto load_tile = [&](int it) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int e = tid + NT * i, r = e >> 3, c = e & 7;
+            const long kk = min(it * 64 + r, S - 1);  // rows past the end: valid memory, zeroed at the write
+            kreg[i] = *reinterpret_cast<const u16x8*>(kb + kk * ld_kv + c * 8);
+            vreg[i] = *reinterpret_cast<const u16x8*>(vb + kk * ld_kv + c * 8);
+        }
+    };
+    auto write_tile = [&](int it, int buf) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int e = tid + NT * i, r = e >> 3, c = e & 7;
+            const bool ok = it * 64 + r < S;
+            u16x8 kv = ok ? kreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            const u16x8 vv = ok ? vreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            if (ROPE_IN) {
+                const long kk = min(it * 64 + r, S - 1);
+                kv = rope_u16x8(kv, cosT + kk * (D / 2) + c * 4, sinT + kk * (D / 2) + c * 4, 1.f);
+            }
+            *reinterpret_cast<u16x8*>(Ks + buf * TILE + swz<RB>(r, c)) = kv;
+            *reinterpret_cast<u16x8*>(Vs + buf * TILE + swz<RB>(r, c)) = vv;
+        }
+    };
+
+    load_tile(0);
+    write_tile(0, 0);
+    __syncthreads();
+
+    const int trow = 4 * hh + ((l & 15) >> 2);          // tr-read row inside a 16-key step
+    const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);  // tr-read column inside a 32-wide d tile
+    for (int it = 0; it < nkt; ++it) {
+        const int cur = it & 1, k0 = it * 64;
+        if (it + 1 < nkt) load_tile(it + 1);
+        char* Kc = Ks + cur * TILE;
+        const char* Vc = Vs + cur * TILE;
+        if (!CAUSAL || k0 <= qw + 31) {
+            const bool need_mask = (CAUSAL && k0 + 63 > qw) || (k0 + 64 > S);
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh) {
+                if (CAUSAL && k0 + 32 * kh > qw + 31) break;  // this 32-key half is past every query of the wave
+                f32x16 sp, dp = nd;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sp[r] = 0.f;
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
+                    sp = mfma(lds_row16(Kc, koff), qf[ks], sp);
+                    dp = mfma(lds_row16(Vc, koff), of[ks], dp);
+                }
+                // P^T = exp2(S^T c - lse), dS^T = P^T (dP^T - delta); key = row of the accumulator, query = lane
+                if (need_mask) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = k0 + 32 * kh + acc_row(r, hh);
+                        const float p = fast_exp2(fmaf(sp[r], scale_log2, nl));
+                        const bool ok = key < S && (!CAUSAL || key <= q);
+                        dp[r] = ok ? p * dp[r] : 0.f;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(fmaf(sp[r], scale_log2, nl)) * dp[r];
+                }
+                // dQ^T += K^T.dS^T: registers 8s..8s+7 are k-step s (keys 16 s ..) in the MFMA's permuted order
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    bf16x8 db;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) db[j] = (__bf16)dp[8 * s + j];
+                    const int kr = 32 * kh + 16 * s;
+#pragma unroll
+                    for (int dt = 0; dt < 2; ++dt)
+                        acc[dt] = mfma(lds_tr_pair(Kc, tr_off<RB>(kr + trow, 32 * dt + tcol),
+                                                   tr_off<RB>(kr + 8 + trow, 32 * dt + tcol)),
+                                       db, acc[dt]);
+                }
+            }
+        }
+        if (it + 1 < nkt) write_tile(it + 1, cur ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: dQ = scale * R(-pos) dQ^T (query on the lane, 4 consecutive d per register group)
+    if (q_ok) {
+        __bf16* dqp = dQ + ((long)b * S + q) * ld_dq + (long)h * D;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d0 = 32 * dt + 8 * i + 4 * hh;
+                float x[4] = {acc[dt][4 * i] * scale, acc[dt][4 * i + 1] * scale, acc[dt][4 * i + 2] * scale,
+                              acc[dt][4 * i + 3] * scale};
+                if (ROPE) {
+#pragma unroll
+                    for (int pr = 0; pr < 2; ++pr) {
+                        const float c = cosT[(long)q * (D / 2) + d0 / 2 + pr];
+                        const float sn = sinT[(long)q * (D / 2) + d0 / 2 + pr];
+                        const float a = x[2 * pr], bb = x[2 * pr + 1];
+                        x[2 * pr] = a * c + bb * sn;
+                        x[2 * pr + 1] = -a * sn + bb * c;
+                    }
+                }
+                *reinterpret_cast<u16x4*>(dqp + d0) = u16x4{f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+            }
+    }
+}
+
+template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW>
+__global__ void __launch_bounds__(NW * 64, 2)
+fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
+                  long ld_q, long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
+                  const float* __restrict__ DELTA, __bf16* __restrict__ dK, __bf16* __restrict__ dV, long ld_dkv,
+                  float* __restrict__ dKVpart, const float* __restrict__ cosT, const float* __restrict__ sinT, int B,
+                  int H, int Hkv, int S, float scale_log2, float scale, int group) {
+    constexpr int NT = NW * 64, KB = 32 * NW, CPT = cpt<NW>();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Qs = smem;                                             // [2][64 q][128 B]  (roped Q)
+    char* dOs = smem + 2 * TILE;                                 // [2][64 q][128 B]
+    float* lseS = reinterpret_cast<float*>(smem + 4 * TILE);     // [2][64]  -lse / c
+    float* dltS = lseS + 128;                                    // [2][64]  -delta
+
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    const int nkb = (S + KB - 1) / KB;
+    int kblk, bh;  // causal: key block 0 (the most query tiles) first
+    grouped_order((int)blockIdx.x, nkb, B * H, group, kblk, bh);
+    const int b = bh / H, h = bh % H, G = H / Hkv, hk = h / G;
+    const int kb0 = kblk * KB, kw0 = kb0 + 32 * w, key = kw0 + l31;
+    const bool key_ok = key < S;
+    const long kpos = key_ok ? key : S - 1;
+
+    // ---- pinned B operands: K (roped) and V rows of the lane's key, d = 16 ks + 8 hh + j
+    bf16x8 kf[KS], vf[KS];
+    {
+        const __bf16* kp = K + ((long)b * S + kpos) * ld_kv + (long)hk * D;
+        const __bf16* vp = Vv + ((long)b * S + kpos) * ld_kv + (long)hk * D;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int d0 = 16 * ks + 8 * hh;
+            u16x8 tk = key_ok ? *reinterpret_cast<const u16x8*>(kp + d0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            const u16x8 tv = key_ok ? *reinterpret_cast<const u16x8*>(vp + d0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            if (ROPE_IN) tk = rope_u16x8(tk, cosT + kpos * (D / 2) + d0 / 2, sinT + kpos * (D / 2) + d0 / 2, 1.f);
+            kf[ks] = __builtin_bit_cast(bf16x8, tk);
+            vf[ks] = __builtin_bit_cast(bf16x8, tv);
+        }
+    }
+
+    f32x16 dk[2], dv[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+
+    const int m_start = CAUSAL ? kb0 : 0;  // kb0 is a multiple of 64
+    const int nqt = m_start < S ? (S - m_start + 63) / 64 : 0;
+    const __bf16* qb = Q + (long)b * S * ld_q + (long)h * D;
+    const __bf16* ob = dO + (long)b * S * ld_do + (long)h * D;
+    const long sbase = ((long)b * H + h) * S;
+    u16x8 qreg[CPT], oreg[CPT];
+    float lreg = 0.f, dreg = 0.f;
+    auto load_tile = [&](int it) {
+        const int m0 = m_start + it * 64;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int e = tid + NT * i, r = e >> 3, c = e & 7;
+            const long qq = min(m0 + r, S - 1);
+            qreg[i] = *reinterpret_cast<const u16x8*>(qb + qq * ld_q + c * 8);
+            oreg[i] = *reinterpret_cast<const u16x8*>(ob + qq * ld_do + c * 8);
+        }
+        const long idx = sbase + min(m0 + l, S - 1);  // every wave loads the stats (wave 0 writes them)
+        lreg = LSE[idx];
+        dreg = DELTA[idx];
+    };
+    auto write_tile = [&](int it, int buf) {
+        const int m0 = m_start + it * 64;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int e = tid + NT * i, r = e >> 3, c = e & 7;
+            const bool ok = m0 + r < S;
+            u16x8 qv = ok ? qreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            const u16x8 ov = ok ? oreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            if (ROPE_IN) {
+                const long qq = min(m0 + r, S - 1);
+                qv = rope_u16x8(qv, cosT + qq * (D / 2) + c * 4, sinT + qq * (D / 2) + c * 4, 1.f);
+            }
+            *reinterpret_cast<u16x8*>(Qs + buf * TILE + swz<RB>(r, c)) = qv;
+            *reinterpret_cast<u16x8*>(dOs + buf * TILE + swz<RB>(r, c)) = ov;
+        }
+        if (tid < 64) {  // the S / dP accumulators' starting values: -lse / c and -delta
+            const bool ok = m0 + tid < S;
+            lseS[buf * 64 + tid] = (!ok || lreg == INFINITY) ? -INFINITY : -lreg / scale_log2;
+            dltS[buf * 64 + tid] = ok ? -dreg : 0.f;
+        }
+    };
+
+    if (nqt > 0) {
+        load_tile(0);
+        write_tile(0, 0);
+    }
+    __syncthreads();
+
+    const int trow = 4 * hh + ((l & 15) >> 2);
+    const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
+    const int klim = CAUSAL ? (key_ok ? key : S) : (key_ok ? 0 : S);
+    const unsigned span = (unsigned)(S - klim);  // valid query q: (unsigned)(q - klim) < span
+    for (int it = 0; it < nqt; ++it) {
+        const int cur = it & 1, m0 = m_start + it * 64;
+        if (it + 1 < nqt) load_tile(it + 1);
+        char* Qc = Qs + cur * TILE;
+        char* Oc = dOs + cur * TILE;
+        const float* lc = lseS + cur * 64;
+        const float* dc = dltS + cur * 64;
+        if (!CAUSAL || m0 + 63 >= kw0) {
+            const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + 64 > S) || (kw0 + 32 > S);
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt) {
+                if (CAUSAL && m0 + 32 * qt + 31 < kw0) continue;  // every query of this half precedes every key
+                f32x16 sp, dp;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int qi = qt * 32 + 8 * i + 4 * hh;  // rows qi..qi+3 of registers 4i..4i+3
+                    const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
+                    const f32x4 dl = *reinterpret_cast<const f32x4*>(dc + qi);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) { sp[4 * i + j] = lv[j]; dp[4 * i + j] = dl[j]; }
+                }
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
+                    sp = mfma(lds_row16(Qc, off), kf[ks], sp);
+                    dp = mfma(lds_row16(Oc, off), vf[ks], dp);
+                }
+                if (need_mask) {
+                    const int qoff = m0 + qt * 32 - klim;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float p = fast_exp2(sp[r] * scale_log2);
+                        const bool ok = (unsigned)(qoff + acc_row(r, hh)) < span;
+                        sp[r] = ok ? p : 0.f;
+                        dp[r] = ok ? p * dp[r] : 0.f;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float p = fast_exp2(sp[r] * scale_log2);
+                        sp[r] = p;
+                        dp[r] *= p;
+                    }
+                }
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    bf16x8 pb, db;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        pb[j] = (__bf16)sp[8 * ss + j];
+                        db[j] = (__bf16)dp[8 * ss + j];
+                    }
+                    const int qr = qt * 32 + 16 * ss;
+#pragma unroll
+                    for (int dt = 0; dt < 2; ++dt) {
+                        const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
+                        const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
+                        dv[dt] = mfma(lds_tr_pair(Oc, o0, o1), pb, dv[dt]);
+                        dk[dt] = mfma(lds_tr_pair(Qc, o0, o1), db, dk[dt]);
+                    }
+                }
+            }
+        }
+        if (it + 1 < nqt) write_tile(it + 1, cur ^ 1);
+        __syncthreads();
+    }
+
+    if (!key_ok) return;
+    if (G > 1) {  // GQA: fp32 partials of this query head -> [b, s, h, {dK, dV}, D] for fa_dkv_reduce_kernel
+        float* pk = dKVpart + (((long)b * S + key) * H + h) * 2 * D;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d0 = dt * 32 + 8 * i + 4 * hh;
+                *reinterpret_cast<f32x4*>(pk + d0) =
+                    f32x4{dk[dt][4 * i], dk[dt][4 * i + 1], dk[dt][4 * i + 2], dk[dt][4 * i + 3]};
+                *reinterpret_cast<f32x4*>(pk + D + d0) =
+                    f32x4{dv[dt][4 * i], dv[dt][4 * i + 1], dv[dt][4 * i + 2], dv[dt][4 * i + 3]};
+            }
+        return;
+    }
+    // ---- dK = scale * R(-pos) dK^T, dV = dV^T (key on the lane, d in registers)
+    __bf16* dkp = dK + ((long)b * S + key) * ld_dkv + (long)hk * D;
+    __bf16* dvp = dV + ((long)b * S + key) * ld_dkv + (long)hk * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int d0 = dt * 32 + 8 * i + 4 * hh;
+            float x[4] = {dk[dt][4 * i] * scale, dk[dt][4 * i + 1] * scale, dk[dt][4 * i + 2] * scale,
+                          dk[dt][4 * i + 3] * scale};
+            if (ROPE) {
+#pragma unroll
+                for (int pr = 0; pr < 2; ++pr) {
+                    const float c = cosT[kpos * (D / 2) + d0 / 2 + pr];
+                    const float sn = sinT[kpos * (D / 2) + d0 / 2 + pr];
+                    const float a = x[2 * pr], bb = x[2 * pr + 1];
+                    x[2 * pr] = a * c + bb * sn;
+                    x[2 * pr + 1] = -a * sn + bb * c;
+                }
+            }
+            *reinterpret_cast<u16x4*>(dkp + d0) = u16x4{f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+            *reinterpret_cast<u16x4*>(dvp + d0) = u16x4{f2bf(dv[dt][4 * i]), f2bf(dv[dt][4 * i + 1]),
+                                                        f2bf(dv[dt][4 * i + 2]), f2bf(dv[dt][4 * i + 3])};
+        }
+}
+
+}  // namespace split
+}  // namespace fa
+}  // namespace bpe
+
+using namespace bpe;
+using namespace bpe::fa;
+
+// Backward form: 0 = split (default for D = 64), 1 = fused (flash_attn_bwd.hip, the atomics form).  Initial value
+// from BPE_FA_BWD ("fused" / "split"), changeable at run time (fa_bwd_config) for same-process A/B and tests.
+// Waves per workgroup of the two split kernels (4 or 8 each): BPE_FA_SPLIT_NW="<dq>,<dkv>", default 4,4.
+static int g_mode = -1, g_nw_dq = 4, g_nw_dkv = 4;
+
+static void config_init() {
+    if (g_mode >= 0) return;
+    const char* e = getenv("BPE_FA_BWD");
+    g_mode = (e && e[0] == 'f') ? 1 : 0;
+    if (const char* n = getenv("BPE_FA_SPLIT_NW")) {
+        int a = 4, c = 4;
+        if (sscanf(n, "%d,%d", &a, &c) >= 1) {
+            g_nw_dq = a == 8 ? 8 : 4;
+            g_nw_dkv = c == 8 ? 8 : 4;
+        }
+    }
+}
+
+bool fa_bwd_split_active(int D) {
+    config_init();
+    return D == 64 && g_mode == 0;
+}
+
+// mode < 0 / nw <= 0 leave a setting unchanged; returns the mode in force afterwards
+int fa_bwd_config(int mode, int nw_dq, int nw_dkv) {
+    config_init();
+    if (mode >= 0) g_mode = mode ? 1 : 0;
+    if (nw_dq > 0) g_nw_dq = nw_dq == 8 ? 8 : 4;
+    if (nw_dkv > 0) g_nw_dkv = nw_dkv == 8 ? 8 : 4;
+    return g_mode;
+}
+
+template <bool C, bool R, bool RIN, int NW>
+static void dq_launch(const FaArgs& a, hipStream_t s) {
+    const int nqb = (a.S + 32 * NW - 1) / (32 * NW);
+    split::fa_bwd_dq_kernel<C, R, RIN, NW><<<nqb * a.B * a.H, NW * 64, 4 * split::TILE, s>>>(
+        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do, a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin,
+        a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
+}
+
+template <bool C, bool R, bool RIN, int NW>
+static void dkv_launch(const FaArgs& a, hipStream_t s) {
+    const int nkb = (a.S + 32 * NW - 1) / (32 * NW);
+    split::fa_bwd_dkv_kernel<C, R, RIN, NW><<<nkb * a.B * a.H, NW * 64, 4 * split::TILE + 1024, s>>>(
+        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.dkv_part, a.cos,
+        a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
+}
+
+template <bool C, bool R, bool RIN>
+static void split_launch(const FaArgs& a, hipStream_t s) {
+    config_init();
+    const int nq = g_nw_dq, nk = g_nw_dkv;
+    if (nq == 8) dq_launch<C, R, RIN, 8>(a, s); else dq_launch<C, R, RIN, 4>(a, s);
+    if (nk == 8) dkv_launch<C, R, RIN, 8>(a, s); else dkv_launch<C, R, RIN, 4>(a, s);
+}
+
+void launch_fa_dkv_reduce(const FaArgs& a, hipStream_t s);  // flash_attn_bwd.hip
+
+bool launch_fa_bwd_split(const FaArgs& a, hipStream_t s) {
+    if (!fa_bwd_split_active(a.D)) return false;
+    // rope: 0 none, 1 rotate Q / K on load and dQ / dK on output, 2 outputs only (Q / K pre-rotated)
+    if (a.causal) {
+        if (a.rope == 1) split_launch<true, true, true>(a, s);
+        else if (a.rope == 2) split_launch<true, true, false>(a, s);
+        else split_launch<true, false, false>(a, s);
+    } else {
+        if (a.rope == 1) split_launch<false, true, true>(a, s);
+        else if (a.rope == 2) split_launch<false, true, false>(a, s);
+        else split_launch<false, false, false>(a, s);
+    }
+    if (a.Hkv < a.H) launch_fa_dkv_reduce(a, s);
+    return true;
+}

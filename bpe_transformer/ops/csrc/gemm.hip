@@ -141,7 +141,7 @@ gemm_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B
         __syncthreads();
     }
     // epilogue.  MFMA(A-frag, B-frag): column = lane -> output column j, registers -> rows i.
-    if (splits == 1) {
+    if (slab == nullptr) {  // one split straight into C; else fp32 partials (splits > 1, or an fp32 C)
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -169,8 +169,10 @@ gemm_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B
     }
 }
 
-// C = beta*C + sum_s slab[s]  (fixed order -> deterministic); 4 outputs per thread
-__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, __bf16* __restrict__ C,
+// C = beta*C + sum_s slab[s]  (fixed order -> deterministic); 4 outputs per thread.  CT = __bf16 or float (fp32
+// gradient buffers: the sum is added to C without a bf16 rounding)
+template <typename CT>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, CT* __restrict__ C,
                                                             long ldc, float beta, int Mo, int No, int splits) {
     const long total4 = (long)Mo * No / 4;
     for (long t = blockIdx.x * 256L + threadIdx.x; t < total4; t += (long)gridDim.x * 256) {
@@ -181,15 +183,22 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
             const f32x4 v = *reinterpret_cast<const f32x4*>(slab + (long)k * Mo * No + e);
             s += v;
         }
-        u16x4* cp = reinterpret_cast<u16x4*>(C + i * ldc + j);
-        if (beta != 0.f) {
-            const u16x4 c = *cp;
-            s[0] += beta * bf2f(c[0]); s[1] += beta * bf2f(c[1]);
-            s[2] += beta * bf2f(c[2]); s[3] += beta * bf2f(c[3]);
+        if constexpr (sizeof(CT) == 4) {
+            f32x4* cp = reinterpret_cast<f32x4*>(C + i * ldc + j);
+            if (beta != 0.f) s += beta * *cp;
+            *cp = s;
+        } else {
+            u16x4* cp = reinterpret_cast<u16x4*>(C + i * ldc + j);
+            if (beta != 0.f) {
+                const u16x4 c = *cp;
+                s[0] += beta * bf2f(c[0]); s[1] += beta * bf2f(c[1]);
+                s[2] += beta * bf2f(c[2]); s[3] += beta * bf2f(c[3]);
+            }
+            *cp = u16x4{f2bf(s[0]), f2bf(s[1]), f2bf(s[2]), f2bf(s[3])};
         }
-        *cp = u16x4{f2bf(s[0]), f2bf(s[1]), f2bf(s[2]), f2bf(s[3])};
     }
 }
+
 
 
 // ---------------------------------------------------------------------------
@@ -469,7 +478,7 @@ gemm256_tn_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restri
         __builtin_amdgcn_s_barrier();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (splits == 1) {
+    if (slab == nullptr) {  // one split straight into C; else fp32 partials (splits > 1, or an fp32 C)
         for_each_acc(acc, l, [&](int il, int jl, float v) {
             const long i = i0 + wr + il, j = j0 + wc + jl;
             if (beta != 0.f) v += beta * bf2f(*reinterpret_cast<const u16*>(C + i * ldc + j));
@@ -531,14 +540,18 @@ static void launch_g256(const __bf16* a, long lda, const __bf16* b, long ldb, fl
     }
 }
 
-void splitk_reduce(const float* slab, void* C, long ldc, float beta, int M, int N, int splits, hipStream_t s) {
+void splitk_reduce(const float* slab, void* C, long ldc, float beta, int M, int N, int splits, int c_f32,
+                   hipStream_t s) {
     const long total4 = (long)M * N / 4;
     const int g = (int)std::min<long>((total4 + 255) / 256, 2048);
-    splitk_reduce_kernel<<<g, 256, 0, s>>>(slab, (__bf16*)C, ldc, beta, M, N, splits);
+    if (c_f32)
+        splitk_reduce_kernel<float><<<g, 256, 0, s>>>(slab, (float*)C, ldc, beta, M, N, splits);
+    else
+        splitk_reduce_kernel<__bf16><<<g, 256, 0, s>>>(slab, (__bf16*)C, ldc, beta, M, N, splits);
 }
 
 void launch_gemm(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-                 float beta, int Mo, int No, int R, int splits, float* slab, int tile, hipStream_t s) {
+                 float beta, int Mo, int No, int R, int splits, float* slab, int tile, int c_f32, hipStream_t s) {
     const __bf16* a = (const __bf16*)A;
     const __bf16* b = (const __bf16*)B;
     __bf16* c = (__bf16*)C;
@@ -552,5 +565,5 @@ void launch_gemm(int a_kmajor, int b_kmajor, const void* A, long lda, const void
         else { if (b_kmajor) G(false, true); else G(false, false); }
 #undef G
     }
-    if (splits > 1) splitk_reduce(slab, c, ldc, beta, Mo, No, splits, s);
+    if (slab != nullptr) splitk_reduce(slab, C, ldc, beta, Mo, No, splits, c_f32, s);
 }

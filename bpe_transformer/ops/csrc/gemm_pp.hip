@@ -899,18 +899,16 @@ static void launch_pp(const __bf16* a, long lda, const __bf16* b, long ldb, floa
     }
 }
 
-void splitk_reduce(const float* slab, void* C, long ldc, float beta, int M, int N, int splits, hipStream_t s);
-
 void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-                    float beta, int M, int N, int R, int splits, float* slab, hipStream_t s) {
+                    float beta, int M, int N, int R, int splits, float* slab, int c_f32, hipStream_t s) {
     const __bf16* a = (const __bf16*)A;
     const __bf16* b = (const __bf16*)B;
     __bf16* c = (__bf16*)C;
 #define L(AK, BKM, SL) launch_pp<AK, BKM, SL>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s)
-    if (splits > 1) {
+    if (slab != nullptr) {  // splits > 1, or an fp32 C: fp32 partials, then the ordered reduce
         if (a_kmajor) { if (b_kmajor) L(true, true, true); else L(true, false, true); }
         else { if (b_kmajor) L(false, true, true); else L(false, false, true); }
-        splitk_reduce(slab, C, ldc, beta, M, N, splits, s);
+        splitk_reduce(slab, C, ldc, beta, M, N, splits, c_f32, s);
     } else {
         if (a_kmajor) { if (b_kmajor) L(true, true, false); else L(true, false, false); }
         else { if (b_kmajor) L(false, true, false); else L(false, false, false); }

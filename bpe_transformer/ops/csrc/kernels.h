@@ -57,18 +57,20 @@ void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,
                           float margin, int fmt, hipStream_t s);
 
-// gemm.hip
+// gemm.hip.  C is bf16, or fp32 with c_f32 (gradient buffers); slab = fp32 partials [splits][Mo][No], required
+// for splits > 1 or an fp32 C, null otherwise (one split written straight into the bf16 C)
 size_t gemm_lds_bytes();
 bool gemm_shape_ok(int Mo, int No, int R, int splits, int tile);
 void launch_gemm(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-                 float beta, int Mo, int No, int R, int splits, float* slab, int tile, hipStream_t s);
+                 float beta, int Mo, int No, int R, int splits, float* slab, int tile, int c_f32, hipStream_t s);
 
-void splitk_reduce(const float* slab, void* C, long ldc, float beta, int M, int N, int splits, hipStream_t s);
+void splitk_reduce(const float* slab, void* C, long ldc, float beta, int M, int N, int splits, int c_f32,
+                   hipStream_t s);
 
-// gemm_pp.hip (8-wave ping-pong, 256 x 256 x 64 tiles, any operand layout)
+// gemm_pp.hip (8-wave ping-pong, 256 x 256 x 64 tiles, any operand layout); C / slab as launch_gemm
 bool gemm_pp_shape_ok(int M, int N, int R, int splits);
 void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-                    float beta, int M, int N, int R, int splits, float* slab, hipStream_t s);
+                    float beta, int M, int N, int R, int splits, float* slab, int c_f32, hipStream_t s);
 
 void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ldw, void* gu, long ldg, void* act,
                                long lda_, int M, int F, int R, hipStream_t s);
@@ -146,3 +148,7 @@ size_t fa_fwd_lds_bytes(int D);
 size_t fa_bwd_lds_bytes(int D);
 void launch_fa_fwd(const FaArgs& a, hipStream_t s);
 void launch_fa_bwd(const FaArgs& a, hipStream_t s);
+// true when launch_fa_bwd takes the split form for head dim D (no fp32 dQ accumulator, no pre / convert passes)
+bool fa_bwd_split_active(int D);
+// backward form 0 split / 1 fused and the split kernels' waves per workgroup; negative / zero = unchanged
+int fa_bwd_config(int mode, int nw_dq, int nw_dkv);

@@ -304,7 +304,9 @@ void gemm(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor
           int64_t splits, int64_t tile) {
     check_cuda(C, "C");
     TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
-                    C.scalar_type() == at::kBFloat16, "gemm: bf16 operands required");
+                    (C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat),
+                "gemm: bf16 operands and a bf16 or fp32 output required");
+    const bool c32 = C.scalar_type() == at::kFloat;
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
                     C.stride(1) == 1, "gemm: 2-D row-major operands required");
     const int Mo = (int)C.size(0), No = (int)C.size(1);
@@ -319,10 +321,10 @@ void gemm(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor
     TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 && C.stride(0) % 4 == 0, "gemm: 16-byte row alignment");
     DevGuard g(C.device());
     at::Tensor slab;
-    if (splits > 1) slab = at::empty({splits, Mo, No}, C.options().dtype(at::kFloat));
+    if (splits > 1 || c32) slab = at::empty({splits, Mo, No}, C.options().dtype(at::kFloat));
     launch_gemm(a_kmajor, b_kmajor, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
-                (float)beta, Mo, No, R, (int)splits, splits > 1 ? slab.data_ptr<float>() : nullptr, (int)tile,
-                cur_stream());
+                (float)beta, Mo, No, R, (int)splits, slab.defined() ? slab.data_ptr<float>() : nullptr, (int)tile,
+                c32 ? 1 : 0, cur_stream());
 }
 
 // 8-wave ping-pong GEMM (256 x 256 x 64 tiles): same operand convention as gemm(); any layout pair.
@@ -330,7 +332,9 @@ void gemm_pp(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kma
              int64_t splits) {
     check_cuda(C, "C");
     TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
-                    C.scalar_type() == at::kBFloat16, "gemm_pp: bf16 operands required");
+                    (C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat),
+                "gemm_pp: bf16 operands and a bf16 or fp32 output required");
+    const bool c32 = C.scalar_type() == at::kFloat;
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
                     C.stride(1) == 1, "gemm_pp: 2-D row-major operands required");
     TORCH_CHECK(A.device() == C.device() && B.device() == C.device(), "gemm_pp: operands on different devices");
@@ -345,10 +349,10 @@ void gemm_pp(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kma
                 "gemm_pp: leading dimension too large for 32-bit tile offsets");
     DevGuard g(C.device());
     at::Tensor slab;
-    if (splits > 1) slab = at::empty({splits, M, N}, C.options().dtype(at::kFloat));
+    if (splits > 1 || c32) slab = at::empty({splits, M, N}, C.options().dtype(at::kFloat));
     launch_gemm_pp(a_kmajor, b_kmajor, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(),
-                   C.stride(0), (float)beta, M, N, R, (int)splits, splits > 1 ? slab.data_ptr<float>() : nullptr,
-                   cur_stream());
+                   C.stride(0), (float)beta, M, N, R, (int)splits, slab.defined() ? slab.data_ptr<float>() : nullptr,
+                   c32 ? 1 : 0, cur_stream());
 }
 
 // dgu = swiglu_bwd(dy @ w2, gu) with the SwiGLU backward in the GEMM epilogue (da never reaches HBM)
@@ -531,6 +535,12 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
     return {o, lse};
 }
 
+// whether fa_bwd uses (and fa_fwd should zero) the fp32 dQ accumulator for head dim D
+bool fa_bwd_needs_dq_acc(int64_t D) { return !fa_bwd_split_active((int)D); }
+int64_t fa_bwd_config_op(int64_t mode, int64_t nw_dq, int64_t nw_dkv) {
+    return fa_bwd_config((int)mode, (int)nw_dq, (int)nw_dkv);
+}
+
 // Returns dqkv = [B*S, (H + 2*Hkv) * D]: dq | dk | dv in the fused QKV-projection layout.
 at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                   const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cos, const at::Tensor& sin, int64_t B,
@@ -552,9 +562,12 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     auto dqkv = at::empty({B * S, W}, q.options());
     auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
     // rows padded to 64 per batch; zeroed by the forward when it was handed this buffer (fa_fwd dq_acc)
-    const bool pre_zeroed = dq_acc_in.has_value() && dq_acc_in->defined();
+    const bool split = fa_bwd_split_active((int)D);  // the split form needs no fp32 dQ accumulator
+    const bool pre_zeroed = !split && dq_acc_in.has_value() && dq_acc_in->defined();
     if (pre_zeroed) check_dq_acc(*dq_acc_in, q, B, S, H, D);
-    auto dq_acc = pre_zeroed ? *dq_acc_in : at::empty({B * ((S + 63) / 64 * 64), H * D}, q.options().dtype(at::kFloat));
+    at::Tensor dq_acc;
+    if (!split)
+        dq_acc = pre_zeroed ? *dq_acc_in : at::empty({B * ((S + 63) / 64 * 64), H * D}, q.options().dtype(at::kFloat));
     at::Tensor dkv_part;
     if (Hkv < H) dkv_part = at::empty({B * S, H * 2 * D}, q.options().dtype(at::kFloat));
     FaArgs a{};
@@ -565,7 +578,8 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     a.B = (int)B; a.H = (int)H; a.Hkv = (int)Hkv; a.S = (int)S; a.D = (int)D;
     a.causal = causal; a.rope = use_rope ? (prerotated ? 2 : 1) : 0; a.scale = (float)scale;
     a.dout = (const __bf16*)d.data_ptr(); a.ld_do = d.stride(0);
-    a.delta = delta.data_ptr<float>(); a.dq_acc = dq_acc.data_ptr<float>(); a.dq_zeroed = pre_zeroed ? 1 : 0;
+    a.delta = delta.data_ptr<float>(); a.dq_acc = split ? nullptr : dq_acc.data_ptr<float>();
+    a.dq_zeroed = pre_zeroed ? 1 : 0;
     __bf16* base = (__bf16*)dqkv.data_ptr();
     a.dq = base; a.ld_dq = W;
     a.dk = base + H * D; a.dv = base + (H + Hkv) * D; a.ld_dkv = W;
@@ -797,6 +811,8 @@ TORCH_LIBRARY(bpe_hip, m) {
           "int S, int H, int Hkv, int D, bool causal, bool rope, float scale, bool prerotated=False, "
           "Tensor? dq_acc=None) -> Tensor");
     m.def("rope_qk_(Tensor(a!) qkv, Tensor cos, Tensor sin, int B, int S, int H, int Hkv, int D) -> ()");
+    m.def("fa_bwd_needs_dq_acc(int D) -> bool", &fa_bwd_needs_dq_acc);  // no tensors: a catch-all kernel
+    m.def("fa_bwd_config(int mode=-1, int nw_dq=0, int nw_dkv=0) -> int", &fa_bwd_config_op);
 }
 
 TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {

@@ -134,6 +134,13 @@ def _candidates(n: int, k: int, t: int) -> list[str]:
     return c + ["blas"]
 
 
+def _blas_acc(g: Tensor, dy: Tensor, x: Tensor) -> None:
+    if g.dtype == dy.dtype:
+        g.addmm_(dy.t(), x)
+    else:  # fp32 gradient buffer, bf16 activations: fp32 product (no bf16 rounding of dW)
+        g.addmm_(dy.t().to(g.dtype), x.to(g.dtype))
+
+
 def _run(route: str, g: Tensor, dy: Tensor, x: Tensor) -> None:
     n, k = g.shape
     t = dy.shape[0]
@@ -144,15 +151,31 @@ def _run(route: str, g: Tensor, dy: Tensor, x: Tensor) -> None:
     elif route == "hip128":
         ops().gemm(dy, False, x, False, g, 1.0, choose_splits(n, k, t), 128)
     else:
-        g.addmm_(dy.t(), x)
+        _blas_acc(g, dy, x)
+
+
+_warned: set = set()
 
 
 def _tune(key: tuple[int, int, int], cands: list[str], g: Tensor, dy: Tensor, x: Tensor) -> str:
     """Time each route once per shape on a scratch output (CUDA events, 3 reps) and keep the fastest.
 
-    Under ``torch.distributed`` the per-route times are MAX-reduced over the ranks before the choice, so every
-    rank takes the same kernel (every rank reaches the first use of a shape in the same program order).
+    Single process only.  Under ``torch.distributed`` with more than one rank nothing is timed here: a timing
+    inside the backward would need a host sync plus a collective in the middle of the step, and any rank whose
+    environment or table differed would deadlock.  An off-table shape there takes the first HIP candidate (the same
+    choice on every rank: it depends on the shape only) and a warning names the shape to add to
+    ``tuning/dw_routes.json``.
     """
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if key not in _warned:
+            _warned.add(key)
+            import warnings
+
+            warnings.warn(f"dW GEMM shape N,K,T={key} is not in ops/tuning/dw_routes.json; using route "
+                          f"'{cands[0]}' without timing (multi-rank job)", stacklevel=3)
+        return cands[0]
     if not _AUTOTUNE or len(cands) == 1 or torch.cuda.is_current_stream_capturing():
         return cands[0]
     scratch = torch.empty_like(g)
@@ -166,13 +189,6 @@ def _tune(key: tuple[int, int, int], cands: list[str], g: Tensor, dy: Tensor, x:
         e.record()
         e.synchronize()
         times.append(s.elapsed_time(e))
-    import torch.distributed as dist
-
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        on_dev = dist.get_backend() == "nccl"
-        tt = torch.tensor(times, dtype=torch.float64, device=g.device if on_dev else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        times = tt.tolist()
     return cands[min(range(len(cands)), key=lambda i: times[i])]
 
 
@@ -187,7 +203,8 @@ def routes_summary() -> dict[str, str]:
 
 
 def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
-    """``g += dy.T @ x`` (bf16, fp32 accumulation).
+    """``g += dy.T @ x`` (bf16 operands, fp32 accumulation; ``g`` bf16 or fp32 -- an fp32 gradient buffer gets the
+    fp32 sum, through the kernels' fp32 partial slab and ordered reduce).
 
     Routes per shape between the 256-tile HIP kernel, the 128-tile HIP kernel and hipBLASLt; the first call
     for a shape times the candidates (``BPE_GEMM_AUTOTUNE=0``: take the HIP kernel whenever it applies).
@@ -196,17 +213,20 @@ def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
     """
     n, k = g.shape
     t = dy.shape[0]
-    ok = (_ENABLED and g.is_cuda and g.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
+    ok = (_ENABLED and g.is_cuda and g.dtype in (torch.bfloat16, torch.float32) and dy.dtype == torch.bfloat16
           and x.dtype == torch.bfloat16 and g.stride(1) == 1 and dy.stride(1) == 1 and x.stride(1) == 1)
     if not ok:
-        g.addmm_(dy.t(), x)
+        _blas_acc(g, dy, x)
         return
-    key = (n, k, t)
+    key = (n, k, t) if g.dtype == torch.bfloat16 else (n, k, t, 32)
     route = _route.get(key)
     if route is None:
         cands = _candidates(n, k, t)
-        fixed = _static_route.get(key)
-        route = _route[key] = fixed if fixed in cands else _tune(key, cands, g, dy, x)
+        if g.dtype == torch.float32 and len(cands) > 1:
+            cands = cands[:-1]  # the HIP kernels write an fp32 C exactly; the library route would cast
+        key3 = (n, k, t)
+        fixed = _static_route.get(key3)
+        route = _route[key] = fixed if fixed in cands else _tune(key3, cands, g, dy, x)
     _run(route, g, dy, x)
 
 

@@ -66,20 +66,43 @@ class FlatParameters:
             self.slots.append(Slot(name, p, off, n))
             reserve.append(r)
             off += (r + ALIGN - 1) // ALIGN * ALIGN
+        self.used = off  # end of the last slot: the layout up to here does not depend on pad_to
         off = (off + pad_to - 1) // pad_to * pad_to
         self.numel = off
         self.data = torch.zeros(off, dtype=self.dtype, device=self.device)
         self.grad = torch.zeros(off, dtype=grad_dtype or self.dtype, device=self.device)
+        # fp32 gradients for bf16 parameters: ``param.grad`` must match the parameter's dtype, so the flat fp32
+        # slots are not attached as ``.grad``.  Kernels that know the flat buffer accumulate into
+        # ``param.main_grad`` (set by the training engine) directly; a gradient that arrives through autograd's
+        # AccumulateGrad is added into the fp32 slot by a post-accumulate hook and released (registered here,
+        # before any data-parallel hook, so those see the slot already updated).
+        self.split_grad = self.grad.dtype != self.dtype
+        self._hooks = []
         with torch.no_grad():
             for s, r in zip(self.slots, reserve):
                 view = self.data[s.offset : s.offset + s.numel].view_as(s.param)
                 view.copy_(s.param.data)
                 s.param.data = view
-                s.param.grad = self.grad[s.offset : s.offset + s.numel].view_as(s.param)
+                if self.split_grad:
+                    s.param.grad = None
+                    self._hooks.append(s.param.register_post_accumulate_grad_hook(self._fold_grad(s)))
+                else:
+                    s.param.grad = self.grad[s.offset : s.offset + s.numel].view_as(s.param)
                 if r != s.numel:
                     cols = s.param.shape[1]
                     s.param._bpe_padded = self.data[s.offset : s.offset + r].view(r // cols, cols)
                     s.param._bpe_padded_grad = self.grad[s.offset : s.offset + r].view(r // cols, cols)
+
+    def _fold_grad(self, slot: Slot):
+        dst = self.grad[slot.offset : slot.offset + slot.numel]
+
+        def hook(p: Tensor) -> None:
+            if p.grad is not None:
+                with torch.no_grad():
+                    dst.add_(p.grad.reshape(-1))
+                p.grad = None
+
+        return hook
 
     @classmethod
     def from_module(cls, module: nn.Module, grad_dtype: torch.dtype | None = None,
@@ -92,6 +115,8 @@ class FlatParameters:
 
     def zero_grad(self) -> None:
         self.grad.zero_()
+        if self.split_grad:
+            return
         for s in self.slots:  # re-attach in case someone set .grad = None
             if s.param.grad is None or s.param.grad.data_ptr() != self.grad[s.offset :].data_ptr():
                 s.param.grad = self.grad[s.offset : s.offset + s.numel].view_as(s.param)
@@ -180,10 +205,14 @@ class FlatAdamW:
                 self.flat.data[s:e].copy_(self.master[s:e])
 
     def state_dict(self) -> dict:
+        """The flat buffers are saved up to the end of the last parameter (``flat.used``), not with the zero tail
+        that the sharding pad (``pad_to = world x 64``) adds, so a checkpoint resumes on any world size and with
+        or without ZeRO-1."""
+        u = self.flat.used
         return {
             "step": self.step_count, "lr": self.lr, "betas": tuple(self.betas), "eps": self.eps,
-            "weight_decay": self.weight_decay, "master": self.master, "exp_avg": self.exp_avg,
-            "exp_avg_sq": self.exp_avg_sq,
+            "weight_decay": self.weight_decay, "master": self.master[:u], "exp_avg": self.exp_avg[:u],
+            "exp_avg_sq": self.exp_avg_sq[:u],
         }
 
     @torch.no_grad()
@@ -194,8 +223,13 @@ class FlatAdamW:
         self.eps = float(sd["eps"])
         self.weight_decay = float(sd["weight_decay"])
         self._build_segments()  # the per-segment decay follows the restored value
-        self.master.copy_(sd["master"])
-        self.exp_avg.copy_(sd["exp_avg"])
-        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        for name, buf in (("master", self.master), ("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
+            src = sd[name].reshape(-1)
+            n = min(src.numel(), buf.numel())
+            if src.numel() < self.flat.used:
+                raise ValueError(f"optimizer state '{name}' has {src.numel()} elements, the model needs "
+                                 f"{self.flat.used}")
+            buf[:n].copy_(src[:n])  # older checkpoints may carry a padded tail: only the zero pad differs
+            buf[n:].zero_()
         if self.master is not self.flat.data:
             self.flat.data.copy_(self.master)

@@ -17,6 +17,10 @@ MI355X / RCCL-over-xGMI design:
     amortise launch latency while still leaving several buckets to overlap.
   * Averaging uses ``ReduceOp.AVG`` on RCCL (no extra scaling pass); on gloo
     (CPU tests) SUM + divide.
+  * ``comm_dtype``: the wire / reduction dtype when it differs from the gradient buffer's.  bf16 gradients
+    reduced as fp32 (each bucket cast into an fp32 staging slice before its collective and back after the wait)
+    are summed across the ring without a bf16 rounding at every hop, for 2x the bytes; fp32 gradients (grad
+    accumulation) reduced as bf16 halve the bytes.  Default: the gradient dtype.
 """
 
 from __future__ import annotations
@@ -32,8 +36,12 @@ from ..optim.flat import FlatParameters
 
 class BucketedAllReduce:
     def __init__(self, flat: FlatParameters, bucket_mb: float = 64.0, process_group=None, overlap: bool = True,
-                 average: bool = True):
+                 average: bool = True, comm_dtype: torch.dtype | None = None):
         self.flat = flat
+        self.comm_dtype = comm_dtype or flat.grad.dtype
+        # staging buffer for a wire dtype other than the gradient's (one flat buffer, sliced like the buckets)
+        self._cbuf = (torch.empty(flat.numel, dtype=self.comm_dtype, device=flat.grad.device)
+                      if self.comm_dtype != flat.grad.dtype else None)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.average = average
@@ -91,6 +99,9 @@ class BucketedAllReduce:
             return
         s, e = self.buckets[b]
         view = self.flat.grad[s:e]
+        if self._cbuf is not None:
+            self._cbuf[s:e].copy_(view)  # on the stream that produced the gradients: ordered after them
+            view = self._cbuf[s:e]
         op = dist.ReduceOp.AVG if (self.average and self._use_avg) else dist.ReduceOp.SUM
         if view.is_cuda and streams.enabled(view):
             # weight gradients may be written on the side stream (ops/streams.py): issue the collective from
@@ -116,6 +127,8 @@ class BucketedAllReduce:
                 self._launch(b)
         for w in self._works:
             w.wait()
+        if self._cbuf is not None:
+            self.flat.grad.copy_(self._cbuf)
         if self.average and not self._use_avg:
             self.flat.grad.div_(self.world)
         self._works = [None] * len(self.buckets)

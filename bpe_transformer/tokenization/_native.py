@@ -4,10 +4,8 @@ from __future__ import annotations
 
 import importlib
 
-try:
-    from . import _bpe_native as native  # noqa: F401
-except ImportError:  # not built yet: compile (g++, seconds) and import
-    from ._native_build import build
+from ._native_build import build, is_fresh
 
+if not is_fresh():  # not built, or built from other sources (content stamp): compile (g++, seconds) first
     build()
-    native = importlib.import_module("bpe_transformer.tokenization._bpe_native")
+native = importlib.import_module("bpe_transformer.tokenization._bpe_native")

@@ -2,12 +2,15 @@
 
 ``python -m bpe_transformer.tokenization._native_build`` compiles
 ``csrc/tokenizer/bpe_native.cpp`` with g++ (-O3, C++20, pthreads) into
-``bpe_transformer/tokenization/_bpe_native<ext-suffix>``.  Incremental: only
-rebuilds when the sources are newer than the library.
+``bpe_transformer/tokenization/_bpe_native<ext-suffix>``.  Incremental by CONTENT:
+the library carries a stamp (``<lib>.stamp``) with the sha256 of the compile
+command and every source / header; a mismatch (sources edited, whatever their
+mtimes) rebuilds, and ``_native.py`` checks the stamp before importing.
 """
 
 from __future__ import annotations
 
+import hashlib
 import subprocess
 import sys
 import sysconfig
@@ -20,24 +23,49 @@ SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 LIB = HERE / f"_bpe_native{SUFFIX}"
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
+STAMP = LIB.with_name(LIB.name + ".stamp")
+
+
+def _cmd() -> tuple[list[str], list[Path]]:
     import pybind11
 
     srcs = [SRC_DIR / "bpe_native.cpp"]
-    deps = srcs + list(SRC_DIR.glob("*.h"))
-    if not force and LIB.exists() and all(d.stat().st_mtime <= LIB.stat().st_mtime for d in deps):
-        return LIB
     cmd = [
         "g++", "-O3", "-std=c++20", "-shared", "-fPIC", "-pthread", "-fvisibility=hidden",
         "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], "-I", str(SRC_DIR),
         *map(str, srcs), "-o", str(LIB),
     ]
+    return cmd, srcs + sorted(SRC_DIR.glob("*.h"))
+
+
+def digest() -> str:
+    """sha256 of the compile flags (not the paths: the tree is copied elsewhere to run) and every source."""
+    cmd, deps = _cmd()
+    h = hashlib.sha256("\0".join(c for c in cmd if c.startswith("-") and c not in ("-I", "-o")).encode())
+    for d in deps:
+        h.update(d.name.encode() + b"\0" + d.read_bytes())
+    return h.hexdigest()
+
+
+def is_fresh() -> bool:
+    try:
+        return LIB.exists() and STAMP.read_text().strip() == digest()
+    except OSError:
+        return False
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if not force and is_fresh():
+        return LIB
+    cmd, _ = _cmd()
+    STAMP.unlink(missing_ok=True)
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("building the native tokenizer failed")
+    STAMP.write_text(digest() + "\n")
     return LIB
 
 

@@ -31,7 +31,19 @@ _SCALARS = {
 
 
 def loads(data: bytes):
-    """Decode a pickle of builtin containers of ints / bytes / str / floats; raise on anything else."""
+    """Decode a pickle of builtin containers of ints / bytes / str / floats; raise on anything else.
+
+    Every failure -- a refused opcode, or a malformed / hostile stream (GET before PUT, an empty stack or mark
+    stack, an unhashable dict key, SETITEM on a list, a truncated opcode) -- raises :class:`UnsafePickleError`."""
+    try:
+        return _loads(data)
+    except UnsafePickleError:
+        raise
+    except (KeyError, IndexError, TypeError, AttributeError, ValueError, EOFError) as e:
+        raise UnsafePickleError(f"malformed pickle ({type(e).__name__}: {e})") from None
+
+
+def _loads(data: bytes):
     stack: list = []
     marks: list[int] = []
     memo: dict[int, object] = {}
@@ -83,6 +95,8 @@ def loads(data: bytes):
             stack[-1].extend(items)
         elif name in _TUPLE_N:
             n = _TUPLE_N[name]
+            if len(stack) < n:
+                raise UnsafePickleError(f"malformed pickle: {name} on a stack of {len(stack)}")
             t = tuple(stack[-n:])
             del stack[-n:]
             stack.append(t)

@@ -61,6 +61,22 @@ class TrainConfig:
     nan_guard: bool = True
     ddp_check_every: int = 0  # >0: every N steps assert bit-identical grads / weights across DP ranks
     zero: int = 0  # 1: sharded data parallelism (reduce-scatter + 1/N AdamW + all-gather, parallel/zero.py)
+    # flat gradient buffer dtype: auto (fp32 when grad_accum > 1, so the micro-batch sum is not rounded to bf16
+    # every add; else the parameter dtype) | bf16 | fp32
+    grad_dtype: str = "auto"
+    comm_dtype: str = "auto"  # data-parallel all-reduce dtype: auto (= grad dtype) | bf16 | fp32
+
+    def resolved_grad_dtype(self, param_dtype):
+        import torch
+
+        if self.grad_dtype == "auto":
+            return torch.float32 if (self.grad_accum > 1 and param_dtype == torch.bfloat16) else None
+        return {"bf16": torch.bfloat16, "fp32": torch.float32}[self.grad_dtype]
+
+    def resolved_comm_dtype(self):
+        import torch
+
+        return None if self.comm_dtype == "auto" else {"bf16": torch.bfloat16, "fp32": torch.float32}[self.comm_dtype]
 
     def to_dict(self) -> dict:
         d = dataclasses.asdict(self)

@@ -39,7 +39,13 @@ class TrainEngine:
         time_phases: bool = False,
         ddp_check_every: int = 0,
         zero: int = 0,
+        grad_dtype: torch.dtype | None = None,
+        comm_dtype: torch.dtype | None = None,
     ):
+        """``grad_dtype``: dtype of the flat gradient buffer (default: the parameters', bf16 on the GPU path);
+        fp32 keeps the weight gradients -- and their sum over grad-accumulation micro-batches -- unrounded
+        (the dW kernels write fp32 through their partial slab).  ``comm_dtype``: the data-parallel all-reduce
+        dtype (default: the gradient dtype; ``parallel/ddp.py``)."""
         self.model = model
         self.dist = dist_info or DistInfo()
         # zero=1: sharded data parallelism (parallel/zero.py) -- reduce-scatter, 1/N of the AdamW work,
@@ -48,7 +54,7 @@ class TrainEngine:
         # the RCCL calls on one GPU)
         self.zero = int(zero) if (self.dist.world_size > 1 or (zero and torch.distributed.is_initialized())) else 0
         pad = self.dist.world_size * ALIGN if self.zero else ALIGN
-        self.flat = FlatParameters.from_module(model, pad_to=pad)
+        self.flat = FlatParameters.from_module(model, grad_dtype=grad_dtype, pad_to=pad)
         for slot in self.flat.slots:  # fused blocks accumulate weight grads straight into the flat buffer
             slot.param.main_grad = self.flat.grad_view(slot).view_as(slot.param)
         self.opt = FlatAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
@@ -56,7 +62,7 @@ class TrainEngine:
         self.ddp = None
         if self.dist.world_size > 1 or self.zero:
             self.ddp = (ShardedDataParallel(self.flat, bucket_mb=bucket_mb) if self.zero
-                        else BucketedAllReduce(self.flat, bucket_mb=bucket_mb))
+                        else BucketedAllReduce(self.flat, bucket_mb=bucket_mb, comm_dtype=comm_dtype))
         if self.ddp is not None:
             self.ddp.broadcast_parameters(0)
             self.opt.master.copy_(self.flat.data)  # keep fp32 master == broadcast weights

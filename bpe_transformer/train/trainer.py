@@ -65,7 +65,9 @@ class Trainer:
         self.engine = TrainEngine(self.model, self.info, lr=o.lr, betas=o.betas, eps=o.eps,
                                   weight_decay=o.weight_decay, max_grad_norm=o.max_grad_norm,
                                   bucket_mb=cfg.bucket_mb, time_phases=cfg.phase_timing,
-                                  ddp_check_every=cfg.ddp_check_every, zero=cfg.zero)
+                                  ddp_check_every=cfg.ddp_check_every, zero=cfg.zero,
+                                  grad_dtype=cfg.resolved_grad_dtype(next(self.model.parameters()).dtype),
+                                  comm_dtype=cfg.resolved_comm_dtype())
         self.schedule = CosineSchedule(o.lr, o.min_lr, o.warmup_iters, o.cosine_cycle_iters or cfg.max_iters)
         ctx = cfg.model.context_length
         if cfg.data.train_path:

@@ -37,6 +37,8 @@
 #include <stdexcept>
 #include <string>
 #include <string_view>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <utility>
@@ -488,8 +490,29 @@ struct Encoder {
     std::unordered_map<uint64_t, std::pair<int32_t, int32_t>> ranks;  // (a,b) -> (rank, merged id)
     SpecialSplitter specials;
     std::vector<int32_t> special_ids;
-    std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>> cache;
+    using Cache = std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>>;
+    Cache cache;  // the calling thread's pre-token cache (worker 0 of every threaded call)
+    // persistent caches of workers 1.. of the threaded calls: a 4 MiB encode_iterable batch then starts warm
+    // instead of with an empty map per thread per call (the pre-token vocabulary of a corpus is small)
+    std::vector<std::unique_ptr<Cache>> worker_cache;
+    std::mutex mu;  // one call at a time per Encoder (calls release the GIL; the caches are not shared-safe)
     size_t cache_limit = 1 << 20;
+
+    Cache& cache_of(int t) {
+        if (t == 0) return cache;
+        while ((int)worker_cache.size() < t) worker_cache.emplace_back(new Cache());
+        return *worker_cache[t - 1];
+    }
+
+    // run fn(worker, cache) on nthreads threads (the caller is worker 0), each with its own persistent cache
+    template <typename F> void run_workers(int nthreads, F&& fn) {
+        nthreads = std::max(1, nthreads);
+        for (int t = 1; t < nthreads; ++t) cache_of(t);  // allocate before the threads start
+        std::vector<std::thread> th;
+        for (int t = 1; t < nthreads; ++t) th.emplace_back([&, t]() { fn(cache_of(t)); });
+        fn(cache);
+        for (auto& x : th) x.join();
+    }
 
     Encoder(const std::unordered_map<int32_t, std::string>& vocab, const std::vector<std::pair<std::string, std::string>>& mg,
             const std::vector<std::string>& sp)
@@ -605,18 +628,13 @@ struct Encoder {
         const int nc = (int)b.size() - 1;
         std::vector<std::vector<int32_t>> parts(nc);
         std::atomic<int> nextc{0};
-        auto work = [&]() {
-            std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>> local;
+        run_workers(nthreads, [&](Cache& local) {
             for (;;) {
                 const int c = nextc.fetch_add(1);
                 if (c >= nc) break;
                 encode_into(std::string_view(text.data() + b[c], b[c + 1] - b[c]), parts[c], local);
             }
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < nthreads; ++t) th.emplace_back(work);
-        work();
-        for (auto& x : th) x.join();
+        });
         size_t total = 0;
         for (auto& p : parts) total += p.size();
         std::vector<int32_t> out;
@@ -756,6 +774,7 @@ PYBIND11_MODULE(_bpe_native, m) {
             std::vector<int32_t> out;
             {
                 py::gil_scoped_release nogil;
+                std::lock_guard<std::mutex> lk(e.mu);
                 e.encode_into(s, out, e.cache);
             }
             return out;
@@ -765,6 +784,7 @@ PYBIND11_MODULE(_bpe_native, m) {
             std::vector<int32_t> out;
             {
                 py::gil_scoped_release nogil;
+                std::lock_guard<std::mutex> lk(e.mu);
                 out = e.encode_parallel(s, nthreads);
             }
             return py::array_t<int32_t>(out.size(), out.data());
@@ -773,19 +793,15 @@ PYBIND11_MODULE(_bpe_native, m) {
             std::vector<std::vector<int32_t>> outs(texts.size());
             {
                 py::gil_scoped_release nogil;
+                std::lock_guard<std::mutex> lk(e.mu);
                 std::atomic<size_t> nx{0};
-                auto work = [&]() {
-                    std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>> local;
+                e.run_workers(std::min<int>(nthreads, (int)texts.size()), [&](Encoder::Cache& local) {
                     for (;;) {
                         const size_t i = nx.fetch_add(1);
                         if (i >= texts.size()) break;
                         e.encode_into(texts[i], outs[i], local);
                     }
-                };
-                std::vector<std::thread> th;
-                for (int t = 1; t < std::max(1, nthreads); ++t) th.emplace_back(work);
-                work();
-                for (auto& x : th) x.join();
+                });
             }
             return outs;
         })
@@ -794,19 +810,15 @@ PYBIND11_MODULE(_bpe_native, m) {
             std::vector<std::vector<int32_t>> outs(texts.size());
             {
                 py::gil_scoped_release nogil;
+                std::lock_guard<std::mutex> lk(e.mu);
                 std::atomic<size_t> nx{0};
-                auto work = [&]() {
-                    std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>> local;
+                e.run_workers(std::min<int>(nthreads, (int)texts.size()), [&](Encoder::Cache& local) {
                     for (;;) {
                         const size_t i = nx.fetch_add(1);
                         if (i >= texts.size()) break;
                         e.encode_into(texts[i], outs[i], local);
                     }
-                };
-                std::vector<std::thread> th;
-                for (int t = 1; t < std::max(1, nthreads); ++t) th.emplace_back(work);
-                work();
-                for (auto& x : th) x.join();
+                });
             }
             std::vector<int64_t> off(texts.size() + 1, 0);
             for (size_t i = 0; i < outs.size(); ++i) off[i + 1] = off[i] + (int64_t)outs[i].size();
@@ -821,12 +833,22 @@ PYBIND11_MODULE(_bpe_native, m) {
                 py::gil_scoped_release nogil;
                 std::string raw = read_file(path);
                 std::string s = sanitize_utf8(raw.data(), raw.size());
+                std::lock_guard<std::mutex> lk(e.mu);
                 out = e.encode_parallel(s, nthreads);
             }
             return py::array_t<int32_t>(out.size(), out.data());
         })
         .def("decode", [](const Encoder& e, const std::vector<int64_t>& ids) { return py::bytes(e.decode(ids)); })
         .def("cache_size", [](const Encoder& e) { return e.cache.size(); })
-        .def("clear_cache", [](Encoder& e) { e.cache.clear(); });
+        .def("worker_cache_sizes", [](const Encoder& e) {
+            std::vector<size_t> n;
+            for (auto& c : e.worker_cache) n.push_back(c->size());
+            return n;
+        })
+        .def("clear_cache", [](Encoder& e) {
+            std::lock_guard<std::mutex> lk(e.mu);
+            e.cache.clear();
+            e.worker_cache.clear();
+        });
 }
 #endif  // BPE_NATIVE_NO_PYTHON

@@ -8,6 +8,8 @@ pure-Python GPT-2 BPE over the same vocab/merges fixtures.
 from __future__ import annotations
 
 import io
+import os
+from pathlib import Path
 import pickle
 
 import pytest
@@ -223,3 +225,113 @@ def test_encode_iterable_memory_is_bounded(tok, workers):
     assert abs(n - reps * expect) <= reps  # chunk cuts may merge a boundary token differently at most once each
     limit = (1 << 20) if workers is None else (24 << 20)
     assert peak < limit, peak
+
+
+_RLIMIT_CHILD = r"""
+import os, resource, sys
+sys.path.insert(0, sys.argv[1])
+from bpe_transformer.tokenization.bpe_tokenizer import BPETokenizer
+
+sample_dir, workers, headroom_mb, stream_mb = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+tok = BPETokenizer.from_files(os.path.join(sample_dir, "sample_tokenizer", "vocab.pkl"),
+                              os.path.join(sample_dir, "sample_tokenizer", "merges.pkl"), ["<|endoftext|>"])
+with open(os.path.join(sample_dir, "tinystories_sample.txt"), encoding="utf-8") as f:
+    lines = f.read().splitlines(keepends=True)
+per = sum(len(x) for x in lines)
+reps = (stream_mb << 20) // per + 1
+expect = len(tok.encode("".join(lines)))
+tok.encode("".join(lines) * 4)  # warm every lazily built structure before the limit
+if workers > 1:
+    list(tok.encode_iterable(iter(lines * 64), n_workers=workers))  # and the worker threads' caches
+
+
+def vm_bytes():
+    with open("/proc/self/status") as f:
+        for ln in f:
+            if ln.startswith("VmSize:"):
+                return int(ln.split()[1]) * 1024
+
+
+limit = vm_bytes() + (headroom_mb << 20)
+resource.setrlimit(resource.RLIMIT_AS, (limit, limit))
+try:  # the limit bites: one allocation of the headroom (+ 8 MB of slack for pages freed since) must fail
+    bytearray((headroom_mb + 8) << 20)
+    print("LIMIT_NOT_EFFECTIVE")
+    sys.exit(3)
+except MemoryError:
+    pass
+
+
+def stream():
+    for _ in range(reps):
+        yield from lines
+
+
+n = 0
+for _ in tok.encode_iterable(stream(), n_workers=workers if workers > 1 else None):
+    n += 1
+assert abs(n - reps * expect) <= reps, (n, reps * expect)
+print("OK", n, reps)
+"""
+
+
+@pytest.mark.parametrize("workers,headroom_mb", [(1, 40), (4, 64)])
+def test_encode_iterable_rlimit_address_space(tmp_path, workers, headroom_mb):
+    """The reference's ``test_encode_iterable_memory_usage`` with a real address-space limit (RLIMIT_AS,
+    ``/root/reference/tests/test_tokenizer.py:19-36,416-446``), which -- unlike tracemalloc -- also bounds the C++
+    core's allocations.  A fresh interpreter (tokenizer only, no torch) warms up, caps its address space at the
+    current size + ``headroom`` (checked to bite: one allocation of the headroom + 8 MB fails), then streams a generated
+    96 MB text through ``encode_iterable``: any O(text) buffer, Python or native, would exceed the cap.  Worker
+    threads get 1 MB stacks (RLIMIT_STACK before exec) and one malloc arena, so thread reservations stay small."""
+    import resource
+    import subprocess
+    import sys
+
+    if not sys.platform.startswith("linux"):
+        pytest.skip("RLIMIT_AS is Linux-specific")
+    root = Path(__file__).resolve().parents[1]
+    script = tmp_path / "child.py"
+    script.write_text(_RLIMIT_CHILD)
+
+    def small_stacks():
+        resource.setrlimit(resource.RLIMIT_STACK, (1 << 20, 1 << 20))
+
+    env = dict(os.environ, MALLOC_ARENA_MAX="1", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, str(script), str(root), str(FIXTURES), str(workers), str(headroom_mb), "96"],
+                       capture_output=True, text=True, timeout=600, env=env, preexec_fn=small_stacks)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), (r.stdout[-500:], r.stderr[-2000:])
+
+
+def test_safe_pickle_malformed_streams_raise_unsafe_error():
+    """Malformed or hostile opcode streams raise UnsafePickleError (a ValueError), never a bare KeyError /
+    IndexError / TypeError / AttributeError, so a caller rejecting bad artifacts by that type catches them all."""
+    import random
+
+    from bpe_transformer.tokenization import safe_pickle
+
+    P = pickle
+    bad = [
+        b"\x80\x04h\x00.",                       # BINGET before any PUT
+        b"\x80\x04s.",                           # SETITEM on an empty stack
+        b"\x80\x04]K\x01K\x02s.",                # SETITEM on a list
+        b"\x80\x04}]K\x01s.",                    # unhashable (list) dict key
+        b"\x80\x04}K\x01a.",                     # APPEND on a dict
+        b"\x80\x04e.",                           # APPENDS with no MARK
+        b"\x80\x04\x86.",                        # TUPLE2 on an empty stack
+        b"\x80\x04K\x01K\x02",                   # no STOP
+        b"\x80\x04",                             # truncated
+    ]
+    good = P.dumps({1: [(b"a", b"b")], 2: "x"}, protocol=4)
+    rng = random.Random(0)
+    for _ in range(300):  # random single-byte corruptions and truncations of a valid stream
+        d = bytearray(good)
+        if rng.random() < 0.5:
+            d[rng.randrange(len(d))] = rng.randrange(256)
+        else:
+            d = d[: rng.randrange(len(d))]
+        bad.append(bytes(d))
+    for data in bad:
+        try:
+            safe_pickle.loads(data)
+        except safe_pickle.UnsafePickleError:
+            pass

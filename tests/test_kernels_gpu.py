@@ -507,9 +507,62 @@ def test_flash_attention_gpt2_shape(gpu_device):
     assert rel(g.cpu(), gr) < 3e-2
 
 
+@pytest.fixture
+def fused_bwd():
+    """Run the test with the fused (fp32-atomics) attention backward, the one that owns the dQ accumulator and the
+    pre-pass / convert kernels (D = 64 defaults to the split form, csrc/flash_attn_bwd_split.hip)."""
+    h = torch.ops.bpe_hip
+    prev = h.fa_bwd_config(1, 0, 0)
+    yield
+    h.fa_bwd_config(prev, 0, 0)
+
+
+@pytest.mark.parametrize("S", [1024, 200, 64, 1000])
+@pytest.mark.parametrize("H,Hkv", [(4, 4), (8, 2)])
+@pytest.mark.parametrize("rope", ["fused", "prerotated", None])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("nw", [(4, 4), (8, 8)])
+def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal, nw):
+    """The split backward (dQ kernel + dK/dV kernel) at 4 and 8 waves per workgroup against the fp32 oracle's
+    autograd and against the fused atomics backward on the same forward outputs: dQ, dK, dV each."""
+    h = torch.ops.bpe_hip
+    B, D = 2, 64
+    torch.manual_seed(11)
+    qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device=gpu_device, dtype=torch.bfloat16)
+    use_rope = rope is not None
+    cos, sin = R.rope_tables(D, S + 5, 10000.0, device=gpu_device)
+    pre = rope == "prerotated"
+    x = qkv.clone()
+    if pre:
+        h.rope_qk_(x, cos, sin, B, S, H, Hkv, D)
+    q, k, v = x[:, : H * D], x[:, H * D : (H + Hkv) * D], x[:, (H + Hkv) * D :]
+    scale = D ** -0.5
+    o, lse = h.fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)
+    do = torch.randn_like(o)
+    prev = h.fa_bwd_config(0, nw[0], nw[1])
+    try:
+        got = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)
+        again = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)
+        h.fa_bwd_config(1, 0, 0)
+        fused = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)
+    finally:
+        h.fa_bwd_config(prev, 4, 4)
+    assert torch.equal(got, again), "split backward is not deterministic"
+    qr = qkv.float().cpu().requires_grad_(True)
+    orf = ops.attention_qkv_reference(qr, B, S, H, Hkv, D, cos.cpu() if use_rope else None,
+                                      sin.cpu() if use_rope else None, causal)
+    orf.backward(do.float().cpu())
+    gr = qr.grad
+    HD, KD = H * D, Hkv * D
+    for name, sl in (("dq", slice(0, HD)), ("dk", slice(HD, HD + KD)), ("dv", slice(HD + KD, HD + 2 * KD))):
+        e = rel(got[:, sl].float().cpu(), gr[:, sl])
+        ef = rel(fused[:, sl].float().cpu(), gr[:, sl])
+        assert e < 3e-2 and e < 1.5 * ef + 1e-3, (name, e, ef)
+
+
 @pytest.mark.parametrize("S,D,H,Hkv,fused", [(1000, 64, 4, 4, False), (192, 128, 8, 4, True), (64, 64, 4, 2, True),
                                               (320, 64, 4, 4, True)])
-def test_flash_dq_acc_zeroed_by_forward(gpu_device, S, D, H, Hkv, fused):
+def test_flash_dq_acc_zeroed_by_forward(gpu_device, S, D, H, Hkv, fused, fused_bwd):
     """fa_fwd handed the backward's fp32 dQ accumulator (filled with NaN here) zeroes every row of it,
     padding included, and fa_bwd then skips its own zeroing: the gradients equal those of the path where the
     backward pre-pass zeroes (the fused blocks use this form) -- dK / dV bitwise, dQ up to the order of its fp32
@@ -533,7 +586,7 @@ def test_flash_dq_acc_zeroed_by_forward(gpu_device, S, D, H, Hkv, fused):
     assert rel(got[:, : H * D].cpu(), ref[:, : H * D].float().cpu()) < 1e-3  # dQ: fp32 atomics, order varies
 
 
-def test_flash_bwd_streaming_path_matches(gpu_device):
+def test_flash_bwd_streaming_path_matches(gpu_device, fused_bwd):
     """Past 128 MB of bf16 activation the backward's pre-pass / dQ-convert kernels switch to non-temporal loads
     (csrc/flash_attn_bwd.hip big_stream).  Batch 96 at the GPT-2 shape takes that path; its gradients must
     equal those of two 48-sequence halves, which take the plain path: dK / dV bitwise, dQ up to atomic order."""
