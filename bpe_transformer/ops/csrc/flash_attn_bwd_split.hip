@@ -10,17 +10,19 @@
 // kernels that each own their output, so nothing is summed across workgroups:
 //
 //   fa_bwd_dq_kernel   (query-major, first):  delta = rowsum(dO * O) for its queries (written for the second
-//       kernel), then per 64-key tile  S^T = K.Q^T,  dP^T = V.dO^T - delta,  P^T = exp2(S^T * c - lse),
+//       kernel), then per 64-key tile  S^T = K.(cQ)^T - lse,  dP^T = V.dO^T - delta,  P^T = exp2(S^T),
 //       dS^T = P^T * dP^T,  dQ^T += K^T.dS^T.   Q and dO are the lane-resident B operands (query on the lane),
 //       pinned in registers for the whole key sweep; K / V tiles are staged in LDS (register staging, guide
 //       T14: loads of tile t+1 issued before tile t's MFMAs, written after them; one barrier per tile).  dS^T
 //       is the B operand of the dQ^T product straight from its accumulator (guide §3).  dQ is scaled,
 //       un-rotated (RoPE) and written as bf16 in the epilogue.
-//   fa_bwd_dkv_kernel  (key-major):  per 64-query tile  S = Q.K^T - lse/c,  dP = dO.V^T - delta (row constants
-//       as the initial accumulators), P = exp2(c S), dS = P dP,  dV^T += dO^T.P,  dK^T += Q^T.dS.  K and V are
+//   fa_bwd_dkv_kernel  (key-major):  per 64-query tile  S = Q.(cK)^T - lse,  dP = dO.V^T - delta (row constants
+//       as the initial accumulators), P = exp2(S), dS = P dP,  dV^T += dO^T.P,  dK^T += Q^T.dS.  K and V are
 //       the pinned B operands (key on the lane); Q / dO rows and their transposed reads come from one LDS image
 //       (fa_common.h).  No dS LDS round trip, no second barrier, no atomics.
 //
+// c = softmax scale * log2(e) is folded into the pinned operand (Q in the dQ kernel, as in the forward; K in the
+// dK/dV kernel, whose Q also feeds dK), so the only VALU between an S accumulator and its exponential is none.
 // The price is the recomputation of S and dP in the dQ kernel (7 MFMA products instead of 5); in exchange the
 // atomics floor, the 402 MB/layer accumulator (4.8 GB at GPT-2 B 128), the zeroing and the two side passes go.
 // GQA: the dK / dV kernel runs per query head and writes fp32 partials summed by fa_dkv_reduce_kernel.
@@ -68,7 +70,14 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     for (int ks = 0; ks < KS; ++ks) {
         const int d0 = 16 * ks + 8 * hh;
         u16x8 tq = *reinterpret_cast<const u16x8*>(Q + qrow * ld_q + (long)h * D + d0);
-        if (ROPE_IN) tq = rope_u16x8(tq, cosT + qc * (D / 2) + d0 / 2, sinT + qc * (D / 2) + d0 / 2, 1.f);
+        // softmax scale * log2(e) folded into the pinned Q (as the forward does): S^T comes out in log2 units
+        if (ROPE_IN) {
+            tq = rope_u16x8(tq, cosT + qc * (D / 2) + d0 / 2, sinT + qc * (D / 2) + d0 / 2, scale_log2);
+        } else {
+            float x[8];
+            unpack8(tq, x);
+            tq = pack8(x, scale_log2);
+        }
         qf[ks] = __builtin_bit_cast(bf16x8, tq);
         const u16x8 tg = *reinterpret_cast<const u16x8*>(dO + qrow * ld_do + (long)h * D + d0);
         const u16x8 to = *reinterpret_cast<const u16x8*>(O + qrow * ld_o + (long)h * D + d0);
@@ -79,10 +88,15 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     dsum += __shfl_xor(dsum, 32, 64);
     if (q_ok && hh == 0) DELTA[((long)b * H + h) * S + q] = dsum;
     const float lse = LSE[((long)b * H + h) * S + qc];
-    const float nl = (q_ok && lse < INFINITY) ? -lse : -INFINITY;  // P = exp2(S c - lse); 0 for empty / pad rows
-    f32x16 nd;                                                       // dP^T starts at -delta (row constant)
+    // row constants as the initial accumulators (query = lane): S^T starts at -lse, so P = exp2(S^T) with no
+    // VALU before the exponential (-inf for empty / pad rows: P = 0); dP^T starts at -delta
+    const float nl = (q_ok && lse < INFINITY) ? -lse : -INFINITY;
+    f32x16 ns, nd;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) nd[r] = -dsum;
+    for (int r = 0; r < 16; ++r) {
+        ns[r] = nl;
+        nd[r] = -dsum;
+    }
 
     f32x16 acc[2];
 #pragma unroll
@@ -136,9 +150,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 #pragma unroll
             for (int kh = 0; kh < 2; ++kh) {
                 if (CAUSAL && k0 + 32 * kh > qw + 31) break;  // this 32-key half is past every query of the wave
-                f32x16 sp, dp = nd;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sp[r] = 0.f;
+                f32x16 sp = ns, dp = nd;
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks) {
                     const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
@@ -150,13 +162,13 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int key = k0 + 32 * kh + acc_row(r, hh);
-                        const float p = fast_exp2(fmaf(sp[r], scale_log2, nl));
+                        const float p = fast_exp2(sp[r]);
                         const bool ok = key < S && (!CAUSAL || key <= q);
                         dp[r] = ok ? p * dp[r] : 0.f;
                     }
                 } else {
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(fmaf(sp[r], scale_log2, nl)) * dp[r];
+                    for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(sp[r]) * dp[r];
                 }
                 // dQ^T += K^T.dS^T: registers 8s..8s+7 are k-step s (keys 16 s ..) in the MFMA's permuted order
 #pragma unroll
@@ -233,9 +245,22 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const int d0 = 16 * ks + 8 * hh;
-            u16x8 tk = key_ok ? *reinterpret_cast<const u16x8*>(kp + d0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-            const u16x8 tv = key_ok ? *reinterpret_cast<const u16x8*>(vp + d0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-            if (ROPE_IN) tk = rope_u16x8(tk, cosT + kpos * (D / 2) + d0 / 2, sinT + kpos * (D / 2) + d0 / 2, 1.f);
+            // unconditional loads (kpos is clamped) consumed by a VALU select here: the wait for them then sits in
+            // this prologue.  (As a branch around the loads, the wait-count pass placed a vmcnt(0) before the first
+            // use of V inside the tile loop -- draining the next tile's prefetch in every half-tile.)
+            u16x8 tk = *reinterpret_cast<const u16x8*>(kp + d0);
+            u16x8 tv = *reinterpret_cast<const u16x8*>(vp + d0);
+            const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+            tk = key_ok ? tk : z;
+            tv = key_ok ? tv : z;
+            // softmax scale * log2(e) folded into the pinned K: S comes out in log2 units
+            if (ROPE_IN) {
+                tk = rope_u16x8(tk, cosT + kpos * (D / 2) + d0 / 2, sinT + kpos * (D / 2) + d0 / 2, scale_log2);
+            } else {
+                float x[8];
+                unpack8(tk, x);
+                tk = pack8(x, scale_log2);
+            }
             kf[ks] = __builtin_bit_cast(bf16x8, tk);
             vf[ks] = __builtin_bit_cast(bf16x8, tv);
         }
@@ -282,9 +307,9 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
             *reinterpret_cast<u16x8*>(Qs + buf * TILE + swz<RB>(r, c)) = qv;
             *reinterpret_cast<u16x8*>(dOs + buf * TILE + swz<RB>(r, c)) = ov;
         }
-        if (tid < 64) {  // the S / dP accumulators' starting values: -lse / c and -delta
+        if (tid < 64) {  // the S / dP accumulators' starting values: -lse and -delta
             const bool ok = m0 + tid < S;
-            lseS[buf * 64 + tid] = (!ok || lreg == INFINITY) ? -INFINITY : -lreg / scale_log2;
+            lseS[buf * 64 + tid] = (!ok || lreg == INFINITY) ? -INFINITY : -lreg;
             dltS[buf * 64 + tid] = ok ? -dreg : 0.f;
         }
     };
@@ -330,7 +355,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
                     const int qoff = m0 + qt * 32 - klim;
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        const float p = fast_exp2(sp[r] * scale_log2);
+                        const float p = fast_exp2(sp[r]);
                         const bool ok = (unsigned)(qoff + acc_row(r, hh)) < span;
                         sp[r] = ok ? p : 0.f;
                         dp[r] = ok ? p * dp[r] : 0.f;
@@ -338,7 +363,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        const float p = fast_exp2(sp[r] * scale_log2);
+                        const float p = fast_exp2(sp[r]);
                         sp[r] = p;
                         dp[r] *= p;
                     }

@@ -131,6 +131,29 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// fp8 operands (F8 != 0, K-major images only).  An fp8 K-tile of 128 values is byte-for-byte the 128-byte row
+// segment of a bf16 K-tile of 64, so the staging (DMA, swizzle, fragment reads) is the bf16 kernel's, run on
+// the matrices reinterpreted as bf16 rows of half the length.  The two bf16 k-step fragments of a lane (16-byte
+// chunks g and 4 + g of its row, g = lane >> 4) together are the 32 bytes one
+// v_mfma_scale_f32_16x16x128_f8f6f4 takes per lane: the lanes then cover every k of the 128 exactly once, in
+// the same order for both operands, so the products sum over k correctly.  Block scales are 1 (E8M0 127);
+// the per-tensor inverse scales are applied in the epilogue.  F8: 1 = e4m3 x e4m3, 2 = e5m2 (A) x e4m3 (B).
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ i32x8 cat8(bf16x8 lo, bf16x8 hi) {
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const i32x4 a = __builtin_bit_cast(i32x4, lo), b = __builtin_bit_cast(i32x4, hi);
+    return i32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// C += B-operand x A-operand (the kernel issues (B, A) so a register holds 4 consecutive output columns);
+// cbsz = format of the first operand (B = the weight, e4m3), blgp = the second's (A: e4m3, or e5m2 for F8 2)
+template <int F8>
+__device__ __forceinline__ f32x4 mfma_f8(const bf16x8 (&b)[2], const bf16x8 (&a)[2], f32x4 c) {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat8(b[0], b[1]), cat8(a[0], a[1]), c, 0,
+                                                             F8 == 2 ? 1 : 0, 0, 127, 0, 127);
+}
+
 struct Frags {
     bf16x8 a[4][2];  // A (output rows): 4 i-blocks of the current m half x 2 k-steps
     bf16x8 b[2][2];  // B (output cols): 2 j-blocks of the current n half x 2 k-steps
@@ -157,25 +180,37 @@ __device__ __forceinline__ void load_b(Frags& f, char* img, int wl, int n, int l
         for (int ks = 0; ks < 2; ++ks) f.b[jb][ks] = frag<BKM, SUB>(img, 4 * wl + 2 * n + jb, ks, l);
 }
 
+template <int F8 = 0>
 __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const Frags& f, int m, int n) {
 #pragma unroll
     for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
+        for (int jb = 0; jb < 2; ++jb) {
+            if constexpr (F8 != 0) {
+                acc[4 * m + ib][2 * n + jb] = mfma_f8<F8>(f.b[jb], f.a[ib], acc[4 * m + ib][2 * n + jb]);
+            } else {
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-                acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
+                for (int ks = 0; ks < 2; ++ks)
+                    acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
+            }
+        }
 }
 
 // Half of a quadrant (i-blocks 2h, 2h+1): the MFMA section can then issue one DMA piece between its halves.
+template <int F8 = 0>
 __device__ __forceinline__ void mma_half(f32x4 (&acc)[8][4], const Frags& f, int m, int n, int h) {
 #pragma unroll
     for (int ib = 2 * h; ib < 2 * h + 2; ++ib)
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
+        for (int jb = 0; jb < 2; ++jb) {
+            if constexpr (F8 != 0) {
+                acc[4 * m + ib][2 * n + jb] = mfma_f8<F8>(f.b[jb], f.a[ib], acc[4 * m + ib][2 * n + jb]);
+            } else {
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-                acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
+                for (int ks = 0; ks < 2; ++ks)
+                    acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
+            }
+        }
 }
 
 // One K-tile: four (load section, barrier, MFMA section, barrier) phases.  `cur` is read, `nxt` is the DMA
@@ -290,7 +325,7 @@ __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2
 // SPLIT (spread mode 2, BPE_GPP_SPREAD; the default for the weight-gradient layout): the second piece of each
 // pair is issued by the same wave in its MFMA section,
 // between the two halves of the quadrant, so a load section carries one piece; the waits become vmcnt(3).
-template <bool AK, bool BKM, int DIAG, bool SPLIT = false>
+template <bool AK, bool BKM, int DIAG, bool SPLIT = false, int F8 = 0>
 __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
                                              const __bf16* an, const __bf16* bn, const SpreadOff& so, int g, int wl,
                                              int l, f32x4 (&acc)[8][4]) {
@@ -315,15 +350,15 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
         }
         bar();
         if constexpr (SPLIT) {
-            mma_half(acc, f, m, n, 0);
+            mma_half<F8>(acc, f, m, n, 0);
             if (dma) {
                 __builtin_amdgcn_sched_barrier(0);
                 dma_one(t0, off[1], img, lb + 64);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            mma_half(acc, f, m, n, 1);
+            mma_half<F8>(acc, f, m, n, 1);
         } else {
-            mma_quadrant(acc, f, m, n);
+            mma_quadrant<F8>(acc, f, m, n);
         }
         bar();
     };
@@ -359,9 +394,11 @@ struct Epi {
     __bf16* act = nullptr;  // EPI_SWIGLU_FWD: a = silu(g) * u, [M][F]
     long ld_act = 0;
     int prio = 0;  // 1: group 1 (the younger waves 4-7) runs at s_setprio 1 (guide T5, static form)
+    const float* sa = nullptr;  // F8: device-resident per-tensor inverse scales of A and B (output x sa x sb)
+    const float* sb = nullptr;
 };
 
-template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, int SPREAD = 0>
+template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, int SPREAD = 0, int F8 = 0>
 __global__ void __launch_bounds__(NT, 1)
 gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
                float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int M, int N, int R,
@@ -422,8 +459,8 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
             char* cur = smem + (kt & 1) * STAGE;
             char* nxt = smem + ((kt + 1) & 1) * STAGE;
             const long k1 = (long)(kb + kt + 1) * BK;
-            ktile_spread<AK, BKM, DIAG, SPREAD == 2>(cur, nxt, kt + 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
-                                                     tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc);
+            ktile_spread<AK, BKM, DIAG, SPREAD == 2, F8>(cur, nxt, kt + 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
+                                                         tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc);
         }
     } else {
         int oa[4], ob[4];
@@ -470,6 +507,8 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
                 if (st_on) *reinterpret_cast<f32x4*>(sp + i * N + j) = acc[ib][jb];
             }
     } else {
+        float osc = 1.f;  // F8: the product of the operands' inverse scales (device-resident, one load)
+        if constexpr (F8 != 0) osc = ep.sa[0] * ep.sb[0];
         // stage bf16 tile as [256][512 B], 16-byte chunk c of row i at c ^ (i & 15)
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib)
@@ -477,7 +516,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
             for (int jb = 0; jb < 4; ++jb) {
                 const int i = 128 * g + 16 * ib + (l & 15);
                 const int j = 64 * wl + 16 * jb + 4 * (l >> 4);
-                const f32x4 v = acc[ib][jb];
+                const f32x4 v = F8 != 0 ? acc[ib][jb] * osc : acc[ib][jb];
                 const u16x4 p = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
                 *reinterpret_cast<u16x4*>(smem + i * 512 + ((((j >> 3) ^ (i & 15))) << 4) + ((j & 7) << 1)) = p;
             }
@@ -819,6 +858,28 @@ void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ld
     ep.prio = prio_mode();
     k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)X, ldx, (const __bf16*)W13, ldw, nullptr, nullptr, 0, 0.f, M, 2 * F,
                                   R, 1, ep);
+}
+
+// C[M][N] (bf16) = (A8 . B8^T) * sa * sb with A8 [M][K], B8 [N][K] fp8 row-major (K-major), row strides in
+// bytes; fmt_a 0 = e4m3, 1 = e5m2; B is e4m3.  M, N multiples of 256, K of 128, strides of 16 bytes.
+void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                     int fmt_a, const float* sa, const float* sb, hipStream_t s) {
+    static bool attr1 = false, attr2 = false;
+    auto* k1 = &gemm_pp_kernel<true, true, false, 0, EPI_NONE, 1, 1>;
+    auto* k2 = &gemm_pp_kernel<true, true, false, 0, EPI_NONE, 1, 2>;
+    auto* k = fmt_a == 1 ? k2 : k1;
+    bool& attr = fmt_a == 1 ? attr2 : attr1;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        attr = true;
+    }
+    Epi ep{};
+    ep.prio = prio_mode();
+    ep.sa = sa;
+    ep.sb = sb;
+    // the fp8 rows as bf16 rows of half the length: R = K / 2 "bf16" elements = K / 128 K-tiles of 128 fp8
+    k<<<(M / BT) * (N / BT), NT, LDS_BYTES, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, nullptr,
+                                                  (__bf16*)C, ldc, 0.f, M, N, K / 2, 1, ep);
 }
 
 bool gemm_pp_shape_ok(int M, int N, int R, int splits) {

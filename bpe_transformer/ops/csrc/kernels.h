@@ -72,6 +72,11 @@ bool gemm_pp_shape_ok(int M, int N, int R, int splits);
 void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                     float beta, int M, int N, int R, int splits, float* slab, int c_f32, hipStream_t s);
 
+// fp8 x fp8 -> bf16 on the ping-pong kernel with v_mfma_scale_f32_16x16x128_f8f6f4: C = A8 B8^T * sa * sb,
+// A8 [M][K] (fmt_a 0 e4m3 / 1 e5m2), B8 [N][K] e4m3, both K-major; strides in bytes (A, B) / elements (C)
+void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                     int fmt_a, const float* sa, const float* sb, hipStream_t s);
+
 void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ldw, void* gu, long ldg, void* act,
                                long lda_, int M, int F, int R, hipStream_t s);
 void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,

@@ -355,6 +355,31 @@ void gemm_pp(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kma
                    c32 ? 1 : 0, cur_stream());
 }
 
+// y = (a8 @ b8^T) * sa * sb in bf16: a8 [M, K] e4m3 / e5m2, b8 [N, K] e4m3 (both K-major), sa / sb device fp32
+// scalars (the per-tensor inverse scales); the hand-written fp8 MFMA ping-pong kernel (gemm_pp.hip)
+at::Tensor gemm_fp8(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor& sa, const at::Tensor& sb) {
+    check_cuda(a8, "a8");
+    check_cuda(b8, "b8");
+    const bool a_e5 = a8.scalar_type() == at::kFloat8_e5m2;
+    TORCH_CHECK((a8.scalar_type() == at::kFloat8_e4m3fn || a_e5) && b8.scalar_type() == at::kFloat8_e4m3fn,
+                "gemm_fp8: a8 must be float8_e4m3fn or float8_e5m2, b8 float8_e4m3fn");
+    TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.stride(1) == 1 && b8.stride(1) == 1 && a8.size(1) == b8.size(1),
+                "gemm_fp8: a8 [M, K] and b8 [N, K] row-major with a common K");
+    const int64_t M = a8.size(0), N = b8.size(0), K = a8.size(1);
+    TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0,
+                "gemm_fp8: M, N must be multiples of 256 and K of 128");
+    TORCH_CHECK(a8.stride(0) % 16 == 0 && b8.stride(0) % 16 == 0 && (a8.stride(0) * 256) < (1L << 32),
+                "gemm_fp8: 16-byte aligned rows");
+    TORCH_CHECK(sa.scalar_type() == at::kFloat && sb.scalar_type() == at::kFloat && sa.numel() >= 1 &&
+                    sb.numel() >= 1 && sa.device() == a8.device() && sb.device() == a8.device(),
+                "gemm_fp8: sa / sb must be fp32 device scalars");
+    DevGuard g(a8.device());
+    auto y = at::empty({M, N}, a8.options().dtype(at::kBFloat16));
+    launch_gemm_fp8(a8.data_ptr(), a8.stride(0), b8.data_ptr(), b8.stride(0), y.data_ptr(), y.stride(0), (int)M,
+                    (int)N, (int)K, a_e5 ? 1 : 0, sa.data_ptr<float>(), sb.data_ptr<float>(), cur_stream());
+    return y;
+}
+
 // dgu = swiglu_bwd(dy @ w2, gu) with the SwiGLU backward in the GEMM epilogue (da never reaches HBM)
 at::Tensor gemm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& w2, const at::Tensor& gu) {
     check_cuda(gu, "gu");
@@ -795,6 +820,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
     m.def("gemm_swiglu_bwd(Tensor dy, Tensor w2, Tensor gu) -> Tensor");
     m.def("gemm_swiglu_fwd(Tensor x, Tensor w13) -> (Tensor, Tensor)");
+    m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb) -> Tensor");
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
@@ -834,6 +860,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("gemm_pp", &gemm_pp);
     m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
     m.impl("gemm_swiglu_fwd", &gemm_swiglu_fwd);
+    m.impl("gemm_fp8", &gemm_fp8);
     m.impl("cast_fp8", &cast_fp8);
     m.impl("transpose_bf16", &transpose_bf16);
     m.impl("cast_fp8_t", &cast_fp8_t);

@@ -2,8 +2,11 @@
 
 Recipe (BASELINE.json "Llama-style 1.1B fp8 MFMA path"):
   * the four projection GEMMs of every block run as fp8 x fp8 -> bf16 on the
-    MFMA fp8 units (hipBLASLt via ``torch._scaled_mm``, measured ~2x the bf16
-    rate on MI355X at the 1.1B shapes, ``benchmarks/fp8_probe.py``);
+    MFMA fp8 units: the hand-written ping-pong kernel with
+    ``v_mfma_scale_f32_16x16x128_f8f6f4`` (``csrc/gemm_pp.hip``, F8 variants;
+    per-tensor inverse scales applied in its epilogue, read from the device)
+    wherever the shape is 256 x 256 x 128-tiled, hipBLASLt's
+    ``torch._scaled_mm`` otherwise or with ``BPE_FP8_GEMM=lib`` (A/B);
   * activations and weights are quantised by ``csrc/fp8.hip`` with a scale
     derived from an amax history (delayed scaling, powers of two); the cast
     pass also records this step's amax, and one launch per step refreshes all
@@ -17,6 +20,8 @@ Recipe (BASELINE.json "Llama-style 1.1B fp8 MFMA path"):
 
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import Tensor
 
@@ -25,6 +30,20 @@ from ._ext import ops
 FP8 = torch.float8_e4m3fn
 BF8 = torch.float8_e5m2
 _FMT = {"e4m3": (FP8, 0), "e5m2": (BF8, 1)}
+_LIB = os.environ.get("BPE_FP8_GEMM", "hip") == "lib"
+
+
+def mm_fp8(a8: Tensor, b8: Tensor, sa: Tensor, sb: Tensor) -> Tensor:
+    """``(a8 @ b8.T) * sa * sb`` in bf16; a8 [M, K] e4m3 / e5m2, b8 [N, K] e4m3, sa / sb fp32 device scalars.
+
+    The HIP fp8 MFMA kernel for 256 x 256 x 128-aligned shapes (every projection of the configs here), hipBLASLt
+    otherwise (or with ``BPE_FP8_GEMM=lib``)."""
+    M, K = a8.shape
+    N = b8.shape[0]
+    if (not _LIB and M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and a8.stride(1) == 1 and b8.stride(1) == 1
+            and a8.stride(0) % 16 == 0 and b8.stride(0) % 16 == 0 and b8.dtype == FP8):
+        return ops().gemm_fp8(a8, b8, sa.reshape(1), sb.reshape(1))
+    return torch._scaled_mm(a8, b8.t(), scale_a=sa, scale_b=sb, out_dtype=torch.bfloat16)
 
 
 class Fp8State:
@@ -84,8 +103,7 @@ class Fp8State:
             w8, w8t = self.cast_t(w, w_slot)
         else:
             w8, w8t = self.cast(w, w_slot), None
-        y = torch._scaled_mm(x8, w8.t(), scale_a=self.inv_scale[x_slot], scale_b=self.inv_scale[w_slot],
-                             out_dtype=torch.bfloat16)
+        y = mm_fp8(x8, w8, self.inv_scale[x_slot], self.inv_scale[w_slot])
         if not keep_w8:
             return y
         return y, (w8t if w8t is not None else w8.t().contiguous())
@@ -93,11 +111,10 @@ class Fp8State:
 
 def dgrad(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8State, w_slot: int) -> Tensor:
     """``g @ W`` with g: [M, N] bf16 quantised to e5m2 (slot ``g_slot`` of ``g_state``) and W the forward's e4m3
-    copy in the [K, N] layout ``w8t`` (its scale in slot ``w_slot`` of ``w_state``): the library wants the
-    second operand column-major, i.e. W^T contiguous."""
+    copy in the [K, N] layout ``w8t`` (its scale in slot ``w_slot`` of ``w_state``): both operands contiguous
+    along the reduction (N), the layout of the fp8 kernel and of the library."""
     g8 = g_state.cast(g.contiguous(), g_slot)
-    return torch._scaled_mm(g8, w8t.t(), scale_a=g_state.inv_scale[g_slot], scale_b=w_state.inv_scale[w_slot],
-                            out_dtype=torch.bfloat16)
+    return mm_fp8(g8, w8t, g_state.inv_scale[g_slot], w_state.inv_scale[w_slot])
 
 
 def quantize_reference(x: Tensor, scale: float, fmt: str = "e4m3") -> Tensor:

@@ -691,3 +691,79 @@ def test_update_scales(gpu_device):
     amax.copy_(torch.tensor([2.0, 0.0, 1000.0], device=gpu_device).view(torch.int32))
     torch.ops.bpe_hip.update_scales(amax, hist, scale, inv, 1, 1.0, 1)
     assert scale.tolist() == [16384.0, 1.0, 32.0]  # row 2: pos 1 overwrote the old 3000 -> max 1000
+
+
+# ---------------------------------------------------------------- hand-written fp8 GEMM (gemm_pp.hip, F8)
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 256, 384), (256, 768, 1024)])
+@pytest.mark.parametrize("fmt_a", ["e4m3", "e5m2"])
+def test_gemm_fp8_exact(gpu_device, M, N, K, fmt_a):
+    """y = (a8 @ b8^T) * sa * sb on the fp8 MFMA ping-pong kernel, exact on small-integer operands (fp32 sums of
+    integers are exact; the bf16 output is the round-to-nearest of the exact value) with power-of-two scales:
+    checks the fragment / k mapping of v_mfma_scale_f32_16x16x128_f8f6f4 for both operand formats."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randint(-4, 5, (M, K), generator=g).float()
+    b = torch.randint(-4, 5, (N, K), generator=g).float()
+    a[3, :] = 0.0  # an all-zero row and column
+    b[:, 5] = 0.0
+    dt_a = torch.float8_e4m3fn if fmt_a == "e4m3" else torch.float8_e5m2
+    a8 = a.to(dt_a).to(gpu_device)
+    b8 = b.to(torch.float8_e4m3fn).to(gpu_device)
+    sa = torch.tensor([0.25], device=gpu_device)
+    sb = torch.tensor([2.0], device=gpu_device)
+    y = torch.ops.bpe_hip.gemm_fp8(a8, b8, sa, sb)
+    ref = ((a @ b.t()) * 0.5).to(torch.bfloat16)
+    assert y.dtype == torch.bfloat16 and y.shape == (M, N)
+    assert torch.equal(y.cpu(), ref)
+
+
+def test_gemm_fp8_random_vs_dequantised(gpu_device):
+    """Random e4m3 operands at a Llama projection shape against the fp32 product of the dequantised operands."""
+    torch.manual_seed(7)
+    M, N, K = 1024, 2560, 2048
+    a8 = (torch.randn(M, K, device=gpu_device) * 2).to(torch.float8_e4m3fn)
+    b8 = (torch.randn(N, K, device=gpu_device) * 2).to(torch.float8_e4m3fn)
+    sa = torch.tensor([0.125], device=gpu_device)
+    sb = torch.tensor([0.0625], device=gpu_device)
+    y = torch.ops.bpe_hip.gemm_fp8(a8, b8, sa, sb)
+    ref = (a8.float() @ b8.float().t()) * (0.125 * 0.0625)
+    assert rel(y.float(), ref) < 5e-3
+
+
+# ---------------------------------------------------------------- fp32 gradient buffers (gemm.hip / gemm_pp.hip)
+@pytest.mark.parametrize("kernel,tile", [("pp", 0), ("gemm", 256), ("gemm", 128)])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_gemm_fp32_output_accumulates_unrounded(gpu_device, kernel, tile, splits):
+    """dW kernels writing an fp32 C (an fp32 gradient buffer): C = beta * C + dY^T X through the fp32 partial slab
+    and the ordered reduce -- exact on small-integer operands, including a C value no bf16 can hold."""
+    torch.manual_seed(2)
+    N, K, T = 512, 256, 4096
+    dy = torch.randint(-2, 3, (T, N), device=gpu_device).to(torch.bfloat16)
+    x = torch.randint(-2, 3, (T, K), device=gpu_device).to(torch.bfloat16)
+    C = torch.randint(-3, 4, (N, K), device=gpu_device).float() + 1.0 / 256  # not representable in bf16
+    ref = C.double() + dy.double().t() @ x.double()
+    if kernel == "pp":
+        torch.ops.bpe_hip.gemm_pp(dy, False, x, False, C, 1.0, splits)
+    else:
+        torch.ops.bpe_hip.gemm(dy, False, x, False, C, 1.0, splits, tile)
+    assert torch.equal(C.double().cpu(), ref.cpu())
+
+
+def test_accumulate_weight_grad_fp32_buffer(gpu_device):
+    """The dW route with an fp32 gradient view (TrainEngine(grad_dtype=fp32)): four accumulations stay within
+    fp32 rounding of the fp64 sum, where a bf16 buffer is off by its own rounding."""
+    from bpe_transformer.ops.gemm import accumulate_weight_grad
+
+    torch.manual_seed(3)
+    T, N, K = 8192, 768, 768
+    g32 = torch.zeros(N, K, device=gpu_device)
+    g16 = torch.zeros(N, K, device=gpu_device, dtype=torch.bfloat16)
+    ref = torch.zeros(N, K, device=gpu_device, dtype=torch.float64)
+    for _ in range(4):
+        dy = torch.randn(T, N, device=gpu_device, dtype=torch.bfloat16)
+        x = torch.randn(T, K, device=gpu_device, dtype=torch.bfloat16)
+        accumulate_weight_grad(g32, dy, x)
+        accumulate_weight_grad(g16, dy, x)
+        ref += dy.double().t() @ x.double()
+    e32 = float((g32.double() - ref).norm() / ref.norm())
+    e16 = float((g16.double() - ref).norm() / ref.norm())
+    assert e32 < 1e-6 and e16 > 100 * e32, (e32, e16)

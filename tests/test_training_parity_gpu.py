@@ -1,0 +1,193 @@
+"""At-scale training parity: the fused HIP training engine against an independent eager PyTorch implementation.
+
+The reference implies one training step (``/root/reference/tests/test_optimizer.py:18-25``: forward, cross-entropy,
+backward, clip, AdamW with a cosine schedule).  Here both implementations train the same GPT-2-shaped model
+(d_model 768, 12 heads, SwiGLU d_ff 2048, RoPE, RMSNorm; 2 layers so the test stays short) from identical
+weights on the same real-token batches for 150 steps:
+
+* ours: ``TrainEngine`` -- bf16 weights, fp32 master and moments in the flat AdamW kernel, fused blocks (split
+  flash attention, SwiGLU GEMM epilogues, TN-layout input gradients), fused LM head + CE, device-side clip;
+* eager: a separate module tree written here with ``torch.nn.functional.scaled_dot_product_attention``, fp32
+  parameters under bf16 autocast, ``torch.optim.AdamW``, ``clip_grad_norm_`` and the same cosine schedule.
+
+Tokens: the reference's sample TinyStories tokenizer (10 000 vocab) over ``corpus.en`` + ``tinystories_sample.txt``.
+batch x seq = 4 x 1024 (a multiple of 256, so every fused path engages).  A second run accumulates 4 micro-batches
+of one sequence per step (fp32 gradient buffer).  Set ``BPE_PARITY_LOG=<dir>`` to write both loss curves.
+"""
+
+from __future__ import annotations
+
+import json
+import math
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .conftest import FIXTURES
+
+pytestmark = pytest.mark.gpu
+
+STEPS, B, S = 150, 4, 1024
+D, L, H, FF, THETA = 768, 2, 12, 2048, 10000.0
+LR_MAX, LR_MIN, WARMUP = 1e-3, 1e-4, 10
+
+
+def _lr(it: int) -> float:
+    from bpe_transformer.optim.schedule import get_lr_cosine_schedule
+
+    return get_lr_cosine_schedule(it, LR_MAX, LR_MIN, WARMUP, STEPS)
+
+
+class _RMS(nn.Module):
+    def __init__(self, d, eps=1e-5):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(d))
+        self.eps = eps
+
+    def forward(self, x):
+        xf = x.float()
+        return xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps) * self.weight.float()
+
+
+def _rope(x, cos, sin):  # x [B, H, S, Dh], interleaved pairs (2i, 2i+1)
+    x1, x2 = x[..., 0::2].float(), x[..., 1::2].float()
+    out = torch.stack((x1 * cos - x2 * sin, x1 * sin + x2 * cos), dim=-1)
+    return out.flatten(-2).to(x.dtype)
+
+
+class _Attn(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.q_proj = nn.Linear(D, D, bias=False)
+        self.k_proj = nn.Linear(D, D, bias=False)
+        self.v_proj = nn.Linear(D, D, bias=False)
+        self.output_proj = nn.Linear(D, D, bias=False)
+
+    def forward(self, x, cos, sin):
+        b, s, _ = x.shape
+        q, k, v = (p(x).view(b, s, H, D // H).transpose(1, 2) for p in (self.q_proj, self.k_proj, self.v_proj))
+        q, k = _rope(q, cos, sin), _rope(k, cos, sin)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        return self.output_proj(o.transpose(1, 2).reshape(b, s, D))
+
+
+class _FFN(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.w1 = nn.Linear(D, FF, bias=False)
+        self.w2 = nn.Linear(FF, D, bias=False)
+        self.w3 = nn.Linear(D, FF, bias=False)
+
+    def forward(self, x):
+        return self.w2(F.silu(self.w1(x)) * self.w3(x))
+
+
+class _Block(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.ln1, self.attn, self.ln2, self.ffn = _RMS(D), _Attn(), _RMS(D), _FFN()
+
+    def forward(self, x, cos, sin):
+        x = x + self.attn(self.ln1(x), cos, sin)
+        return x + self.ffn(self.ln2(x))
+
+
+class EagerLM(nn.Module):
+    """Independent implementation with the reference's parameter names (``tests/adapters.py:311-353``)."""
+
+    def __init__(self, vocab):
+        super().__init__()
+        self.token_embeddings = nn.Embedding(vocab, D)
+        self.layers = nn.ModuleList(_Block() for _ in range(L))
+        self.ln_final = _RMS(D)
+        self.lm_head = nn.Linear(D, vocab, bias=False)
+        inv = THETA ** (-torch.arange(0, D // H, 2, dtype=torch.float64) / (D // H))
+        ang = torch.arange(S, dtype=torch.float64)[:, None] * inv[None, :]
+        self.register_buffer("cos", ang.cos().float(), persistent=False)
+        self.register_buffer("sin", ang.sin().float(), persistent=False)
+
+    def loss(self, x, y):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            h = self.token_embeddings(x)
+            for blk in self.layers:
+                h = blk(h, self.cos, self.sin)
+            logits = self.lm_head(self.ln_final(h))
+        return F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), y.reshape(-1))
+
+
+def _tokens():
+    from bpe_transformer.tokenization import BPETokenizer
+
+    tok = BPETokenizer.from_files(FIXTURES / "sample_tokenizer" / "vocab.pkl",
+                                  FIXTURES / "sample_tokenizer" / "merges.pkl", ["<|endoftext|>"])
+    text = (FIXTURES / "corpus.en").read_text(encoding="utf-8") + "<|endoftext|>"
+    text += (FIXTURES / "tinystories_sample.txt").read_text(encoding="utf-8") * 8
+    return torch.tensor(tok.encode(text), dtype=torch.long), len(tok.vocab)
+
+
+def _batches(ids, n, micro, dev):
+    g = torch.Generator().manual_seed(1234)
+    out = []
+    for _ in range(n):
+        st = torch.randint(0, ids.numel() - S - 1, (micro,), generator=g)
+        w = torch.stack([ids[s : s + S + 1] for s in st.tolist()]).to(dev)
+        out.append((w[:, :-1].contiguous(), w[:, 1:].contiguous()))
+    return out
+
+
+def _run(accum: int, gpu_device):
+    from bpe_transformer.models import TransformerLM
+    from bpe_transformer.train.engine import TrainEngine
+
+    ids, vocab = _tokens()
+    torch.manual_seed(0)
+    ours = TransformerLM(vocab, S, D, L, H, FF, THETA, device=gpu_device, dtype=torch.bfloat16)
+    eager = EagerLM(vocab).to(gpu_device)
+    missing, unexpected = eager.load_state_dict({k: v.float() for k, v in ours.state_dict().items()}, strict=False)
+    assert not missing and not [k for k in unexpected if "rope" not in k], (missing, unexpected)
+    eng = TrainEngine(ours, lr=LR_MAX, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0,
+                      grad_dtype=torch.float32 if accum > 1 else None)
+    decay = [p for p in eager.parameters() if p.dim() >= 2]
+    nodecay = [p for p in eager.parameters() if p.dim() < 2]
+    opt = torch.optim.AdamW([{"params": decay, "weight_decay": 0.1}, {"params": nodecay, "weight_decay": 0.0}],
+                            lr=LR_MAX, betas=(0.9, 0.95), eps=1e-8)
+    micro = B // accum
+    data = _batches(ids, STEPS * accum, micro, gpu_device)
+    lo, le = [], []
+    for it in range(STEPS):
+        mb = data[it * accum : (it + 1) * accum]
+        lo.append(eng.train_step(mb, lr=_lr(it)))
+        lr = _lr(it)
+        for gr in opt.param_groups:
+            gr["lr"] = lr
+        opt.zero_grad(set_to_none=True)
+        tot = 0.0
+        for x, y in mb:
+            loss = eager.loss(x, y)
+            (loss / accum).backward()
+            tot += loss.detach()
+        torch.nn.utils.clip_grad_norm_(eager.parameters(), 1.0)
+        opt.step()
+        le.append(tot / accum)
+    lo = [float(v) for v in torch.stack(lo).cpu()]
+    le = [float(v) for v in torch.stack(le).cpu()]
+    return lo, le
+
+
+@pytest.mark.parametrize("accum", [1, 4])
+def test_fused_engine_tracks_eager_pytorch(gpu_device, accum):
+    lo, le = _run(accum, gpu_device)
+    assert all(math.isfinite(v) for v in lo + le)
+    rel = [abs(a - b) / b for a, b in zip(lo, le)]
+    log = os.environ.get("BPE_PARITY_LOG")
+    if log:
+        os.makedirs(log, exist_ok=True)
+        with open(os.path.join(log, f"parity_gpt2shape_L{L}_accum{accum}.json"), "w") as f:
+            json.dump({"steps": STEPS, "batch": B, "seq": S, "accum": accum, "ours": lo, "eager": le,
+                       "max_rel": max(rel), "final_rel": rel[-1]}, f)
+    assert le[-1] < le[0] - 2.0, "the eager reference did not learn: the comparison would be vacuous"
+    assert max(rel) < 0.02, (max(rel), rel.index(max(rel)))
+    assert rel[-1] < 0.01, rel[-1]

@@ -21,3 +21,5 @@ python3 -m bpe_transformer.utils.pmc $OUT/p1 $OUT/p2 $OUT/p3 --match fa_ > $OUT/
 find $OUT -name "*.csv" -size +20M -delete
 cat $OUT/summary.txt
 find $OUT/st -name "*kernel_stats.csv" | head -1 | xargs cat | cut -c1-200 | head -20
+timeout -k 10 300 python benchmarks/attn_bench.py --batch 128 --bwd-ab --iters 10 > $OUT/ab.log 2>&1
+cat $OUT/ab.log
