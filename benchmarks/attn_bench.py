@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--bwd-ab", action="store_true",
                     help="interleaved same-process A/B of the backward forms: fused (atomics) and split at 4/8 "
                          "waves per workgroup (ops.fa_bwd_config)")
+    ap.add_argument("--fwd-ab", action="store_true",
+                    help="interleaved same-process A/B of the D = 64 forward versions 2 (fa_fwd_kernel) and 4 "
+                         "(flash_attn_fwd_v4.hip) (ops.fa_fwd_config)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--mode", choices=["block", "fused"], default="block",
                     help="block = the training path (rope_qk_ in place, then pre-rotated kernels; rope time reported "
@@ -58,9 +61,30 @@ def main():
         bwd(o, lse)
     torch.cuda.synchronize()
     fl = 4.0 * B * H * S * S * D / 2
+    if a.fwd_ab:
+        prev = hip.fa_fwd_config(0)
+        times = {2: [], 4: []}
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for _ in range(a.rounds):
+            for ver in times:
+                hip.fa_fwd_config(ver)
+                hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
+                ev[0].record()
+                for _ in range(a.iters):
+                    hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
+                ev[1].record()
+                torch.cuda.synchronize()
+                times[ver].append(ev[0].elapsed_time(ev[1]) / a.iters)
+        hip.fa_fwd_config(prev)
+        for ver, t in times.items():
+            t = sorted(t)
+            print(json.dumps({"shape": [B, S, H, Hkv, D], "fwd_version": ver, "fwd_ms_median": round(t[len(t) // 2], 4),
+                              "fwd_ms_min": round(t[0], 4), "fwd_tflops": round(fl / t[len(t) // 2] / 1e9, 1)}))
+        if not a.bwd_ab:
+            return
     if a.bwd_ab:
-        arms = {"fused": (1, 0, 0), "split4x4": (0, 4, 4), "split8x8": (0, 8, 8), "split4x8": (0, 4, 8),
-                "split8x4": (0, 8, 4)}
+        arms = {"fused": (1, 0, 0), "split4x4": (0, 4, 4), "split4x8": (0, 4, 8), "split8x4": (0, 8, 4),
+                "split4_ppdkv": (0, 4, 2), "split8_ppdkv": (0, 8, 2)}
         prev = hip.fa_bwd_config(-1, 0, 0)
         times = {k: [] for k in arms}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -74,7 +98,7 @@ def main():
                 ev[1].record()
                 torch.cuda.synchronize()
                 times[name].append(ev[0].elapsed_time(ev[1]) / a.iters)
-        hip.fa_bwd_config(prev, 4, 4)
+        hip.fa_bwd_config(prev, 4, 2)
         for name, t in times.items():
             t = sorted(t)
             print(json.dumps({"shape": [B, S, H, Hkv, D], "arm": name, "bwd_ms_median": round(t[len(t) // 2], 4),

@@ -432,6 +432,274 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
         }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Ping-pong dK / dV kernel (the default for the split form).  Same math as fa_bwd_dkv_kernel; the schedule is the
+// one that keeps the ping-pong GEMM's matrix pipe busy (gemm_pp.hip, guide §5 8-phase template): 8 waves in two
+// groups of four; waves w and w + 4 share a SIMD and own adjacent 32-key blocks (keys kb0 + 64 (w & 3) +
+// 32 (w >> 2)); group 1 runs one barrier interval behind group 0.  A wave's work is a chain of half-steps
+// j = 2 t + h (query tile t, 32-query half h), each cut into two segments separated by barriers:
+//   M(j): MFMA section -- dV^T += dO^T.P and dK^T += Q^T.dS of half-step j - 1 (operands read in V(j - 1)),
+//         then S = Q.(cK)^T - lse and dP = dO.V^T - delta of half-step j (16 MFMAs, the rows and the row
+//         constants read at the top of the section so they land under the first 8 MFMAs)
+//   V(j): VALU section -- P = exp2(S), dS = P dP, bf16 packing, the transposed reads dV/dK(j) will need,
+//         and the staging of the next query tile.
+// So in every barrier interval one wave of each SIMD issues 16 MFMAs while its partner exponentiates: the
+// softmax VALU (~300 cycles per half-step) hides under the partner's 512 MFMA cycles.
+// Staging: query tile t + 1 is written into LDS buffer (t + 1) & 1 in V(2t) -- group g the rows [32 g, +32) of
+// Q and dO and their row constants -- from registers loaded in V(2t - 2), and is first read in M(2t + 2).
+// WAR: that buffer's previous tile (t - 1) was last read in V(2t - 1) (transposed reads), which group 1 runs in
+// the interval before group 0's V(2t).  RAW: group 1's writes (its V(2t)) land two intervals before group 0's
+// M(2t + 2).  Every section that writes LDS retires its writes (lgkmcnt(0)) before its closing barrier.
+constexpr int PPNW = 8;
+
+__device__ __forceinline__ void pp_bar() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool CAUSAL, bool ROPE, bool ROPE_IN>
+__global__ void __launch_bounds__(PPNW * 64, 1)
+fa_bwd_dkv_pp_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
+                     long ld_q, long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
+                     const float* __restrict__ DELTA, __bf16* __restrict__ dK, __bf16* __restrict__ dV, long ld_dkv,
+                     float* __restrict__ dKVpart, const float* __restrict__ cosT, const float* __restrict__ sinT,
+                     int B, int H, int Hkv, int S, float scale_log2, float scale, int group) {
+    constexpr int KB = 32 * PPNW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Qs = smem;                                          // [2][64 q][128 B]  (roped Q)
+    char* dOs = smem + 2 * TILE;                              // [2][64 q][128 B]
+    float* lseS = reinterpret_cast<float*>(smem + 4 * TILE);  // [2][64]  -lse
+    float* dltS = lseS + 128;                                 // [2][64]  -delta
+
+    const int tid = threadIdx.x, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = w >> 2, wl = w & 3, gt = tid & 255;  // group, wave in group, thread in group
+    const int nkb = (S + KB - 1) / KB;
+    int kblk, bh;
+    grouped_order((int)blockIdx.x, nkb, B * H, group, kblk, bh);
+    const int b = bh / H, h = bh % H, G = H / Hkv, hk = h / G;
+    const int kb0 = kblk * KB, kw0 = kb0 + 64 * wl + 32 * g, key = kw0 + l31;
+    const bool key_ok = key < S;
+    const long kpos = key_ok ? key : S - 1;
+
+    bf16x8 kf[KS], vf[KS];
+    {
+        const __bf16* kp = K + ((long)b * S + kpos) * ld_kv + (long)hk * D;
+        const __bf16* vp = Vv + ((long)b * S + kpos) * ld_kv + (long)hk * D;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int d0 = 16 * ks + 8 * hh;
+            u16x8 tk = *reinterpret_cast<const u16x8*>(kp + d0);
+            u16x8 tv = *reinterpret_cast<const u16x8*>(vp + d0);
+            const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+            tk = key_ok ? tk : z;
+            tv = key_ok ? tv : z;
+            if (ROPE_IN) {
+                tk = rope_u16x8(tk, cosT + kpos * (D / 2) + d0 / 2, sinT + kpos * (D / 2) + d0 / 2, scale_log2);
+            } else {
+                float x[8];
+                unpack8(tk, x);
+                tk = pack8(x, scale_log2);
+            }
+            kf[ks] = __builtin_bit_cast(bf16x8, tk);
+            vf[ks] = __builtin_bit_cast(bf16x8, tv);
+        }
+    }
+    f32x16 dk[2], dv[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+
+    const int m_start = CAUSAL ? kb0 : 0;
+    const int nqt = m_start < S ? (S - m_start + 63) / 64 : 0;
+    const int J = 2 * nqt;  // half-steps
+    const __bf16* qb = Q + (long)b * S * ld_q + (long)h * D;
+    const __bf16* ob = dO + (long)b * S * ld_do + (long)h * D;
+    const long sbase = ((long)b * H + h) * S;
+    // staging: group g owns rows [32 g, +32) of every tile: one Q chunk and one dO chunk per thread, and (threads
+    // gt < 32) that row's lse / delta
+    const int srow = 32 * g + (gt >> 3), sc = gt & 7;
+    u16x8 qreg, oreg;
+    float lreg = 0.f, dreg = 0.f;
+    auto load_tile = [&](int t) {
+        const long qq = min(m_start + t * 64 + srow, S - 1);
+        qreg = *reinterpret_cast<const u16x8*>(qb + qq * ld_q + sc * 8);
+        oreg = *reinterpret_cast<const u16x8*>(ob + qq * ld_do + sc * 8);
+        const long idx = sbase + min(m_start + t * 64 + 32 * g + (gt & 31), S - 1);
+        lreg = LSE[idx];
+        dreg = DELTA[idx];
+    };
+    auto write_tile = [&](int t) {
+        const int buf = t & 1, m0 = m_start + t * 64;
+        const bool ok = m0 + srow < S;
+        u16x8 qv = ok ? qreg : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        const u16x8 ov = ok ? oreg : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (ROPE_IN) {
+            const long qq = min(m0 + srow, S - 1);
+            qv = rope_u16x8(qv, cosT + qq * (D / 2) + sc * 4, sinT + qq * (D / 2) + sc * 4, 1.f);
+        }
+        *reinterpret_cast<u16x8*>(Qs + buf * TILE + swz<RB>(srow, sc)) = qv;
+        *reinterpret_cast<u16x8*>(dOs + buf * TILE + swz<RB>(srow, sc)) = ov;
+        if (gt < 32) {
+            const int r = 32 * g + gt;
+            const bool okr = m0 + r < S;
+            lseS[buf * 64 + r] = (!okr || lreg == INFINITY) ? -INFINITY : -lreg;
+            dltS[buf * 64 + r] = okr ? -dreg : 0.f;
+        }
+    };
+
+    const int trow = 4 * hh + ((l & 15) >> 2);
+    const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
+    const int klim = CAUSAL ? (key_ok ? key : S) : (key_ok ? 0 : S);
+    const unsigned span = (unsigned)(S - klim);
+
+    // prologue: tile 0 staged and visible; tile 1 in registers
+    if (nqt > 0) {
+        load_tile(0);
+        write_tile(0);
+        if (nqt > 1) load_tile(1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_bar();
+    if (g == 1) pp_bar();  // the stagger
+
+    f32x16 sp, dp;          // S / dP of the current half-step (from its M section to its V section)
+    bf16x8 pb[2], db[2];    // bf16 P / dS of the previous half-step (V -> next M)
+    bf16x8 tq[2][2], to[2][2];  // its transposed Q / dO fragments [ss][dt]
+    bool prev_active = false;
+    for (int j = 0; j <= J; ++j) {
+        const int t = j >> 1, hf = j & 1, m0 = m_start + t * 64;
+        const bool active = j < J && (!CAUSAL || m0 + 32 * hf + 31 >= kw0);
+        // ---------------- M(j): the previous half-step's dV / dK MFMAs (operands already in registers) are issued
+        // first; the row reads of this half-step follow (a scheduling fence keeps the compiler from hoisting all
+        // of them above: register pressure) and land while those MFMAs run.
+        {
+            if (prev_active) {
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+                    for (int dt = 0; dt < 2; ++dt) {
+                        dv[dt] = mfma(to[ss][dt], pb[ss], dv[dt]);
+                        dk[dt] = mfma(tq[ss][dt], db[ss], dk[dt]);
+                    }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (active) {
+                char* Qc = Qs + (t & 1) * TILE;
+                char* Oc = dOs + (t & 1) * TILE;
+                const float* lc = lseS + (t & 1) * 64;
+                const float* dc = dltS + (t & 1) * 64;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int qi = hf * 32 + 8 * i + 4 * hh;
+                    const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
+                    const f32x4 dl = *reinterpret_cast<const f32x4*>(dc + qi);
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) { sp[4 * i + jj] = lv[jj]; dp[4 * i + jj] = dl[jj]; }
+                }
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    const int off = swz<RB>(hf * 32 + l31, 2 * ks + hh);
+                    sp = mfma(lds_row16(Qc, off), kf[ks], sp);
+                    dp = mfma(lds_row16(Oc, off), vf[ks], dp);
+                }
+            }
+        }
+        pp_bar();
+        if (j == J) break;
+        // ---------------- V(j)
+        {
+            char* Qc = Qs + (t & 1) * TILE;
+            char* Oc = dOs + (t & 1) * TILE;
+            if (active) {
+                const bool need_mask = (CAUSAL && m0 + 32 * hf < kw0 + 31) || (m0 + 32 * hf + 32 > S) || (kw0 + 32 > S);
+                if (need_mask) {
+                    const int qoff = m0 + hf * 32 - klim;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float p = fast_exp2(sp[r]);
+                        const bool ok = (unsigned)(qoff + acc_row(r, hh)) < span;
+                        sp[r] = ok ? p : 0.f;
+                        dp[r] = ok ? p * dp[r] : 0.f;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float p = fast_exp2(sp[r]);
+                        sp[r] = p;
+                        dp[r] *= p;
+                    }
+                }
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) {
+                        pb[ss][jj] = (__bf16)sp[8 * ss + jj];
+                        db[ss][jj] = (__bf16)dp[8 * ss + jj];
+                    }
+                    const int qr = hf * 32 + 16 * ss;
+#pragma unroll
+                    for (int dt = 0; dt < 2; ++dt) {
+                        const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
+                        const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
+                        to[ss][dt] = lds_tr_pair(Oc, o0, o1);
+                        tq[ss][dt] = lds_tr_pair(Qc, o0, o1);
+                    }
+                }
+            }
+            prev_active = active;
+            if (hf == 0 && t + 1 < nqt) {  // stage tile t + 1 (loaded two half-steps ago), then load tile t + 2
+                write_tile(t + 1);
+                if (t + 2 < nqt) load_tile(t + 2);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        pp_bar();
+    }
+    if (g == 0) pp_bar();
+
+    if (!key_ok) return;
+    if (G > 1) {
+        float* pk = dKVpart + (((long)b * S + key) * H + h) * 2 * D;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d0 = dt * 32 + 8 * i + 4 * hh;
+                *reinterpret_cast<f32x4*>(pk + d0) =
+                    f32x4{dk[dt][4 * i], dk[dt][4 * i + 1], dk[dt][4 * i + 2], dk[dt][4 * i + 3]};
+                *reinterpret_cast<f32x4*>(pk + D + d0) =
+                    f32x4{dv[dt][4 * i], dv[dt][4 * i + 1], dv[dt][4 * i + 2], dv[dt][4 * i + 3]};
+            }
+        return;
+    }
+    __bf16* dkp = dK + ((long)b * S + key) * ld_dkv + (long)hk * D;
+    __bf16* dvp = dV + ((long)b * S + key) * ld_dkv + (long)hk * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int d0 = dt * 32 + 8 * i + 4 * hh;
+            float x[4] = {dk[dt][4 * i] * scale, dk[dt][4 * i + 1] * scale, dk[dt][4 * i + 2] * scale,
+                          dk[dt][4 * i + 3] * scale};
+            if (ROPE) {
+#pragma unroll
+                for (int pr = 0; pr < 2; ++pr) {
+                    const float c = cosT[kpos * (D / 2) + d0 / 2 + pr];
+                    const float sn = sinT[kpos * (D / 2) + d0 / 2 + pr];
+                    const float a = x[2 * pr], bb = x[2 * pr + 1];
+                    x[2 * pr] = a * c + bb * sn;
+                    x[2 * pr + 1] = -a * sn + bb * c;
+                }
+            }
+            *reinterpret_cast<u16x4*>(dkp + d0) = u16x4{f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+            *reinterpret_cast<u16x4*>(dvp + d0) = u16x4{f2bf(dv[dt][4 * i]), f2bf(dv[dt][4 * i + 1]),
+                                                        f2bf(dv[dt][4 * i + 2]), f2bf(dv[dt][4 * i + 3])};
+        }
+}
+
 }  // namespace split
 }  // namespace fa
 }  // namespace bpe
@@ -441,18 +709,19 @@ using namespace bpe::fa;
 
 // Backward form: 0 = split (default for D = 64), 1 = fused (flash_attn_bwd.hip, the atomics form).  Initial value
 // from BPE_FA_BWD ("fused" / "split"), changeable at run time (fa_bwd_config) for same-process A/B and tests.
-// Waves per workgroup of the two split kernels (4 or 8 each): BPE_FA_SPLIT_NW="<dq>,<dkv>", default 4,4.
-static int g_mode = -1, g_nw_dq = 4, g_nw_dkv = 4;
+// Waves per workgroup of the two split kernels: BPE_FA_SPLIT_NW="<dq>,<dkv>": dq 4 or 8; dkv 4 or 8 (the plain
+// kernel) or 2 (the ping-pong kernel: 8 waves in two staggered groups).  Default 4,2.
+static int g_mode = -1, g_nw_dq = 4, g_nw_dkv = 2;  // g_nw_dkv: 2 = the ping-pong dK/dV kernel (8 waves)
 
 static void config_init() {
     if (g_mode >= 0) return;
     const char* e = getenv("BPE_FA_BWD");
     g_mode = (e && e[0] == 'f') ? 1 : 0;
     if (const char* n = getenv("BPE_FA_SPLIT_NW")) {
-        int a = 4, c = 4;
+        int a = 4, c = 2;
         if (sscanf(n, "%d,%d", &a, &c) >= 1) {
             g_nw_dq = a == 8 ? 8 : 4;
-            g_nw_dkv = c == 8 ? 8 : 4;
+            g_nw_dkv = c == 8 ? 8 : c == 4 ? 4 : 2;
         }
     }
 }
@@ -467,7 +736,7 @@ int fa_bwd_config(int mode, int nw_dq, int nw_dkv) {
     config_init();
     if (mode >= 0) g_mode = mode ? 1 : 0;
     if (nw_dq > 0) g_nw_dq = nw_dq == 8 ? 8 : 4;
-    if (nw_dkv > 0) g_nw_dkv = nw_dkv == 8 ? 8 : 4;
+    if (nw_dkv > 0) g_nw_dkv = nw_dkv == 8 ? 8 : nw_dkv == 4 ? 4 : 2;
     return g_mode;
 }
 
@@ -488,11 +757,21 @@ static void dkv_launch(const FaArgs& a, hipStream_t s) {
 }
 
 template <bool C, bool R, bool RIN>
+static void dkv_pp_launch(const FaArgs& a, hipStream_t s) {
+    const int nkb = (a.S + 32 * split::PPNW - 1) / (32 * split::PPNW);
+    split::fa_bwd_dkv_pp_kernel<C, R, RIN><<<nkb * a.B * a.H, split::PPNW * 64, 4 * split::TILE + 1024, s>>>(
+        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.dkv_part, a.cos,
+        a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
+}
+
+template <bool C, bool R, bool RIN>
 static void split_launch(const FaArgs& a, hipStream_t s) {
     config_init();
     const int nq = g_nw_dq, nk = g_nw_dkv;
     if (nq == 8) dq_launch<C, R, RIN, 8>(a, s); else dq_launch<C, R, RIN, 4>(a, s);
-    if (nk == 8) dkv_launch<C, R, RIN, 8>(a, s); else dkv_launch<C, R, RIN, 4>(a, s);
+    if (nk == 2) dkv_pp_launch<C, R, RIN>(a, s);
+    else if (nk == 8) dkv_launch<C, R, RIN, 8>(a, s);
+    else dkv_launch<C, R, RIN, 4>(a, s);
 }
 
 void launch_fa_dkv_reduce(const FaArgs& a, hipStream_t s);  // flash_attn_bwd.hip

@@ -532,6 +532,7 @@ static bool fwd_v3_enabled() {
 }
 
 void launch_fa_fwd(const FaArgs& a, hipStream_t s) {
+    if (launch_fa_fwd_v4(a, s)) return;  // D = 64 without in-kernel RoPE (flash_attn_fwd_v4.hip)
     // rope 2 = Q / K already rotated: no RoPE inside the kernel
     if (a.D == 64 && a.rope != 1 && fwd_v3_enabled()) {
         if (a.causal) fwd_v3_launch<true>(a, s); else fwd_v3_launch<false>(a, s);

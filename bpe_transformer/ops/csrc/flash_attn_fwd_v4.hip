@@ -1,0 +1,222 @@
+// Flash attention forward v4 (D = 64, Q / K pre-rotated or no RoPE), gfx950 (MI355X).
+//
+// Parity target: reference contracts K7/K9/K10 (`tests/adapters.py:92-184`), as fa_fwd_kernel.
+//
+// Same geometry as fa_fwd_kernel (4 waves x 32 queries, swapped S^T = K.Q^T with the query on the lane,
+// register-staged double-buffered K / V, one barrier per 64-key tile, deferred rescale), restructured for the
+// VALU budget, which is what bounds D = 64 (a 32 x 64 score tile per wave costs 16 MFMAs but ~1000 cycles of
+// VALU in fa_fwd_kernel: per score a subtract, an exponential, a row-sum add, plus zeroing moves):
+//   * the running max is folded into the S accumulator's starting value (guide: "row constants as the initial
+//     accumulator"; the query is the lane, so it is one broadcast tuple): S' = K.(cQ)^T - m comes out of the
+//     MFMA ready for P = exp2(S'), no subtraction.  Only the rare rescale (a tile max more than 8 above m, or
+//     the first tile) subtracts, and then moves m and the tuple;
+//   * the row sum l is an MFMA: ones^T . P^T (a constant bf16 1.0 A operand, the same P^T fragments as P.V),
+//     accumulated -- and rescaled -- like O.  It sums the bf16-rounded P that O sums, and the 33 adds + the
+//     cross-lane exchange per tile leave the VALU for the matrix pipe, which has room;
+//   * K / V rows past the sequence end are loaded clamped (valid rows) instead of zero-filled behind a branch:
+//     their scores are masked to -inf, so P = 0 there; no zeroing moves, no branch around the loads.
+#include "fa_common.h"
+#include "kernels.h"
+
+#include <cstdlib>
+
+namespace bpe {
+namespace fa {
+namespace v4 {
+
+constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4, SPT = 2;  // SPT: 16-byte chunks per thread and tensor
+constexpr float THR = 8.0f;                                        // deferred-rescale threshold (log2 units)
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 2)
+fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
+                 long ld_q, long ld_kv, __bf16* __restrict__ O, long ld_o, float* __restrict__ LSE, int B, int H,
+                 int Hkv, int S, float scale_log2, int group, float* __restrict__ DQZ) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Ks = smem;             // [2][64][128 B]
+    char* Vs = smem + 2 * TILE;  // [2][64][128 B]
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    const int nqb = (S + 127) / 128;
+    int qrank, bh;
+    grouped_order((int)blockIdx.x, nqb, B * H, group, qrank, bh);
+    const int qb = nqb - 1 - qrank;  // heaviest (last) query blocks first
+    const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+    const int q0 = qb * 128, qw0 = q0 + 32 * w, qrow = qw0 + l31;
+
+    // Q fragments (B operand of S^T = K.Q^T), softmax scale * log2(e) folded in; rows past the end clamped
+    bf16x8 qf[KS];
+    {
+        const long qpos = min(qrow, S - 1);
+        const __bf16* qp = Q + ((long)b * S + qpos) * ld_q + (long)h * D;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            float x[8];
+            unpack8(*reinterpret_cast<const u16x8*>(qp + 16 * ks + 8 * hh), x);
+            qf[ks] = __builtin_bit_cast(bf16x8, pack8(x, scale_log2));
+        }
+    }
+    const int n_end = CAUSAL ? min(S, q0 + 128) : S;
+    const int ntiles = (n_end + 63) / 64;
+    const __bf16* kbase = K + (long)b * S * ld_kv + (long)hk * D;
+    const __bf16* vbase = Vv + (long)b * S * ld_kv + (long)hk * D;
+    u16x8 kreg[SPT], vreg[SPT];
+    auto load_tile = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int e = tid + 256 * i, row = e >> 3, c = e & 7;
+            const long key = min(t * 64 + row, S - 1);
+            kreg[i] = *reinterpret_cast<const u16x8*>(kbase + key * ld_kv + c * 8);
+            vreg[i] = *reinterpret_cast<const u16x8*>(vbase + key * ld_kv + c * 8);
+        }
+    };
+    auto write_tile = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int e = tid + 256 * i, row = e >> 3, c = e & 7;
+            *reinterpret_cast<u16x8*>(Ks + buf * TILE + swz<RB>(row, c)) = kreg[i];
+            *reinterpret_cast<u16x8*>(Vs + buf * TILE + swz<RB>(row, c)) = vreg[i];
+        }
+    };
+
+    f32x16 o[2], lacc, nm;  // O^T (d rows, query lane), row sums (every register), -m (S accumulator start)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        o[0][r] = 0.f;
+        o[1][r] = 0.f;
+        lacc[r] = 0.f;
+        nm[r] = 0.f;
+    }
+    float m_run = 0.f;
+    bf16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+
+    const int trow = 4 * hh + ((l & 15) >> 2);
+    const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
+
+    load_tile(0);
+    write_tile(0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const int cur = t & 1, n0 = t * 64;
+        if (t + 1 < ntiles) load_tile(t + 1);
+        if (!CAUSAL || n0 <= qw0 + 31) {
+            const char* Kc = Ks + cur * TILE;
+            char* Vc = Vs + cur * TILE;
+            f32x16 s[2];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+                s[kt] = nm;
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    s[kt] = mfma(lds_row16(Kc, swz<RB>(kt * 32 + l31, 2 * ks + hh)), qf[ks], s[kt]);
+            }
+            if ((CAUSAL && n0 + 63 > qw0) || (n0 + 64 > S)) {  // diagonal / ragged tile (wave-uniform)
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = n0 + kt * 32 + acc_row(r, hh);
+                        if ((CAUSAL && key > qrow) || key >= S) s[kt][r] = -INFINITY;
+                    }
+            }
+            float mt = s[0][0];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kt][r]);
+            mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+            // rescale (rare): the first tile sets m; later, a tile whose max exceeds m by more than THR moves it.
+            // Every P of this tile is formed after the decision (guide T13 hazard).
+            const bool grow = t == 0 || mt > THR;
+            if (!__all(!grow)) {
+                const float d = grow ? mt : 0.f;
+                const float alpha = t == 0 ? 0.f : fast_exp2(-d);  // tile 0: O, l are still zero
+                m_run += d;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    o[0][r] *= alpha;
+                    o[1][r] *= alpha;
+                    lacc[r] *= alpha;
+                    nm[r] = -m_run;
+                    s[0][r] -= d;
+                    s[1][r] -= d;
+                }
+            }
+            bf16x8 pf[4];  // P^T fragments: k-step kk = (key half kt, 16-key step ss) in the permuted k order
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int kt = kk >> 1, ss = kk & 1;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pf[kk][j] = (__bf16)fast_exp2(s[kt][8 * ss + j]);
+            }
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int kb = (kk >> 1) * 32 + 16 * (kk & 1);
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt)
+                    o[dt] = mfma(lds_tr_pair(Vc, tr_off<RB>(kb + trow, dt * 32 + tcol),
+                                             tr_off<RB>(kb + 8 + trow, dt * 32 + tcol)),
+                                 pf[kk], o[dt]);
+                lacc = mfma(ones, pf[kk], lacc);
+            }
+        }
+        if (t + 1 < ntiles) write_tile(cur ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: O = O^T / l (query on the lane, 4 consecutive d per register group), LSE = m + log2 l
+    if (qrow < S) {
+        const float lsum = lacc[0];
+        const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+        __bf16* op = O + ((long)b * S + qrow) * ld_o + (long)h * D;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const u16x4 v = {f2bf(o[dt][4 * i] * inv), f2bf(o[dt][4 * i + 1] * inv),
+                                 f2bf(o[dt][4 * i + 2] * inv), f2bf(o[dt][4 * i + 3] * inv)};
+                *reinterpret_cast<u16x4*>(op + dt * 32 + 8 * i + 4 * hh) = v;
+            }
+        if (hh == 0) LSE[((long)b * H + h) * S + qrow] = lsum > 0.f ? m_run + __log2f(lsum) : INFINITY;
+    }
+    if (DQZ != nullptr) {  // the fused (atomics) backward's fp32 dQ accumulator, zeroed as fa_fwd_kernel does
+        constexpr int C4 = D / 4;
+        const int spad = (S + 63) & ~63;
+        const int rows = min(128, spad - q0);
+        float* zb = DQZ + ((long)b * spad + q0) * ((long)H * D) + (long)h * D;
+        for (int e = tid; e < rows * C4; e += 256) {
+            const int r = e / C4, c = e % C4;
+            *reinterpret_cast<float4*>(zb + (long)r * H * D + 4 * c) = float4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+}
+
+}  // namespace v4
+}  // namespace fa
+}  // namespace bpe
+
+using namespace bpe;
+using namespace bpe::fa;
+
+// forward version for D = 64 without in-kernel RoPE: 4 (default, this file) or 2 (fa_fwd_kernel); BPE_FA_FWD
+// sets the initial value, fa_fwd_config changes it at run time (A/B, tests)
+static int g_fwd_ver = -1;
+
+int fa_fwd_config(int ver) {
+    if (g_fwd_ver < 0) {
+        const char* e = getenv("BPE_FA_FWD");
+        g_fwd_ver = (e && atoi(e) == 2) ? 2 : 4;
+    }
+    if (ver > 0) g_fwd_ver = ver == 2 ? 2 : 4;
+    return g_fwd_ver;
+}
+
+bool launch_fa_fwd_v4(const FaArgs& a, hipStream_t s) {
+    if (a.D != 64 || a.rope == 1 || fa_fwd_config(0) != 4) return false;
+    const int nqb = (a.S + 127) / 128;
+    auto* k = a.causal ? &v4::fa_fwd_v4_kernel<true> : &v4::fa_fwd_v4_kernel<false>;
+    k<<<nqb * a.B * a.H, 256, 4 * v4::TILE, s>>>(a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.lse, a.B, a.H, a.Hkv,
+                                                 a.S, a.scale * LOG2E, fa_group(a.B * a.H), a.dq_acc);
+    return true;
+}

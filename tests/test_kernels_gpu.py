@@ -521,10 +521,11 @@ def fused_bwd():
 @pytest.mark.parametrize("H,Hkv", [(4, 4), (8, 2)])
 @pytest.mark.parametrize("rope", ["fused", "prerotated", None])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("nw", [(4, 4), (8, 8)])
+@pytest.mark.parametrize("nw", [(4, 2), (4, 4), (8, 8)])
 def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal, nw):
-    """The split backward (dQ kernel + dK/dV kernel) at 4 and 8 waves per workgroup against the fp32 oracle's
-    autograd and against the fused atomics backward on the same forward outputs: dQ, dK, dV each."""
+    """The split backward (dQ kernel + dK/dV kernel) -- dK/dV on the ping-pong kernel (nw[1] == 2) or the plain
+    one at 4 / 8 waves -- against the fp32 oracle's autograd and against the fused atomics backward on the same
+    forward outputs: dQ, dK, dV each."""
     h = torch.ops.bpe_hip
     B, D = 2, 64
     torch.manual_seed(11)
@@ -546,7 +547,7 @@ def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal
         h.fa_bwd_config(1, 0, 0)
         fused = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)
     finally:
-        h.fa_bwd_config(prev, 4, 4)
+        h.fa_bwd_config(prev, 4, 2)
     assert torch.equal(got, again), "split backward is not deterministic"
     qr = qkv.float().cpu().requires_grad_(True)
     orf = ops.attention_qkv_reference(qr, B, S, H, Hkv, D, cos.cpu() if use_rope else None,
@@ -557,7 +558,9 @@ def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal
     for name, sl in (("dq", slice(0, HD)), ("dk", slice(HD, HD + KD)), ("dv", slice(HD + KD, HD + 2 * KD))):
         e = rel(got[:, sl].float().cpu(), gr[:, sl])
         ef = rel(fused[:, sl].float().cpu(), gr[:, sl])
-        assert e < 3e-2 and e < 1.5 * ef + 1e-3, (name, e, ef)
+        # the split kernels fold the softmax scale into bf16 Q (dQ kernel, as the forward does) / K (dK/dV kernel):
+        # one more bf16 rounding in the recomputed scores than the fused kernel's fp32 scaling
+        assert e < 3e-2 and e < 2.0 * ef + 2e-3, (name, e, ef)
 
 
 @pytest.mark.parametrize("S,D,H,Hkv,fused", [(1000, 64, 4, 4, False), (192, 128, 8, 4, True), (64, 64, 4, 2, True),
@@ -767,3 +770,30 @@ def test_accumulate_weight_grad_fp32_buffer(gpu_device):
     e32 = float((g32.double() - ref).norm() / ref.norm())
     e16 = float((g16.double() - ref).norm() / ref.norm())
     assert e32 < 1e-6 and e16 > 100 * e32, (e32, e16)
+
+
+@pytest.mark.parametrize("S,H,Hkv,causal", [(1024, 4, 4, True), (200, 8, 2, True), (1000, 4, 4, False), (64, 2, 2, True)])
+def test_flash_fwd_v4_matches_v2_and_oracle(gpu_device, S, H, Hkv, causal):
+    """The D = 64 forward v4 (running max in the S accumulator's start, row sum by MFMA) against fa_fwd_kernel
+    (v2) on the same inputs and against the fp32 oracle: O and the base-2 LSE."""
+    h = torch.ops.bpe_hip
+    B, D = 2, 64
+    torch.manual_seed(21)
+    qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device=gpu_device, dtype=torch.bfloat16)
+    qkv[:, : H * D] *= 2.0
+    q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
+    e = torch.empty(0, 0, device=gpu_device)
+    prev = h.fa_fwd_config(0)
+    try:
+        h.fa_fwd_config(4)
+        o4, l4 = h.fa_fwd(q, k, v, e, e, B, S, H, Hkv, D, causal, False, D ** -0.5, False)
+        h.fa_fwd_config(2)
+        o2, l2 = h.fa_fwd(q, k, v, e, e, B, S, H, Hkv, D, causal, False, D ** -0.5, False)
+    finally:
+        h.fa_fwd_config(prev)
+    orf = ops.attention_qkv_reference(qkv.float().cpu(), B, S, H, Hkv, D, None, None, causal)
+    e4, e2 = rel(o4.float().cpu(), orf), rel(o2.float().cpu(), orf)
+    assert e4 < 1e-2 and e4 < 1.5 * e2 + 1e-3, (e4, e2)
+    # v4's row sum is the MFMA sum of the bf16-rounded P that O accumulates (v2 adds the fp32 P): rows with few
+    # keys differ by up to ~one bf16 rounding of P, 2^-9 -> 0.003 in log2 units
+    assert torch.allclose(l4, l2, atol=6e-3, rtol=1e-4), float((l4 - l2).abs().max())
