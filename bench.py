@@ -84,6 +84,10 @@ def main() -> int:
     ap.add_argument("--comm-dtype", choices=["auto", "bf16", "fp32"], default="auto",
                     help="data-parallel all-reduce dtype (auto = the gradient dtype; fp32 with bf16 gradients "
                          "sums across ranks without a bf16 rounding per ring hop)")
+    ap.add_argument("--lm-head-mode", choices=["logits", "streamed"], default="logits",
+                    help="LM head + CE: one [tokens, vocab] logits buffer (default) or streamed token chunks with "
+                         "dh / dW formed in the forward (no full logits; ops/loss.py)")
+    ap.add_argument("--lm-head-chunk", type=int, default=0, help="token rows per chunk (0 = the mode's default)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = the plumbing config path (fp32, no HIP kernels), e.g. --model tinystories-17m --seq 256")
     ap.add_argument("--json-out", default=None)
@@ -109,6 +113,7 @@ def main() -> int:
     model = TransformerLM.from_config(cfg, device=dev, dtype=dtype)
     if args.precision == "fp8":
         model.enable_fp8()
+    model.lm_head_mode, model.lm_head_chunk = args.lm_head_mode, args.lm_head_chunk or None
     # phase timing: device events around forward / backward / exposed collective wait / clip + AdamW, read once
     # after the timed loop (stderr; the driver's scaling run then shows how much all-reduce stays exposed)
     gdt = {"bf16": torch.bfloat16, "fp32": torch.float32}[args.grad_dtype] if on_gpu else None
@@ -176,6 +181,7 @@ def main() -> int:
         "final_loss": round(loss_v, 4),
         "gemm_tuning": tuning,
         "grad_dtype": str(engine.flat.grad.dtype).replace("torch.", ""),
+        "lm_head_mode": args.lm_head_mode,
         "allreduce_dtype": (str(engine.ddp.comm_dtype if hasattr(engine.ddp, "comm_dtype") else
                                 engine.flat.grad.dtype).replace("torch.", "") if engine.ddp is not None else None),
     }

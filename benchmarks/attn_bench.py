@@ -63,7 +63,7 @@ def main():
     fl = 4.0 * B * H * S * S * D / 2
     if a.fwd_ab:
         prev = hip.fa_fwd_config(0)
-        times = {2: [], 4: []}
+        times = {2: [], 4: [], 5: []}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for _ in range(a.rounds):
             for ver in times:
@@ -84,7 +84,7 @@ def main():
             return
     if a.bwd_ab:
         arms = {"fused": (1, 0, 0), "split4x4": (0, 4, 4), "split4x8": (0, 4, 8), "split8x4": (0, 8, 4),
-                "split4_ppdkv": (0, 4, 2), "split8_ppdkv": (0, 8, 2)}
+                "split4_ppdkv": (0, 4, 2), "split_pp_both": (0, 2, 2)}
         prev = hip.fa_bwd_config(-1, 0, 0)
         times = {k: [] for k in arms}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -98,7 +98,7 @@ def main():
                 ev[1].record()
                 torch.cuda.synchronize()
                 times[name].append(ev[0].elapsed_time(ev[1]) / a.iters)
-        hip.fa_bwd_config(prev, 4, 2)
+        hip.fa_bwd_config(prev, 4, 4)
         for name, t in times.items():
             t = sorted(t)
             print(json.dumps({"shape": [B, S, H, Hkv, D], "arm": name, "bwd_ms_median": round(t[len(t) // 2], 4),

@@ -137,7 +137,9 @@ class TransformerLM(nn.Module):
         """Mean next-token cross-entropy; fused LM head + CE on the GPU."""
         h = self.hidden_states(in_indices)
         self._fence(self.lm_head)
-        return ops.lm_head_cross_entropy(h, self.lm_head.weight, targets, ignore_index)
+        return ops.lm_head_cross_entropy(h, self.lm_head.weight, targets, ignore_index,
+                                         chunk=getattr(self, "lm_head_chunk", None),
+                                         mode=getattr(self, "lm_head_mode", None))
 
     def load_reference_state_dict(self, state_dict: dict, strict: bool = True):
         """Load a reference-format state dict (strips ``torch.compile``'s ``_orig_mod.`` prefix,

@@ -700,6 +700,205 @@ fa_bwd_dkv_pp_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K,
         }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Ping-pong dQ kernel (the default for the split form).  Same math as fa_bwd_dq_kernel, on the schedule of
+// fa_bwd_dkv_pp_kernel: 8 waves in two staggered groups, waves w and w + 4 (one SIMD) owning adjacent 32-query
+// blocks (queries q0 + 64 (w & 3) + 32 (w >> 2)); per half-step j = 2 t + h (key tile t, 32-key half h):
+//   M(j): dQ^T += K^T.dS^T of half-step j - 1 (its transposed K fragments and bf16 dS read / packed in V(j - 1)),
+//         then S^T = K.(cQ)^T - lse and dP^T = V.dO^T - delta of half-step j (12 MFMAs)
+//   V(j): P^T = exp2(S^T), dS^T = P^T dP^T, bf16 packing, the transposed K reads for M(j + 1), and the staging of
+//         the next key tile (group g the rows [32 g, +32) of K and V, from registers loaded in V(2t - 2)).
+// delta = rowsum(dO * O) is computed in the prologue and written for the dK/dV kernel, as in fa_bwd_dq_kernel.
+template <bool CAUSAL, bool ROPE, bool ROPE_IN>
+__global__ void __launch_bounds__(PPNW * 64, 1)
+fa_bwd_dq_pp_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
+                    long ld_q, long ld_kv, const __bf16* __restrict__ O, long ld_o, const __bf16* __restrict__ dO,
+                    long ld_do, const float* __restrict__ LSE, float* __restrict__ DELTA, __bf16* __restrict__ dQ,
+                    long ld_dq, const float* __restrict__ cosT, const float* __restrict__ sinT, int B, int H, int Hkv,
+                    int S, float scale_log2, float scale, int group) {
+    constexpr int QB = 32 * PPNW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Ks = smem;             // [2][64 keys][128 B]  (roped K)
+    char* Vs = smem + 2 * TILE;  // [2][64 keys][128 B]
+
+    const int tid = threadIdx.x, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = w >> 2, wl = w & 3, gt = tid & 255;
+    const int nqb = (S + QB - 1) / QB;
+    int rank, bh;
+    grouped_order((int)blockIdx.x, nqb, B * H, group, rank, bh);
+    const int qblk = CAUSAL ? nqb - 1 - rank : rank;
+    const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+    const int q0 = qblk * QB, qw = q0 + 64 * wl + 32 * g, q = qw + l31;
+    const bool q_ok = q < S;
+    const long qc = q_ok ? q : S - 1;
+    const long qrow = (long)b * S + qc;
+
+    bf16x8 qf[KS], of[KS];
+    float dsum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int d0 = 16 * ks + 8 * hh;
+        u16x8 tq = *reinterpret_cast<const u16x8*>(Q + qrow * ld_q + (long)h * D + d0);
+        if (ROPE_IN) {
+            tq = rope_u16x8(tq, cosT + qc * (D / 2) + d0 / 2, sinT + qc * (D / 2) + d0 / 2, scale_log2);
+        } else {
+            float x[8];
+            unpack8(tq, x);
+            tq = pack8(x, scale_log2);
+        }
+        qf[ks] = __builtin_bit_cast(bf16x8, tq);
+        const u16x8 tg = *reinterpret_cast<const u16x8*>(dO + qrow * ld_do + (long)h * D + d0);
+        const u16x8 to = *reinterpret_cast<const u16x8*>(O + qrow * ld_o + (long)h * D + d0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dsum += bf2f(tg[i]) * bf2f(to[i]);
+        of[ks] = __builtin_bit_cast(bf16x8, tg);
+    }
+    dsum += __shfl_xor(dsum, 32, 64);
+    if (q_ok && hh == 0) DELTA[((long)b * H + h) * S + q] = dsum;
+    const float lse = LSE[((long)b * H + h) * S + qc];
+    const float nl = (q_ok && lse < INFINITY) ? -lse : -INFINITY;
+    f32x16 ns, nd;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        ns[r] = nl;
+        nd[r] = -dsum;
+    }
+    f32x16 acc[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
+
+    const int kend = CAUSAL ? min(S, q0 + QB) : S;
+    const int nkt = (kend + 63) / 64;
+    const int J = 2 * nkt;
+    const __bf16* kb = K + (long)b * S * ld_kv + (long)hk * D;
+    const __bf16* vb = Vv + (long)b * S * ld_kv + (long)hk * D;
+    const int srow = 32 * g + (gt >> 3), sc = gt & 7;
+    u16x8 kreg, vreg;
+    auto load_tile = [&](int t) {
+        const long kk = min(t * 64 + srow, S - 1);
+        kreg = *reinterpret_cast<const u16x8*>(kb + kk * ld_kv + sc * 8);
+        vreg = *reinterpret_cast<const u16x8*>(vb + kk * ld_kv + sc * 8);
+    };
+    auto write_tile = [&](int t) {
+        const bool ok = t * 64 + srow < S;
+        u16x8 kv = ok ? kreg : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        const u16x8 vv = ok ? vreg : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (ROPE_IN) {
+            const long kk = min(t * 64 + srow, S - 1);
+            kv = rope_u16x8(kv, cosT + kk * (D / 2) + sc * 4, sinT + kk * (D / 2) + sc * 4, 1.f);
+        }
+        *reinterpret_cast<u16x8*>(Ks + (t & 1) * TILE + swz<RB>(srow, sc)) = kv;
+        *reinterpret_cast<u16x8*>(Vs + (t & 1) * TILE + swz<RB>(srow, sc)) = vv;
+    };
+
+    const int trow = 4 * hh + ((l & 15) >> 2);
+    const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
+    if (nkt > 0) {
+        load_tile(0);
+        write_tile(0);
+        if (nkt > 1) load_tile(1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_bar();
+    if (g == 1) pp_bar();
+
+    f32x16 sp, dp;
+    bf16x8 db[2];      // bf16 dS^T of the previous half-step, k-steps s = 0, 1
+    bf16x8 kt_[2][2];  // its transposed K fragments [s][dt]
+    bool prev_active = false;
+    for (int j = 0; j <= J; ++j) {
+        const int t = j >> 1, hf = j & 1, k0 = t * 64 + 32 * hf;
+        const bool active = j < J && (!CAUSAL || k0 <= qw + 31);
+        // ---------------- M(j)
+        {
+            if (prev_active) {
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+                    for (int dt = 0; dt < 2; ++dt) acc[dt] = mfma(kt_[ss][dt], db[ss], acc[dt]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (active) {
+                const char* Kc = Ks + (t & 1) * TILE;
+                const char* Vc = Vs + (t & 1) * TILE;
+                sp = ns;
+                dp = nd;
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    const int koff = swz<RB>(32 * hf + l31, 2 * ks + hh);
+                    sp = mfma(lds_row16(Kc, koff), qf[ks], sp);
+                    dp = mfma(lds_row16(Vc, koff), of[ks], dp);
+                }
+            }
+        }
+        pp_bar();
+        if (j == J) break;
+        // ---------------- V(j)
+        {
+            char* Kc = Ks + (t & 1) * TILE;
+            if (active) {
+                const bool need_mask = (CAUSAL && k0 + 31 > qw) || (k0 + 32 > S);
+                if (need_mask) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = k0 + acc_row(r, hh);
+                        const float p = fast_exp2(sp[r]);
+                        const bool ok = key < S && (!CAUSAL || key <= q);
+                        dp[r] = ok ? p * dp[r] : 0.f;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(sp[r]) * dp[r];
+                }
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) db[ss][jj] = (__bf16)dp[8 * ss + jj];
+                    const int kr = 32 * hf + 16 * ss;
+#pragma unroll
+                    for (int dt = 0; dt < 2; ++dt)
+                        kt_[ss][dt] = lds_tr_pair(Kc, tr_off<RB>(kr + trow, 32 * dt + tcol),
+                                                  tr_off<RB>(kr + 8 + trow, 32 * dt + tcol));
+                }
+            }
+            prev_active = active;
+            if (hf == 0 && t + 1 < nkt) {
+                write_tile(t + 1);
+                if (t + 2 < nkt) load_tile(t + 2);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        pp_bar();
+    }
+    if (g == 0) pp_bar();
+
+    if (q_ok) {
+        __bf16* dqp = dQ + ((long)b * S + q) * ld_dq + (long)h * D;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d0 = 32 * dt + 8 * i + 4 * hh;
+                float x[4] = {acc[dt][4 * i] * scale, acc[dt][4 * i + 1] * scale, acc[dt][4 * i + 2] * scale,
+                              acc[dt][4 * i + 3] * scale};
+                if (ROPE) {
+#pragma unroll
+                    for (int pr = 0; pr < 2; ++pr) {
+                        const float c = cosT[(long)q * (D / 2) + d0 / 2 + pr];
+                        const float sn = sinT[(long)q * (D / 2) + d0 / 2 + pr];
+                        const float a = x[2 * pr], bb = x[2 * pr + 1];
+                        x[2 * pr] = a * c + bb * sn;
+                        x[2 * pr + 1] = -a * sn + bb * c;
+                    }
+                }
+                *reinterpret_cast<u16x4*>(dqp + d0) = u16x4{f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+            }
+    }
+}
+
 }  // namespace split
 }  // namespace fa
 }  // namespace bpe
@@ -709,18 +908,19 @@ using namespace bpe::fa;
 
 // Backward form: 0 = split (default for D = 64), 1 = fused (flash_attn_bwd.hip, the atomics form).  Initial value
 // from BPE_FA_BWD ("fused" / "split"), changeable at run time (fa_bwd_config) for same-process A/B and tests.
-// Waves per workgroup of the two split kernels: BPE_FA_SPLIT_NW="<dq>,<dkv>": dq 4 or 8; dkv 4 or 8 (the plain
-// kernel) or 2 (the ping-pong kernel: 8 waves in two staggered groups).  Default 4,2.
-static int g_mode = -1, g_nw_dq = 4, g_nw_dkv = 2;  // g_nw_dkv: 2 = the ping-pong dK/dV kernel (8 waves)
+// Waves per workgroup of the two split kernels: BPE_FA_SPLIT_NW="<dq>,<dkv>", each 4 or 8 (the plain kernels) or
+// 2 (the ping-pong kernels: 8 waves in two staggered groups).  Default 4,4: the measured best on MI355X
+// (profiles/bench/ab_attn_pp_b128.log: the ping-pong pair runs at 2 waves per SIMD and loses 13-27 %).
+static int g_mode = -1, g_nw_dq = 4, g_nw_dkv = 4;
 
 static void config_init() {
     if (g_mode >= 0) return;
     const char* e = getenv("BPE_FA_BWD");
     g_mode = (e && e[0] == 'f') ? 1 : 0;
     if (const char* n = getenv("BPE_FA_SPLIT_NW")) {
-        int a = 4, c = 2;
+        int a = 4, c = 4;
         if (sscanf(n, "%d,%d", &a, &c) >= 1) {
-            g_nw_dq = a == 8 ? 8 : 4;
+            g_nw_dq = a == 8 ? 8 : a == 4 ? 4 : 2;
             g_nw_dkv = c == 8 ? 8 : c == 4 ? 4 : 2;
         }
     }
@@ -735,7 +935,7 @@ bool fa_bwd_split_active(int D) {
 int fa_bwd_config(int mode, int nw_dq, int nw_dkv) {
     config_init();
     if (mode >= 0) g_mode = mode ? 1 : 0;
-    if (nw_dq > 0) g_nw_dq = nw_dq == 8 ? 8 : 4;
+    if (nw_dq > 0) g_nw_dq = nw_dq == 8 ? 8 : nw_dq == 4 ? 4 : 2;
     if (nw_dkv > 0) g_nw_dkv = nw_dkv == 8 ? 8 : nw_dkv == 4 ? 4 : 2;
     return g_mode;
 }
@@ -757,6 +957,14 @@ static void dkv_launch(const FaArgs& a, hipStream_t s) {
 }
 
 template <bool C, bool R, bool RIN>
+static void dq_pp_launch(const FaArgs& a, hipStream_t s) {
+    const int nqb = (a.S + 32 * split::PPNW - 1) / (32 * split::PPNW);
+    split::fa_bwd_dq_pp_kernel<C, R, RIN><<<nqb * a.B * a.H, split::PPNW * 64, 4 * split::TILE, s>>>(
+        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do, a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin,
+        a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
+}
+
+template <bool C, bool R, bool RIN>
 static void dkv_pp_launch(const FaArgs& a, hipStream_t s) {
     const int nkb = (a.S + 32 * split::PPNW - 1) / (32 * split::PPNW);
     split::fa_bwd_dkv_pp_kernel<C, R, RIN><<<nkb * a.B * a.H, split::PPNW * 64, 4 * split::TILE + 1024, s>>>(
@@ -768,7 +976,9 @@ template <bool C, bool R, bool RIN>
 static void split_launch(const FaArgs& a, hipStream_t s) {
     config_init();
     const int nq = g_nw_dq, nk = g_nw_dkv;
-    if (nq == 8) dq_launch<C, R, RIN, 8>(a, s); else dq_launch<C, R, RIN, 4>(a, s);
+    if (nq == 2) dq_pp_launch<C, R, RIN>(a, s);
+    else if (nq == 8) dq_launch<C, R, RIN, 8>(a, s);
+    else dq_launch<C, R, RIN, 4>(a, s);
     if (nk == 2) dkv_pp_launch<C, R, RIN>(a, s);
     else if (nk == 8) dkv_launch<C, R, RIN, 8>(a, s);
     else dkv_launch<C, R, RIN, 4>(a, s);

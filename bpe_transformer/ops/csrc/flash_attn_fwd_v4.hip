@@ -192,6 +192,209 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// v5: the v4 math on the ping-pong schedule of the split backward kernels (flash_attn_bwd_split.hip): 8 waves in
+// two groups of four, waves w and w + 4 (one SIMD) owning adjacent 32-query blocks (queries q0 + 64 (w & 3) +
+// 32 (w >> 2); a workgroup covers 256 queries), group 1 one barrier interval behind group 0.  Per 64-key tile t:
+//   M(t): O^T += V^T.P^T and l += ones.P^T of tile t - 1 (12 MFMAs; operands from V(t - 1)), then
+//         S'^T = K.(cQ)^T - m of tile t (8 MFMAs, K rows read at the top)
+//   V(t): mask, tile max, the rare rescale, P^T = exp2(S'^T) in bf16, the V^T reads for M(t + 1), and staging.
+// Three K / V buffers: tile t + 2 is written in V(t) into buffer (t + 2) % 3 (group g its rows [32 g, +32), from
+// registers loaded in V(t - 1)); that buffer's tile t - 1 was last read in V(t - 1), which group 1 runs in the
+// interval before group 0's V(t), and tile t + 2 is first read in M(t + 2), two intervals after group 1's write.
+constexpr int PPW = 8;
+
+__device__ __forceinline__ void pbar() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(PPW * 64, 1)
+fa_fwd_pp_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
+                 long ld_q, long ld_kv, __bf16* __restrict__ O, long ld_o, float* __restrict__ LSE, int B, int H,
+                 int Hkv, int S, float scale_log2, int group, float* __restrict__ DQZ) {
+    constexpr int QB = 32 * PPW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Ks = smem;             // [3][64][128 B]
+    char* Vs = smem + 3 * TILE;  // [3][64][128 B]
+    const int tid = threadIdx.x, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = w >> 2, wl = w & 3, gt = tid & 255;
+    const int nqb = (S + QB - 1) / QB;
+    int qrank, bh;
+    grouped_order((int)blockIdx.x, nqb, B * H, group, qrank, bh);
+    const int qb = nqb - 1 - qrank;
+    const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+    const int q0 = qb * QB, qw0 = q0 + 64 * wl + 32 * g, qrow = qw0 + l31;
+
+    bf16x8 qf[KS];
+    {
+        const long qpos = min(qrow, S - 1);
+        const __bf16* qp = Q + ((long)b * S + qpos) * ld_q + (long)h * D;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            float x[8];
+            unpack8(*reinterpret_cast<const u16x8*>(qp + 16 * ks + 8 * hh), x);
+            qf[ks] = __builtin_bit_cast(bf16x8, pack8(x, scale_log2));
+        }
+    }
+    const int n_end = CAUSAL ? min(S, q0 + QB) : S;
+    const int ntiles = (n_end + 63) / 64;
+    const __bf16* kbase = K + (long)b * S * ld_kv + (long)hk * D;
+    const __bf16* vbase = Vv + (long)b * S * ld_kv + (long)hk * D;
+    const int srow = 32 * g + (gt >> 3), sc = gt & 7;
+    u16x8 kreg, vreg;
+    auto load_tile = [&](int t) {
+        const long key = min(t * 64 + srow, S - 1);
+        kreg = *reinterpret_cast<const u16x8*>(kbase + key * ld_kv + sc * 8);
+        vreg = *reinterpret_cast<const u16x8*>(vbase + key * ld_kv + sc * 8);
+    };
+    auto write_tile = [&](int t) {
+        const int buf = t % 3;
+        *reinterpret_cast<u16x8*>(Ks + buf * TILE + swz<RB>(srow, sc)) = kreg;
+        *reinterpret_cast<u16x8*>(Vs + buf * TILE + swz<RB>(srow, sc)) = vreg;
+    };
+
+    f32x16 o[2], lacc, nm;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        o[0][r] = 0.f;
+        o[1][r] = 0.f;
+        lacc[r] = 0.f;
+        nm[r] = 0.f;
+    }
+    float m_run = 0.f;
+    bf16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+    const int trow = 4 * hh + ((l & 15) >> 2);
+    const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
+
+    // prologue: tiles 0 and 1 staged and visible, tile 2 in registers
+    load_tile(0);
+    write_tile(0);
+    if (ntiles > 1) {
+        load_tile(1);
+        write_tile(1);
+    }
+    if (ntiles > 2) load_tile(2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pbar();
+    if (g == 1) pbar();
+
+    f32x16 s[2];
+    bf16x8 pf[4];       // bf16 P^T of the previous tile, k-steps kk
+    bf16x8 vt[4][2];    // its V^T fragments [kk][dt]
+    bool prev_active = false;
+    for (int t = 0; t <= ntiles; ++t) {
+        const int n0 = t * 64;
+        const bool active = t < ntiles && (!CAUSAL || n0 <= qw0 + 31);
+        // ---------------- M(t)
+        if (prev_active) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(vt[kk][dt], pf[kk], o[dt]);
+                lacc = mfma(ones, pf[kk], lacc);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (active) {
+            const char* Kc = Ks + (t % 3) * TILE;
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+                s[kt] = nm;
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    s[kt] = mfma(lds_row16(Kc, swz<RB>(kt * 32 + l31, 2 * ks + hh)), qf[ks], s[kt]);
+            }
+        }
+        pbar();
+        if (t == ntiles) break;
+        // ---------------- V(t)
+        if (active) {
+            char* Vc = Vs + (t % 3) * TILE;
+            if ((CAUSAL && n0 + 63 > qw0) || (n0 + 64 > S)) {
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = n0 + kt * 32 + acc_row(r, hh);
+                        if ((CAUSAL && key > qrow) || key >= S) s[kt][r] = -INFINITY;
+                    }
+            }
+            float mt = s[0][0];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kt][r]);
+            mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+            // O and l hold tiles < t only (tile t - 1 was added in M(t)): a rescale here covers exactly them
+            const bool grow = t == 0 || mt > THR;
+            if (!__all(!grow)) {
+                const float d = grow ? mt : 0.f;
+                const float alpha = t == 0 ? 0.f : fast_exp2(-d);
+                m_run += d;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    o[0][r] *= alpha;
+                    o[1][r] *= alpha;
+                    lacc[r] *= alpha;
+                    nm[r] = -m_run;
+                    s[0][r] -= d;
+                    s[1][r] -= d;
+                }
+            }
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int kt = kk >> 1, ss = kk & 1;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pf[kk][j] = (__bf16)fast_exp2(s[kt][8 * ss + j]);
+                const int kb = kt * 32 + 16 * ss;
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt)
+                    vt[kk][dt] = lds_tr_pair(Vc, tr_off<RB>(kb + trow, dt * 32 + tcol),
+                                             tr_off<RB>(kb + 8 + trow, dt * 32 + tcol));
+            }
+        }
+        prev_active = active;
+        if (t + 2 < ntiles) {
+            write_tile(t + 2);
+            if (t + 3 < ntiles) load_tile(t + 3);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pbar();
+    }
+    if (g == 0) pbar();
+
+    if (qrow < S) {
+        const float lsum = lacc[0];
+        const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+        __bf16* op = O + ((long)b * S + qrow) * ld_o + (long)h * D;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const u16x4 v = {f2bf(o[dt][4 * i] * inv), f2bf(o[dt][4 * i + 1] * inv),
+                                 f2bf(o[dt][4 * i + 2] * inv), f2bf(o[dt][4 * i + 3] * inv)};
+                *reinterpret_cast<u16x4*>(op + dt * 32 + 8 * i + 4 * hh) = v;
+            }
+        if (hh == 0) LSE[((long)b * H + h) * S + qrow] = lsum > 0.f ? m_run + __log2f(lsum) : INFINITY;
+    }
+    if (DQZ != nullptr) {
+        constexpr int C4 = D / 4;
+        const int spad = (S + 63) & ~63;
+        const int rows = min(QB, spad - q0);
+        float* zb = DQZ + ((long)b * spad + q0) * ((long)H * D) + (long)h * D;
+        for (int e = tid; e < rows * C4; e += PPW * 64) {
+            const int r = e / C4, c = e % C4;
+            *reinterpret_cast<float4*>(zb + (long)r * H * D + 4 * c) = float4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+}
+
 }  // namespace v4
 }  // namespace fa
 }  // namespace bpe
@@ -203,17 +406,28 @@ using namespace bpe::fa;
 // sets the initial value, fa_fwd_config changes it at run time (A/B, tests)
 static int g_fwd_ver = -1;
 
+// 2 (fa_fwd_kernel), 4 (fa_fwd_v4_kernel, the default) or 5 (fa_fwd_pp_kernel); BPE_FA_FWD sets the initial value
 int fa_fwd_config(int ver) {
     if (g_fwd_ver < 0) {
         const char* e = getenv("BPE_FA_FWD");
-        g_fwd_ver = (e && atoi(e) == 2) ? 2 : 4;
+        const int v = e ? atoi(e) : 4;
+        g_fwd_ver = (v == 2 || v == 5) ? v : 4;
     }
-    if (ver > 0) g_fwd_ver = ver == 2 ? 2 : 4;
+    if (ver > 0) g_fwd_ver = (ver == 2 || ver == 5) ? ver : 4;
     return g_fwd_ver;
 }
 
 bool launch_fa_fwd_v4(const FaArgs& a, hipStream_t s) {
-    if (a.D != 64 || a.rope == 1 || fa_fwd_config(0) != 4) return false;
+    const int ver = fa_fwd_config(0);
+    if (a.D != 64 || a.rope == 1 || ver == 2) return false;
+    if (ver == 5) {
+        const int nqb = (a.S + 32 * v4::PPW - 1) / (32 * v4::PPW);
+        auto* k = a.causal ? &v4::fa_fwd_pp_kernel<true> : &v4::fa_fwd_pp_kernel<false>;
+        k<<<nqb * a.B * a.H, v4::PPW * 64, 6 * v4::TILE, s>>>(a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.lse, a.B,
+                                                              a.H, a.Hkv, a.S, a.scale * LOG2E, fa_group(a.B * a.H),
+                                                              a.dq_acc);
+        return true;
+    }
     const int nqb = (a.S + 127) / 128;
     auto* k = a.causal ? &v4::fa_fwd_v4_kernel<true> : &v4::fa_fwd_v4_kernel<false>;
     k<<<nqb * a.B * a.H, 256, 4 * v4::TILE, s>>>(a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.lse, a.B, a.H, a.Hkv,

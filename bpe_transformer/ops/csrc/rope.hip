@@ -4,12 +4,17 @@
 // verified against `tests/_snapshots/test_rope.npz`: pairs are
 // (x[2i], x[2i+1]), inv_freq_i = theta^(-2i/d), angle = pos * inv_freq_i.
 //
-// In the training hot path RoPE is fused into the attention kernels (applied
-// while Q/K tiles are staged); this kernel serves the standalone op and its
-// backward (inverse rotation).  cos/sin come from a host-precomputed fp32
+// Training hot path: at D = 64 rope_qk_kernel rotates Q and K of the fused
+// qkv buffer in place before the attention kernels (which un-rotate dQ / dK
+// in their epilogues); other head sizes rotate inside the attention kernels.
+// rope_kernel serves the standalone op and its backward (inverse rotation).  cos/sin come from a host-precomputed fp32
 // table [max_seq, d/2] (guide App. B: no on-device trig in memory-bound ops).
 // x is [R, H, D] contiguous, position of row r = pos[r].
 #include "common.h"
+
+#include <climits>
+#include <cstdint>
+#include <stdexcept>
 #include "kernels.h"
 
 namespace bpe {
@@ -46,20 +51,26 @@ __global__ void __launch_bounds__(256) rope_kernel(const T* __restrict__ x, T* _
 // positions 0..S-1 in every sequence): the training path rotates Q and K ONCE here, so the flash-attention
 // forward stages K tiles by LDS-DMA with no per-tile rotation and the backward re-reads rotated Q / K (it
 // un-rotates dQ / dK on output).  One 16-byte chunk (4 pairs) per thread step; V columns are not touched.
+// 2-D grid: blockIdx.x selects 64 chunk columns of a row (a chunk = 8 values = 4 pairs), blockIdx.y a group of
+// 4 * RQK_RPT rows; thread (col, sub) rotates chunk col of rows sub, sub + 4, ...  All index math is 32-bit per
+// row (the flat 64-bit `i / cpr`, `r % S` form ran at 3.2 TB/s: profiles/gpt2small_bf16_s1024_b128_kernels_v10.md).
+constexpr int RQK_RPT = 8;
 __global__ void __launch_bounds__(256) rope_qk_kernel(__bf16* __restrict__ qkv, long ld, const float* __restrict__ cosT,
-                                                      const float* __restrict__ sinT, long rows, int S, int cpr,
-                                                      int D) {
-    const long total = rows * cpr;  // cpr = (H + Hkv) * D / 8 chunks per row
-    const int half = D / 2;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const long r = i / cpr;
-        const int c = (int)(i - r * cpr);
-        const int d0 = (c * 8) % D;
-        const long p = r % S;
-        __bf16* px = qkv + r * ld + c * 8;
+                                                     const float* __restrict__ sinT, int rows, int S, int cpr,
+                                                     int D) {
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (c >= cpr) return;
+    const int half = D / 2, d2 = ((c * 8) % D) / 2;
+    const int r0 = blockIdx.y * (4 * RQK_RPT) + (threadIdx.x >> 6);
+#pragma unroll 4
+    for (int k = 0; k < RQK_RPT; ++k) {
+        const int r = r0 + 4 * k;
+        if (r >= rows) break;
+        const int p = r % S;
+        __bf16* px = qkv + (long)r * ld + c * 8;
         const u16x8 v = *reinterpret_cast<const u16x8*>(px);
-        const f32x4 cs = *reinterpret_cast<const f32x4*>(cosT + p * half + d0 / 2);
-        const f32x4 sn = *reinterpret_cast<const f32x4*>(sinT + p * half + d0 / 2);
+        const f32x4 cs = *reinterpret_cast<const f32x4*>(cosT + p * half + d2);
+        const f32x4 sn = *reinterpret_cast<const f32x4*>(sinT + p * half + d2);
         u16x8 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -78,8 +89,9 @@ using namespace bpe;
 void launch_rope_qk(void* qkv, long ld, const float* cosT, const float* sinT, long rows, int S, int H, int Hkv, int D,
                     hipStream_t s) {
     const int cpr = (H + Hkv) * D / 8;
-    const int grid = stream_grid((size_t)rows * cpr, 256, 8192);
-    rope_qk_kernel<<<grid, 256, 0, s>>>((__bf16*)qkv, ld, cosT, sinT, rows, S, cpr, D);
+    if (rows > INT32_MAX / 2) throw std::runtime_error("rope_qk_: too many rows");
+    const dim3 grid((cpr + 63) / 64, (unsigned)((rows + 4 * RQK_RPT - 1) / (4 * RQK_RPT)));
+    rope_qk_kernel<<<grid, 256, 0, s>>>((__bf16*)qkv, ld, cosT, sinT, (int)rows, S, cpr, D);
 }
 
 void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,

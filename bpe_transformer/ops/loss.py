@@ -1,11 +1,24 @@
 """Cross-entropy ops (``csrc/cross_entropy.hip``).
 
-``lm_head_cross_entropy`` fuses the LM-head GEMM with softmax-CE: the logits
-buffer is written once by the GEMM, read by the CE kernel which overwrites it
-IN PLACE with ``(softmax - onehot) / n``, and the backward is two GEMMs scaled
-by the incoming gradient (applied to the small GEMM outputs, never to the
-[tokens, vocab] buffer).  At GPT-2 shape that is one 1.6 GB bf16 buffer per
-step instead of logits + probabilities + gradient.
+``lm_head_cross_entropy`` fuses the LM-head GEMM with softmax-CE.  Two modes:
+
+* ``"logits"`` (default, fastest measured): the logits buffer is written once
+  by the GEMM, read by the CE kernel which overwrites it IN PLACE with
+  ``(softmax - onehot) / n``, and the backward is two GEMMs scaled by the
+  incoming gradient (applied to the small GEMM outputs, never to the
+  [tokens, vocab] buffer).  One [tokens, vocab] bf16 buffer lives from forward
+  to backward (13.2 GB at GPT-2 B 128) instead of logits + probabilities +
+  gradient.
+* ``"streamed"``: the full logits are never materialised.  Token chunks of
+  ``chunk`` rows run GEMM -> CE (in place) -> dh = dlogits W and
+  dW += dlogits^T h inside the forward, through ONE reused [chunk, vocab]
+  buffer; only dh ([tokens, d]) and an fp32 dW ([vocab, d]) are kept for the
+  backward, which scales them by the incoming gradient.  Same GEMM FLOPs as
+  "logits" (nothing is recomputed: the gradient of a mean CE needs only the
+  row's own softmax, known once its chunk's logits exist), memory
+  O(chunk * vocab).  Chunking over the vocabulary instead would need an
+  online max / sum across vocab chunks and a second logits pass for the
+  gradient -- 50 % more head FLOPs for the same memory bound.
 
 Reference contract K13 (``tests/adapters.py:440-455``).
 """
@@ -28,6 +41,16 @@ def default_lmhead_chunk() -> int:
     CE pass over the whole buffer, the measured default: ``docs/performance.md``, knob A/B)."""
     return int(os.environ.get("BPE_LMHEAD_CHUNK", "0"))
 
+
+def default_lmhead_mode() -> str:
+    """``BPE_LMHEAD_MODE``: ``logits`` (default) or ``streamed`` (see the module docstring)."""
+    m = os.environ.get("BPE_LMHEAD_MODE", "logits")
+    if m not in ("logits", "streamed"):
+        raise ValueError(f"BPE_LMHEAD_MODE must be 'logits' or 'streamed', got {m!r}")
+    return m
+
+
+STREAMED_DEFAULT_CHUNK = 16384
 
 _HEAD_DX_TN = os.environ.get("BPE_HEAD_DX_TN", "1") == "1"
 
@@ -104,6 +127,53 @@ class _LMHeadCEFn(torch.autograd.Function):
         return dh, torch.matmul(dlogits.t(), hs), None, None, None
 
 
+class _LMHeadCEStreamedFn(torch.autograd.Function):
+    """The ``"streamed"`` mode: loss, dh and dW formed chunk by chunk in the forward (module docstring)."""
+
+    @staticmethod
+    def forward(ctx, h: Tensor, w: Tensor, targets: Tensor, ignore_index: int, chunk: int):
+        from .gemm import accumulate_weight_grad
+
+        V = w.shape[0]
+        wp = getattr(w, "_bpe_padded", None)
+        if wp is None or wp.data_ptr() != w.data_ptr():
+            wp = w
+        nvalid = (targets != ignore_index).sum().clamp_min(1).to(torch.float32)
+        M = h.shape[0]
+        chunk = min(chunk, M)
+        buf = h.new_empty(chunk, wp.shape[0])
+        dh = torch.empty_like(h)
+        dw = torch.zeros(wp.shape, device=h.device, dtype=torch.float32)
+        parts = []
+        for c0 in range(0, M, chunk):
+            c1 = min(M, c0 + chunk)
+            lc = buf[: c1 - c0]
+            torch.matmul(h[c0:c1], wp.t(), out=lc)
+            # pad columns (zero weight rows) are exactly 0 and untouched by the CE kernel: no dh / dW contribution
+            parts.append(ops().ce_fwd_bwd(lc[:, :V], targets[c0:c1], ignore_index, True, nvalid)[0])
+            dh[c0:c1] = _head_dx(lc, wp)
+            accumulate_weight_grad(dw, lc, h[c0:c1])
+        ctx.save_for_backward(dh, dw)
+        ctx.w_param = w
+        return torch.cat(parts).sum() / nvalid
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        dh, dw = ctx.saved_tensors
+        w = ctx.w_param
+        dh = dh * g.to(dh.dtype)
+        rows = w.shape[0]
+        padded = getattr(w, "_bpe_padded", None) is not None and w._bpe_padded.data_ptr() == w.data_ptr()
+        mg = getattr(w, "_bpe_padded_grad" if padded else "main_grad", None)
+        if mg is not None:
+            mg.add_((dw[: mg.shape[0]] * g.float()).to(mg.dtype))
+            cb = getattr(w, "_bpe_grad_ready", None)
+            if cb is not None:
+                cb(w)
+            return dh, None, None, None, None
+        return dh, (dw[:rows] * g.float()).to(w.dtype), None, None, None
+
+
 class _CrossEntropyFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits: Tensor, targets: Tensor, ignore_index: int):
@@ -133,17 +203,22 @@ def cross_entropy(logits: Tensor, targets: Tensor, ignore_index: int = IGNORE_IN
 
 
 def lm_head_cross_entropy(h: Tensor, weight: Tensor, targets: Tensor, ignore_index: int = IGNORE_INDEX,
-                          chunk: int | None = None) -> Tensor:
+                          chunk: int | None = None, mode: str | None = None) -> Tensor:
     """``cross_entropy(h @ weight.T, targets)`` without keeping separate logits/probs/grad buffers.
 
-    h: ``[..., d]``, weight: ``[V, d]``, targets: ``[...]``.  ``chunk``: run the GEMM + CE in token chunks of
-    this many rows (0 = one pass; None = :func:`default_lmhead_chunk`).
+    h: ``[..., d]``, weight: ``[V, d]``, targets: ``[...]``.  ``mode``: ``"logits"`` or ``"streamed"`` (module
+    docstring; None = :func:`default_lmhead_mode`).  ``chunk``: token-chunk rows (logits mode: 0 = one pass,
+    None = :func:`default_lmhead_chunk`; streamed mode: the reused buffer's rows, None / 0 =
+    ``STREAMED_DEFAULT_CHUNK``).
     """
-    if chunk is None:
-        chunk = default_lmhead_chunk()
+    mode = mode or default_lmhead_mode()
     d = h.shape[-1]
     h2 = h.reshape(-1, d)
     t = targets.reshape(-1).long().contiguous()
+    if h.is_cuda and h.dtype == torch.bfloat16 and mode == "streamed":
+        return _LMHeadCEStreamedFn.apply(h2, weight, t, ignore_index, int(chunk or STREAMED_DEFAULT_CHUNK))
+    if chunk is None:
+        chunk = default_lmhead_chunk()
     if h.is_cuda and h.dtype in (torch.float32, torch.bfloat16):
         return _LMHeadCEFn.apply(h2, weight, t, ignore_index, int(chunk))
     return cross_entropy(h2 @ weight.t(), t, ignore_index)

@@ -65,6 +65,10 @@ class TrainConfig:
     # every add; else the parameter dtype) | bf16 | fp32
     grad_dtype: str = "auto"
     comm_dtype: str = "auto"  # data-parallel all-reduce dtype: auto (= grad dtype) | bf16 | fp32
+    # LM head + CE (ops/loss.py): logits (one [tokens, vocab] buffer, fastest) | streamed (token chunks of
+    # lm_head_chunk rows, dh / dW formed in the forward: memory O(chunk * vocab)); lm_head_chunk 0 = default
+    lm_head_mode: str = "logits"
+    lm_head_chunk: int = 0
 
     def resolved_grad_dtype(self, param_dtype):
         import torch

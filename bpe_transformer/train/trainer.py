@@ -61,6 +61,10 @@ class Trainer:
             if dev.type != "cuda":
                 raise ValueError("precision=fp8 needs the GPU path (MI355X fp8 MFMA)")
             self.model.enable_fp8()
+        if cfg.lm_head_mode not in ("logits", "streamed"):
+            raise ValueError(f"lm_head_mode must be 'logits' or 'streamed', got {cfg.lm_head_mode!r}")
+        self.model.lm_head_mode = cfg.lm_head_mode
+        self.model.lm_head_chunk = cfg.lm_head_chunk or None
         o = cfg.optim
         self.engine = TrainEngine(self.model, self.info, lr=o.lr, betas=o.betas, eps=o.eps,
                                   weight_decay=o.weight_decay, max_grad_norm=o.max_grad_norm,

@@ -126,9 +126,11 @@ def test_lm_head_cross_entropy(gpu_device):
     assert rel(w.grad.cpu(), wr.grad) < 3e-2
 
 
-def test_lm_head_ce_chunked_matches_one_pass(gpu_device):
-    """Token-chunked LM head + CE == one pass: M not a multiple of the chunk, ignore_index rows, the row-padded
-    vocab weight from the flat buffer, and the LM-head dW accumulated in place into the flat gradient."""
+@pytest.mark.parametrize("mode,chunk", [("logits", 384), ("streamed", 384), ("streamed", 4096)])
+def test_lm_head_ce_chunked_matches_one_pass(gpu_device, mode, chunk):
+    """Token-chunked LM head + CE (the logits mode's chunks, or the streamed mode that forms dh / dW in the forward
+    and never holds the full logits) == one pass: M not a multiple of the chunk, ignore_index rows, the
+    row-padded vocab weight from the flat buffer, and the LM-head dW accumulated in place into the flat gradient."""
     from bpe_transformer.optim import FlatParameters
 
     V, d, M = 5003, 256, 1000
@@ -141,14 +143,14 @@ def test_lm_head_ce_chunked_matches_one_pass(gpu_device):
     t = torch.randint(0, V, (M,), device=gpu_device)
     t[::7] = -100
     out = {}
-    for chunk in (0, 384):
+    for key, (md, ck) in {"one": ("logits", 0), "chunked": (mode, chunk)}.items():
         flat.zero_grad()
         h = h0.clone().requires_grad_(True)
-        loss = ops.lm_head_cross_entropy(h, head.weight, t, chunk=chunk)
+        loss = ops.lm_head_cross_entropy(h, head.weight, t, chunk=ck, mode=md)
         (3.0 * loss).backward()
         torch.cuda.synchronize()
-        out[chunk] = (loss.detach().float(), h.grad.float(), flat.grad.float().clone())
-    (l0, dh0, g0), (l1, dh1, g1) = out[0], out[384]
+        out[key] = (loss.detach().float(), h.grad.float(), flat.grad.float().clone())
+    (l0, dh0, g0), (l1, dh1, g1) = out["one"], out["chunked"]
     # same math; only the library GEMM's per-chunk kernel choice (rounding of the bf16 logits) may differ
     assert abs(l0.item() - l1.item()) < 1e-3
     assert rel(dh1, dh0) < 1e-2
@@ -521,10 +523,10 @@ def fused_bwd():
 @pytest.mark.parametrize("H,Hkv", [(4, 4), (8, 2)])
 @pytest.mark.parametrize("rope", ["fused", "prerotated", None])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("nw", [(4, 2), (4, 4), (8, 8)])
+@pytest.mark.parametrize("nw", [(2, 2), (4, 4), (8, 8)])
 def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal, nw):
-    """The split backward (dQ kernel + dK/dV kernel) -- dK/dV on the ping-pong kernel (nw[1] == 2) or the plain
-    one at 4 / 8 waves -- against the fp32 oracle's autograd and against the fused atomics backward on the same
+    """The split backward (dQ kernel + dK/dV kernel) -- the ping-pong kernels (nw == 2) or the plain ones at 4 / 8
+    waves -- against the fp32 oracle's autograd and against the fused atomics backward on the same
     forward outputs: dQ, dK, dV each."""
     h = torch.ops.bpe_hip
     B, D = 2, 64
@@ -547,7 +549,7 @@ def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal
         h.fa_bwd_config(1, 0, 0)
         fused = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)
     finally:
-        h.fa_bwd_config(prev, 4, 2)
+        h.fa_bwd_config(prev, 4, 4)
     assert torch.equal(got, again), "split backward is not deterministic"
     qr = qkv.float().cpu().requires_grad_(True)
     orf = ops.attention_qkv_reference(qr, B, S, H, Hkv, D, cos.cpu() if use_rope else None,
@@ -613,10 +615,12 @@ def test_flash_bwd_streaming_path_matches(gpu_device, fused_bwd):
     assert rel(full[:, : H * D], half[:, : H * D]) < 1e-3
 
 
-def test_rope_qk_inplace(gpu_device):
-    """rope_qk_ rotates exactly the Q and K heads of the fused activation (positions restart per sequence)."""
+@pytest.mark.parametrize("H,Hkv,D", [(4, 2, 64), (32, 4, 64), (12, 12, 64), (4, 4, 128)])
+def test_rope_qk_inplace(gpu_device, H, Hkv, D):
+    """rope_qk_ rotates exactly the Q and K heads of the fused activation (positions restart per sequence); chunk
+    columns per row 48 / 288 / 192 / 128 cover partial and whole 64-column blocks, 200 rows a partial row group."""
     torch.manual_seed(4)
-    B, S, H, Hkv, D = 2, 100, 4, 2, 64
+    B, S = 2, 100
     qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device=gpu_device, dtype=torch.bfloat16)
     cos, sin = R.rope_tables(D, S + 7, 10000.0, device=gpu_device)
     out = qkv.clone()
@@ -772,10 +776,12 @@ def test_accumulate_weight_grad_fp32_buffer(gpu_device):
     assert e32 < 1e-6 and e16 > 100 * e32, (e32, e16)
 
 
-@pytest.mark.parametrize("S,H,Hkv,causal", [(1024, 4, 4, True), (200, 8, 2, True), (1000, 4, 4, False), (64, 2, 2, True)])
-def test_flash_fwd_v4_matches_v2_and_oracle(gpu_device, S, H, Hkv, causal):
-    """The D = 64 forward v4 (running max in the S accumulator's start, row sum by MFMA) against fa_fwd_kernel
-    (v2) on the same inputs and against the fp32 oracle: O and the base-2 LSE."""
+@pytest.mark.parametrize("ver", [4, 5])
+@pytest.mark.parametrize("S,H,Hkv,causal", [(1024, 4, 4, True), (200, 8, 2, True), (1000, 4, 4, False), (64, 2, 2, True),
+                                            (600, 2, 2, True)])
+def test_flash_fwd_v4_matches_v2_and_oracle(gpu_device, S, H, Hkv, causal, ver):
+    """The D = 64 forward v4 (running max in the S accumulator's start, row sum by MFMA) and its ping-pong form v5
+    against fa_fwd_kernel (v2) on the same inputs and against the fp32 oracle: O and the base-2 LSE."""
     h = torch.ops.bpe_hip
     B, D = 2, 64
     torch.manual_seed(21)
@@ -785,7 +791,7 @@ def test_flash_fwd_v4_matches_v2_and_oracle(gpu_device, S, H, Hkv, causal):
     e = torch.empty(0, 0, device=gpu_device)
     prev = h.fa_fwd_config(0)
     try:
-        h.fa_fwd_config(4)
+        h.fa_fwd_config(ver)
         o4, l4 = h.fa_fwd(q, k, v, e, e, B, S, H, Hkv, D, causal, False, D ** -0.5, False)
         h.fa_fwd_config(2)
         o2, l2 = h.fa_fwd(q, k, v, e, e, B, S, H, Hkv, D, causal, False, D ** -0.5, False)

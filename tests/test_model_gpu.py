@@ -196,3 +196,26 @@ def test_padded_lm_head_matches_unpadded(gpu_device):
     assert torch.count_nonzero(ga[1000:]) == 0 and torch.count_nonzero(wp[1000:]) == 0
     e = (ga[:1000].float() - gb.float()).norm() / gb.float().norm()
     assert e < 1e-2, float(e)
+
+
+def test_streamed_lm_head_trains_like_logits_mode(gpu_device):
+    """lm_head_mode "streamed" (dh / dW formed chunk by chunk in the forward, no full logits buffer; ops/loss.py)
+    through the training engine tracks the default logits mode step for step, padded head included."""
+    from bpe_transformer.train.engine import TrainEngine
+
+    _, a = _pair(gpu_device)
+    b = copy.deepcopy(a)
+    b.lm_head_mode, b.lm_head_chunk = "streamed", 96  # 256 tokens -> chunks 96, 96, 64
+    ea = TrainEngine(a, lr=1e-3, weight_decay=0.1, max_grad_norm=1.0)
+    eb = TrainEngine(b, lr=1e-3, weight_decay=0.1, max_grad_norm=1.0)
+    ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    tgt[0, ::5] = -100
+    for _ in range(4):
+        la = ea.train_step([(ids, tgt)])
+        lb = eb.train_step([(ids, tgt)])
+        assert abs(la.item() - lb.item()) < 5e-3, (la.item(), lb.item())
+    assert torch.count_nonzero(b.lm_head.weight._bpe_padded[1000:]) == 0
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        e = (pa.float() - pb.float()).norm() / pa.float().norm()
+        assert e < 1e-2, (n, float(e))
