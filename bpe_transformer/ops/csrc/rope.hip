@@ -51,26 +51,21 @@ __global__ void __launch_bounds__(256) rope_kernel(const T* __restrict__ x, T* _
 // positions 0..S-1 in every sequence): the training path rotates Q and K ONCE here, so the flash-attention
 // forward stages K tiles by LDS-DMA with no per-tile rotation and the backward re-reads rotated Q / K (it
 // un-rotates dQ / dK on output).  One 16-byte chunk (4 pairs) per thread step; V columns are not touched.
-// 2-D grid: blockIdx.x selects 64 chunk columns of a row (a chunk = 8 values = 4 pairs), blockIdx.y a group of
-// 4 * RQK_RPT rows; thread (col, sub) rotates chunk col of rows sub, sub + 4, ...  All index math is 32-bit per
-// row (the flat 64-bit `i / cpr`, `r % S` form ran at 3.2 TB/s: profiles/gpt2small_bf16_s1024_b128_kernels_v10.md).
-constexpr int RQK_RPT = 8;
+// One thread per (row, chunk column c of a head): the cos / sin of that column (32 bytes, from L2) are loaded once
+// and applied to the chunk of every Q and K head of the row (16 bytes each, 4 heads' loads in flight per step).
+// The flat form -- one (row, chunk) per thread, cos / sin re-read per chunk, 64-bit index math -- moved 3x the
+// data bytes through L2 and ran at 3.2 TB/s (profiles/gpt2small_bf16_s1024_b128_kernels_v10.md).
 __global__ void __launch_bounds__(256) rope_qk_kernel(__bf16* __restrict__ qkv, long ld, const float* __restrict__ cosT,
-                                                     const float* __restrict__ sinT, int rows, int S, int cpr,
+                                                     const float* __restrict__ sinT, int rows, int S, int nh,
                                                      int D) {
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    if (c >= cpr) return;
-    const int half = D / 2, d2 = ((c * 8) % D) / 2;
-    const int r0 = blockIdx.y * (4 * RQK_RPT) + (threadIdx.x >> 6);
-#pragma unroll 4
-    for (int k = 0; k < RQK_RPT; ++k) {
-        const int r = r0 + 4 * k;
-        if (r >= rows) break;
-        const int p = r % S;
-        __bf16* px = qkv + (long)r * ld + c * 8;
-        const u16x8 v = *reinterpret_cast<const u16x8*>(px);
-        const f32x4 cs = *reinterpret_cast<const f32x4*>(cosT + p * half + d2);
-        const f32x4 sn = *reinterpret_cast<const f32x4*>(sinT + p * half + d2);
+    const int cph = D / 8, rpb = 256 / cph;
+    const int r = blockIdx.x * rpb + (int)threadIdx.x / cph, c = (int)threadIdx.x % cph;
+    if (r >= rows || (int)threadIdx.x >= rpb * cph) return;
+    const int p = r % S;
+    const f32x4 cs = *reinterpret_cast<const f32x4*>(cosT + p * (D / 2) + 4 * c);
+    const f32x4 sn = *reinterpret_cast<const f32x4*>(sinT + p * (D / 2) + 4 * c);
+    __bf16* row = qkv + (long)r * ld + c * 8;
+    auto rot = [&](const u16x8 v) {
         u16x8 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -78,8 +73,17 @@ __global__ void __launch_bounds__(256) rope_qk_kernel(__bf16* __restrict__ qkv, 
             o[2 * j] = f2bf(a * cs[j] - b * sn[j]);
             o[2 * j + 1] = f2bf(a * sn[j] + b * cs[j]);
         }
-        *reinterpret_cast<u16x8*>(px) = o;
+        return o;
+    };
+    int h = 0;
+    for (; h + 4 <= nh; h += 4) {
+        u16x8 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const u16x8*>(row + (h + i) * D);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<u16x8*>(row + (h + i) * D) = rot(v[i]);
     }
+    for (; h < nh; ++h) *reinterpret_cast<u16x8*>(row + h * D) = rot(*reinterpret_cast<const u16x8*>(row + h * D));
 }
 
 }  // namespace bpe
@@ -88,10 +92,11 @@ using namespace bpe;
 
 void launch_rope_qk(void* qkv, long ld, const float* cosT, const float* sinT, long rows, int S, int H, int Hkv, int D,
                     hipStream_t s) {
-    const int cpr = (H + Hkv) * D / 8;
     if (rows > INT32_MAX / 2) throw std::runtime_error("rope_qk_: too many rows");
-    const dim3 grid((cpr + 63) / 64, (unsigned)((rows + 4 * RQK_RPT - 1) / (4 * RQK_RPT)));
-    rope_qk_kernel<<<grid, 256, 0, s>>>((__bf16*)qkv, ld, cosT, sinT, (int)rows, S, cpr, D);
+    if (D % 8 != 0 || D > 256) throw std::runtime_error("rope_qk_: head size must be a multiple of 8, at most 256");
+    const int rpb = 256 / (D / 8);
+    rope_qk_kernel<<<(unsigned)((rows + rpb - 1) / rpb), 256, 0, s>>>((__bf16*)qkv, ld, cosT, sinT, (int)rows, S,
+                                                                      H + Hkv, D);
 }
 
 void launch_rope(int dtype, const void* x, void* y, const int64_t* pos, const float* cosT, const float* sinT,

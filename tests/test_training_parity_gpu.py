@@ -10,7 +10,8 @@ weights on the same real-token batches for 150 steps:
 * eager: a separate module tree written here with ``torch.nn.functional.scaled_dot_product_attention``, fp32
   parameters under bf16 autocast, ``torch.optim.AdamW``, ``clip_grad_norm_`` and the same cosine schedule.
 
-Tokens: the reference's sample TinyStories tokenizer (10 000 vocab) over ``corpus.en`` + ``tinystories_sample.txt``.
+Tokens: a 4 096-token BPE vocabulary trained here (``train_bpe``) on ``tinystories_sample.txt``, encoding
+``corpus.en`` + ``tinystories_sample.txt`` (the reference's pickled sample tokenizer is not shipped to the GPU box).
 batch x seq = 4 x 1024 (a multiple of 256, so every fused path engages).  A second run accumulates 4 micro-batches
 of one sequence per step (fp32 gradient buffer).  Set ``BPE_PARITY_LOG=<dir>`` to write both loss curves.
 """
@@ -119,10 +120,11 @@ class EagerLM(nn.Module):
 
 
 def _tokens():
+    from bpe_transformer import train_bpe
     from bpe_transformer.tokenization import BPETokenizer
 
-    tok = BPETokenizer.from_files(FIXTURES / "sample_tokenizer" / "vocab.pkl",
-                                  FIXTURES / "sample_tokenizer" / "merges.pkl", ["<|endoftext|>"])
+    vocab, merges = train_bpe(str(FIXTURES / "tinystories_sample.txt"), 4096, ["<|endoftext|>"])
+    tok = BPETokenizer(vocab, merges, ["<|endoftext|>"])
     text = (FIXTURES / "corpus.en").read_text(encoding="utf-8") + "<|endoftext|>"
     text += (FIXTURES / "tinystories_sample.txt").read_text(encoding="utf-8") * 8
     return torch.tensor(tok.encode(text), dtype=torch.long), len(tok.vocab)
