@@ -35,10 +35,6 @@ def main():
     ap.add_argument("--tokens", type=int, default=131072)
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--ff", type=int, default=2048)
-    ap.add_argument("--stagger-ab", default=None,
-                    help="comma list of first-wave stagger rounds (ops.gpp_stagger_config): interleaved A/B of the "
-                         "two fused GEMMs only")
-    ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
     M, d, F = a.tokens, a.dim, a.ff
     h = ops()
@@ -61,22 +57,6 @@ def main():
         "dY@W2 (hipBLASLt)": (lambda: torch.matmul(dy, w2), M * F * 2, gemm_flops),
         "dY@W2 + swiglu_bwd (unfused)": (lambda: h.swiglu_bwd(torch.matmul(dy, w2), gu), 6 * M * F * 2, gemm_flops),
     }
-    if a.stagger_ab:
-        arms = [int(v) for v in a.stagger_ab.split(",")]
-        prev = h.gpp_stagger_config(-1, -1)
-        res = {(n, v): [] for n in ("gemm_swiglu_fwd(fused)", "gemm_swiglu_bwd(fused)") for v in arms}
-        for _ in range(a.rounds):
-            for v in arms:
-                h.gpp_stagger_config(v, v)
-                for n in ("gemm_swiglu_fwd(fused)", "gemm_swiglu_bwd(fused)"):
-                    res[(n, v)].append(timeit(rows[n][0], iters=10))
-        h.gpp_stagger_config(prev // 1000, prev % 1000)
-        for (n, v), t in res.items():
-            t = sorted(t)
-            flops = rows[n][2]
-            print(json.dumps({"op": n, "stagger": v, "ms_median": round(t[len(t) // 2], 4), "ms_min": round(t[0], 4),
-                              "TFps": round(flops / t[len(t) // 2] / 1e9, 1)}), flush=True)
-        return
     for name, (fn, nbytes, flops) in rows.items():
         ms = timeit(fn)
         r = {"op": name, "shape": [M, d, F], "ms": round(ms, 4), "TBps": round(nbytes / ms / 1e9, 2)}

@@ -396,7 +396,6 @@ struct Epi {
     int prio = 0;  // 1: group 1 (the younger waves 4-7) runs at s_setprio 1 (guide T5, static form)
     const float* sa = nullptr;  // F8: device-resident per-tensor inverse scales of A and B (output x sa x sb)
     const float* sb = nullptr;
-    int stagger = 0;  // s_sleep(127) rounds for half of the first wave of workgroups (gpp_stagger_config)
 };
 
 template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, int SPREAD = 0, int F8 = 0>
@@ -423,13 +422,6 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
 
     constexpr bool SPR = SPREAD != 0;
-    // Epilogue-bound fused kernels: every CU starts its first tile together, so all CUs run their main loops
-    // at the same time (HBM idle) and then their epilogues (matrix cores idle).  Delaying every other
-    // workgroup of the first wave by about half a tile shifts half the CUs by half a period; the dispatcher
-    // hands later tiles to whichever CU frees first, so the offset persists and the epilogue traffic of one
-    // half overlaps the main loops of the other.
-    if (ep.stagger > 0 && orig < 256 && ((orig >> 3) & 1))
-        for (int i = 0; i < ep.stagger; ++i) __builtin_amdgcn_s_sleep(127);
     if (ep.prio && g == 1) __builtin_amdgcn_s_setprio(1);  // g is wave-uniform (readfirstlane): a scalar branch
     f32x4 acc[8][4];
 #pragma unroll
@@ -832,29 +824,6 @@ static int spread_mode(bool weight_grad = false) {
     return m >= 0 ? m : (weight_grad ? 2 : 1);
 }
 
-// BPE_GPP_STAGGER="<fwd>,<bwd>": s_sleep(127) rounds (~3.4 us each) for half of the first wave of workgroups of
-// the fused SwiGLU forward / backward GEMMs (see gemm_pp_kernel); changeable at run time (gpp_stagger_config).
-static int g_stagger[2] = {-1, -1};
-
-static void stagger_init() {
-    if (g_stagger[0] >= 0) return;
-    g_stagger[0] = g_stagger[1] = 0;
-    if (const char* e = getenv("BPE_GPP_STAGGER")) {
-        int f = 0, b = 0;
-        const int n = sscanf(e, "%d,%d", &f, &b);
-        if (n >= 1) g_stagger[0] = f > 0 ? f : 0;
-        g_stagger[1] = n == 2 ? (b > 0 ? b : 0) : g_stagger[0];
-    }
-}
-
-// fwd / bwd < 0 leave a setting unchanged; returns the forward setting * 1000 + the backward one afterwards
-int gpp_stagger_config(int fwd, int bwd) {
-    stagger_init();
-    if (fwd >= 0) g_stagger[0] = fwd > 64 ? 64 : fwd;
-    if (bwd >= 0) g_stagger[1] = bwd > 64 ? 64 : bwd;
-    return g_stagger[0] * 1000 + g_stagger[1];
-}
-
 // dgu = swiglu_bwd(dY . W2, gu): A = dY [M][R] (K-major), B = W2 [R][F] (MN-major)
 void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,
                                long ldg, int M, int F, int R, hipStream_t s) {
@@ -870,8 +839,6 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
     const int grid = (M / BT) * (F / BT);
     Epi ep{(const __bf16*)gu, (__bf16*)dgu, ldg, F};
     ep.prio = prio_mode();
-    stagger_init();
-    ep.stagger = g_stagger[1];
     k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)dY, ldy, (const __bf16*)W2, ldw, nullptr, nullptr, 0, 0.f, M, F, R,
                                   1, ep);
 }
@@ -889,8 +856,6 @@ void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ld
     const int grid = (M / BT) * (F / (BT / 2));
     Epi ep{nullptr, (__bf16*)gu, ldg, F, (__bf16*)act, lda_};
     ep.prio = prio_mode();
-    stagger_init();
-    ep.stagger = g_stagger[0];
     k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)X, ldx, (const __bf16*)W13, ldw, nullptr, nullptr, 0, 0.f, M, 2 * F,
                                   R, 1, ep);
 }

@@ -79,7 +79,6 @@ void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, 
 
 void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ldw, void* gu, long ldg, void* act,
                                long lda_, int M, int F, int R, hipStream_t s);
-int gpp_stagger_config(int fwd, int bwd);  // fused SwiGLU GEMMs: first-wave stagger rounds (gemm_pp.hip)
 void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,
                                long ldg, int M, int F, int R, hipStream_t s);
 

@@ -563,7 +563,6 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
 // whether fa_bwd uses (and fa_fwd should zero) the fp32 dQ accumulator for head dim D
 bool fa_bwd_needs_dq_acc(int64_t D) { return !fa_bwd_split_active((int)D); }
 int64_t fa_fwd_config_op(int64_t ver) { return fa_fwd_config((int)ver); }
-int64_t gpp_stagger_config_op(int64_t fwd, int64_t bwd) { return gpp_stagger_config((int)fwd, (int)bwd); }
 int64_t fa_bwd_config_op(int64_t mode, int64_t nw_dq, int64_t nw_dkv) {
     return fa_bwd_config((int)mode, (int)nw_dq, (int)nw_dkv);
 }
@@ -842,7 +841,6 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("fa_bwd_needs_dq_acc(int D) -> bool", &fa_bwd_needs_dq_acc);  // no tensors: a catch-all kernel
     m.def("fa_bwd_config(int mode=-1, int nw_dq=0, int nw_dkv=0) -> int", &fa_bwd_config_op);
     m.def("fa_fwd_config(int ver=0) -> int", &fa_fwd_config_op);
-    m.def("gpp_stagger_config(int fwd=-1, int bwd=-1) -> int", &gpp_stagger_config_op);
 }
 
 TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {

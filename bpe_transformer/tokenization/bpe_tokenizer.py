@@ -128,12 +128,14 @@ class BPETokenizer(Tokenizer):
         n = n_workers or cpu_count()
         return self._native.encode_batch([t.encode(ENCODING_STD) for t in texts], int(n))
 
-    def _encode_batch_stream(self, texts: list[str], n_workers: int) -> Iterator[int]:
+    def _encode_batch_slices(self, texts: list[str], n_workers: int) -> Iterator[list[int]]:
         # ids come back as one int32 array (4 bytes per token, not a Python int each) and are handed out as
-        # ints in 64 Ki-token slices: encode_iterable's memory stays O(batch), not O(batch tokens x 40 bytes)
+        # lists of 64 Ki tokens: encode_iterable's memory stays O(batch), not O(batch tokens x 40 bytes).  The
+        # caller yields each list's items itself: a second generator level per token (yield from a generator
+        # that yields from a list) cost more than the native encode (~0.2 us x 4 M tokens on 20 MB).
         ids, _ = self._native.encode_batch_flat([t.encode(ENCODING_STD) for t in texts], int(n_workers))
         for s in range(0, len(ids), 1 << 16):
-            yield from ids[s : s + (1 << 16)].tolist()
+            yield ids[s : s + (1 << 16)].tolist()
 
     def encode_file(self, path: Path | str, n_workers: int | None = None) -> np.ndarray:
         """Encode a whole utf-8 file with threads; returns int32 token ids."""
@@ -200,9 +202,11 @@ class BPETokenizer(Tokenizer):
             batch.append(piece)
             batch_chars += len(piece)
             if batch_chars >= (1 << 22):
-                yield from self._encode_batch_stream(batch, n_workers)
+                for ids in self._encode_batch_slices(batch, n_workers):
+                    yield from ids
                 batch, batch_chars = [], 0
         if batch:
-            yield from self._encode_batch_stream(batch, n_workers)
+            for ids in self._encode_batch_slices(batch, n_workers):
+                yield from ids
         if buf:
             yield from self.encode(buf)
