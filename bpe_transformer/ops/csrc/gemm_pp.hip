@@ -180,6 +180,19 @@ __device__ __forceinline__ void load_b(Frags& f, char* img, int wl, int n, int l
         for (int ks = 0; ks < 2; ++ks) f.b[jb][ks] = frag<BKM, SUB>(img, 4 * wl + 2 * n + jb, ks, l);
 }
 
+// An empty asm "use" of the accumulators a section just issued MFMAs into (no instruction is emitted).
+// Without it hipcc sinks every v_mfma_scale_f32_16x16x128_f8f6f4 of a K-tile past the phase barriers into the
+// loop latch (the MFMA results are only read after the loop, the barriers are in other basic blocks, and
+// sched_barrier only fences the scheduler inside a block): all 32 fp8 MFMAs of a K-tile then issued in one
+// barrier interval and the ping-pong was gone (24 + 8 MFMAs in two sections, three sections empty).  Pinned,
+// each section issues its own 8.  The bf16 MFMAs are not sunk (tools/isa_mfma_sections.py checks both).
+__device__ __forceinline__ void pin_quadrant(f32x4 (&acc)[8][4], int m, int n, int ib0, int ib1) {
+#pragma unroll
+    for (int ib = ib0; ib < ib1; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) asm volatile("" ::"v"(acc[4 * m + ib][2 * n + jb]));
+}
+
 template <int F8 = 0>
 __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const Frags& f, int m, int n) {
 #pragma unroll
@@ -194,6 +207,7 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const Frags& f,
                     acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
             }
         }
+    if constexpr (F8 != 0) pin_quadrant(acc, m, n, 0, 4);
 }
 
 // Half of a quadrant (i-blocks 2h, 2h+1): the MFMA section can then issue one DMA piece between its halves.
@@ -211,6 +225,7 @@ __device__ __forceinline__ void mma_half(f32x4 (&acc)[8][4], const Frags& f, int
                     acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
             }
         }
+    if constexpr (F8 != 0) pin_quadrant(acc, m, n, 2 * h, 2 * h + 2);
 }
 
 // One K-tile: four (load section, barrier, MFMA section, barrier) phases.  `cur` is read, `nxt` is the DMA
