@@ -2,15 +2,14 @@
 
 Recipe (BASELINE.json "Llama-style 1.1B fp8 MFMA path"):
   * the four projection GEMMs of every block run as fp8 x fp8 -> bf16 on the
-    MFMA fp8 units: hipBLASLt's ``torch._scaled_mm`` by default, or with
-    ``BPE_FP8_GEMM=hip`` the hand-written ping-pong kernel with
+    MFMA fp8 units: the hand-written ping-pong kernel with
     ``v_mfma_scale_f32_16x16x128_f8f6f4`` (``csrc/gemm_pp.hip``, F8 variants;
-    per-tensor inverse scales applied in its epilogue, read from the device).
-    Measured at the Llama-1.1B shapes (``benchmarks/gemm_fp8_bench.py``,
-    ``profiles/bench/gemm_fp8_hip_vs_lib.log``): ours 1.6-2.1 PF/s, the library
-    1.7-3.4 PF/s, bf16 1.1-1.6 PF/s -- our kernel keeps the bf16 kernel's
-    LDS-DMA schedule (an fp8 K-tile of 128 is a bf16 K-tile of 64 byte for
-    byte), whose DMA issue bounds it, so the library stays the default;
+    per-tensor inverse scales applied in its epilogue, read from the device)
+    for the shapes in ``ops/tuning/fp8_routes.json``, where it measured faster
+    than hipBLASLt, and hipBLASLt's ``torch._scaled_mm`` for the rest
+    (``BPE_FP8_GEMM=hip`` / ``lib`` force one path).  At the Llama-1.1B shapes
+    (``benchmarks/gemm_fp8_bench.py``, ``profiles/bench/gemm_fp8_pinned_vs_lib.log``)
+    ours runs 1.5-2.8 PF/s, the library 1.7-3.4 PF/s, bf16 1.1-1.6 PF/s;
   * activations and weights are quantised by ``csrc/fp8.hip`` with a scale
     derived from an amax history (delayed scaling, powers of two); the cast
     pass also records this step's amax, and one launch per step refreshes all
@@ -24,6 +23,7 @@ Recipe (BASELINE.json "Llama-style 1.1B fp8 MFMA path"):
 
 from __future__ import annotations
 
+import json
 import os
 
 import torch
@@ -34,18 +34,49 @@ from ._ext import ops
 FP8 = torch.float8_e4m3fn
 BF8 = torch.float8_e5m2
 _FMT = {"e4m3": (FP8, 0), "e5m2": (BF8, 1)}
-_LIB = os.environ.get("BPE_FP8_GEMM", "lib") != "hip"
+# BPE_FP8_GEMM: "routes" (default) = the HIP kernel for the shapes listed in ops/tuning/fp8_routes.json (where it
+# measured faster than hipBLASLt), hipBLASLt elsewhere; "hip" = the HIP kernel wherever it applies; "lib" =
+# hipBLASLt everywhere
+_MODE = os.environ.get("BPE_FP8_GEMM", "routes")
+if _MODE not in ("routes", "hip", "lib"):
+    raise ValueError(f"BPE_FP8_GEMM must be routes, hip or lib, got {_MODE!r}")
+
+
+def _load_routes() -> set[tuple[int, int, int, str]]:
+    path = os.path.join(os.path.dirname(__file__), "tuning", "fp8_routes.json")
+    try:
+        with open(path) as f:
+            table = json.load(f)
+    except FileNotFoundError:
+        return set()
+    out = set()
+    for key, route in table.get("routes", {}).items():
+        m, n, k, fmt = key.split(",")
+        if route == "hip":
+            out.add((int(m), int(n), int(k), fmt))
+    return out
+
+
+_HIP_ROUTES = _load_routes()
+
+
+def _use_hip(M: int, N: int, K: int, a_dtype) -> bool:
+    if _MODE == "lib":
+        return False
+    if _MODE == "hip":
+        return True
+    return (M, N, K, "e5m2" if a_dtype == torch.float8_e5m2 else "e4m3") in _HIP_ROUTES
 
 
 def mm_fp8(a8: Tensor, b8: Tensor, sa: Tensor, sb: Tensor) -> Tensor:
     """``(a8 @ b8.T) * sa * sb`` in bf16; a8 [M, K] e4m3 / e5m2, b8 [N, K] e4m3, sa / sb fp32 device scalars.
 
-    hipBLASLt, or with ``BPE_FP8_GEMM=hip`` the HIP fp8 MFMA kernel wherever the shape is 256 x 256 x 128-aligned
-    (every projection of the configs here)."""
+    The HIP fp8 MFMA kernel (``gemm_pp.hip``, F8) for the routed shapes (``BPE_FP8_GEMM``, above) when the shape is
+    256 x 256 x 128-aligned, else hipBLASLt."""
     M, K = a8.shape
     N = b8.shape[0]
-    if (not _LIB and M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and a8.stride(1) == 1 and b8.stride(1) == 1
-            and a8.stride(0) % 16 == 0 and b8.stride(0) % 16 == 0 and b8.dtype == FP8):
+    if (_use_hip(M, N, K, a8.dtype) and M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and a8.stride(1) == 1
+            and b8.stride(1) == 1 and a8.stride(0) % 16 == 0 and b8.stride(0) % 16 == 0 and b8.dtype == FP8):
         return ops().gemm_fp8(a8, b8, sa.reshape(1), sb.reshape(1))
     return torch._scaled_mm(a8, b8.t(), scale_a=sa, scale_b=sb, out_dtype=torch.bfloat16)
 

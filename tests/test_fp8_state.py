@@ -34,3 +34,21 @@ def test_model_enable_fp8_assigns_slots():
     st = m.enable_fp8(history=8)
     assert st.n == 24 and st.hist.shape == (24, 8)
     assert [layer.fp8[1] for layer in m.layers] == [0, 8, 16]
+
+
+def test_fp8_gemm_routing(monkeypatch):
+    """BPE_FP8_GEMM routing (ops/fp8.py): the shipped table sends exactly its listed (M, N, K, A-format) shapes to
+    the HIP fp8 kernel; "hip" / "lib" force one path."""
+    import torch
+
+    from bpe_transformer.ops import fp8
+
+    assert (16384, 2560, 2048, "e4m3") in fp8._HIP_ROUTES
+    monkeypatch.setattr(fp8, "_MODE", "routes")
+    assert fp8._use_hip(16384, 2560, 2048, torch.float8_e4m3fn)
+    assert not fp8._use_hip(16384, 2560, 2048, torch.float8_e5m2)  # same shape, other format: not measured
+    assert not fp8._use_hip(16384, 2048, 2048, torch.float8_e4m3fn)
+    monkeypatch.setattr(fp8, "_MODE", "hip")
+    assert fp8._use_hip(16384, 2048, 2048, torch.float8_e4m3fn)
+    monkeypatch.setattr(fp8, "_MODE", "lib")
+    assert not fp8._use_hip(16384, 2560, 2048, torch.float8_e4m3fn)
