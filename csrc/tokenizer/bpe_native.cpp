@@ -165,6 +165,12 @@ static size_t match_at(const uint8_t* s, size_t i, size_t n) {
         const uint8_t kind = cj;  // C_LETTER, C_NUMBER or C_OTHER
         size_t k = j + lj;
         while (k < n) {
+            const uint8_t b = s[k];
+            if (b < 0x80) {  // ASCII: one table lookup, no decode
+                if (g_cls.ascii[b] != kind) break;
+                ++k;
+                continue;
+            }
             int l;
             const uint32_t cp = decode(s, k, n, &l);
             if (classify(cp) != kind) break;
@@ -175,6 +181,13 @@ static size_t match_at(const uint8_t* s, size_t i, size_t n) {
     // 5/6: whitespace run; \s+(?!\S) backtracks one code point when followed by non-space
     size_t k = i, last = i;
     while (k < n) {
+        const uint8_t b = s[k];
+        if (b < 0x80) {
+            if (!(g_cls.ascii[b] & C_SPACE)) break;
+            last = k;
+            ++k;
+            continue;
+        }
         int l;
         const uint32_t cp = decode(s, k, n, &l);
         if (!(classify(cp) & C_SPACE)) break;
@@ -320,19 +333,84 @@ struct SvHash {
 };
 using CountMap = std::unordered_map<std::string, int64_t, SvHash, std::equal_to<>>;
 
-static void count_segment(std::string_view seg, CountMap& m) {
-    for_each_pretoken(seg, [&](std::string_view tok) {
-        auto it = m.find(tok);
-        if (it == m.end()) m.emplace(std::string(tok), 1);
-        else ++it->second;
-    });
+// Pre-token counter over views into the text being counted (which outlives it): open addressing, linear
+// probing, one multiply-mix hash and on a hit one memcmp per pre-token.  The node-based unordered_map it
+// replaces allocated a node per new key and chased a bucket pointer per lookup; this table keeps the
+// (hash, view, count) slots contiguous.  Keys are copied into std::strings only once, at the end (into()).
+class ViewCounter {
+    struct Slot {
+        uint64_t h;
+        const char* p;  // nullptr: empty
+        uint32_t n;
+        int64_t c;
+    };
+    std::vector<Slot> t_;
+    size_t used_ = 0;
+
+    static uint64_t hash(const char* p, size_t n) {
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xff51afd7ed558ccdull);
+        while (n >= 8) {
+            uint64_t v;
+            std::memcpy(&v, p, 8);
+            h = (h ^ v) * 0xff51afd7ed558ccdull;
+            h ^= h >> 32;
+            p += 8;
+            n -= 8;
+        }
+        if (n) {
+            uint64_t v = 0;
+            std::memcpy(&v, p, n);
+            h = (h ^ v) * 0xc4ceb9fe1a85ec53ull;
+        }
+        h ^= h >> 29;
+        h *= 0x9E3779B97F4A7C15ull;
+        return h ^ (h >> 32);
+    }
+    void grow() {
+        std::vector<Slot> old(t_.size() * 2, Slot{0, nullptr, 0, 0});
+        old.swap(t_);
+        const size_t mask = t_.size() - 1;
+        for (const Slot& x : old) {
+            if (!x.p) continue;
+            size_t i = x.h & mask;
+            while (t_[i].p) i = (i + 1) & mask;
+            t_[i] = x;
+        }
+    }
+
+  public:
+    ViewCounter() : t_(size_t(1) << 12, Slot{0, nullptr, 0, 0}) {}
+    void add(std::string_view s) {
+        const uint64_t h = hash(s.data(), s.size());
+        const size_t mask = t_.size() - 1;
+        for (size_t i = h & mask;; i = (i + 1) & mask) {
+            Slot& x = t_[i];
+            if (!x.p) {
+                x = Slot{h, s.data(), (uint32_t)s.size(), 1};
+                if (2 * ++used_ > t_.size()) grow();
+                return;
+            }
+            if (x.h == h && x.n == s.size() && std::memcmp(x.p, s.data(), s.size()) == 0) {
+                ++x.c;
+                return;
+            }
+        }
+    }
+    void into(CountMap& m) const {
+        for (const Slot& x : t_)
+            if (x.p) m[std::string(x.p, x.n)] += x.c;
+    }
+};
+
+static void count_segment(std::string_view seg, ViewCounter& m) {
+    for_each_pretoken(seg, [&](std::string_view tok) { m.add(tok); });
 }
 
 static CountMap count_text_parallel(const std::string& text, const SpecialSplitter& sp, int nthreads) {
     nthreads = std::max(1, nthreads);
     const auto bounds = chunk_bounds(text, sp, nthreads * 4);
     const int nchunks = (int)bounds.size() - 1;
-    std::vector<CountMap> maps(nthreads);
+    std::vector<ViewCounter> maps(nthreads);
     std::atomic<int> nextc{0};
     auto work = [&](int t) {
         for (;;) {
@@ -346,9 +424,8 @@ static CountMap count_text_parallel(const std::string& text, const SpecialSplitt
     for (int t = 1; t < nthreads; ++t) th.emplace_back(work, t);
     work(0);
     for (auto& x : th) x.join();
-    CountMap out = std::move(maps[0]);
-    for (int t = 1; t < nthreads; ++t)
-        for (auto& kv : maps[t]) out[kv.first] += kv.second;
+    CountMap out;
+    for (int t = 0; t < nthreads; ++t) maps[t].into(out);
     return out;
 }
 
