@@ -167,3 +167,29 @@ def test_parallel_pretoken_counts_match_regex_oracle(tmp_path, seed):
         assert Counter(got) == want, n
     assert Counter(native.count_pretokens_file(str(path), [], 8)) == Counter(
         m.group().encode("utf-8") for m in PAT.finditer(text))
+
+
+def test_pretoken_counts_many_unique_tokens(tmp_path):
+    """The native counter (open addressing over text views, grown from 4096 slots) on ~40 000 distinct
+    pre-tokens of 1-40 bytes -- letters, digits, punctuation runs, multi-byte letters -- equals the regex oracle,
+    for one thread and for per-thread tables merged at the end."""
+    from bpe_transformer.tokenization._native import native
+
+    rng = random.Random(7)
+    alpha = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZéüßжπ"
+    parts = []
+    for _ in range(60000):
+        k = rng.random()
+        if k < 0.7:
+            parts.append(" " * rng.randint(0, 1) + "".join(rng.choice(alpha) for _ in range(rng.randint(1, 20))))
+        elif k < 0.85:
+            parts.append(" " + str(rng.randint(0, 10 ** rng.randint(1, 12))))
+        else:
+            parts.append(" " + "".join(rng.choice("!?.,;:-_=+*") for _ in range(rng.randint(1, 6))) + "\n")
+    text = "".join(parts)
+    path = tmp_path / "u.txt"
+    path.write_bytes(text.encode("utf-8"))
+    want = Counter(m.group().encode("utf-8") for m in PAT.finditer(text))
+    assert len(want) > 30000
+    for n in (1, 4):
+        assert Counter(native.count_pretokens_file(str(path), [], n)) == want, n
