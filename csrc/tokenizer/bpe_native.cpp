@@ -337,6 +337,27 @@ using CountMap = std::unordered_map<std::string, int64_t, SvHash, std::equal_to<
 // probing, one multiply-mix hash and on a hit one memcmp per pre-token.  The node-based unordered_map it
 // replaces allocated a node per new key and chased a bucket pointer per lookup; this table keeps the
 // (hash, view, count) slots contiguous.  Keys are copied into std::strings only once, at the end (into()).
+// 64-bit multiply-mix hash of a short byte string (pre-tokens average ~5 bytes)
+static inline uint64_t pretok_hash(const char* p, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xff51afd7ed558ccdull);
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        h = (h ^ v) * 0xff51afd7ed558ccdull;
+        h ^= h >> 32;
+        p += 8;
+        n -= 8;
+    }
+    if (n) {
+        uint64_t v = 0;
+        std::memcpy(&v, p, n);
+        h = (h ^ v) * 0xc4ceb9fe1a85ec53ull;
+    }
+    h ^= h >> 29;
+    h *= 0x9E3779B97F4A7C15ull;
+    return h ^ (h >> 32);
+}
+
 class ViewCounter {
     struct Slot {
         uint64_t h;
@@ -347,25 +368,6 @@ class ViewCounter {
     std::vector<Slot> t_;
     size_t used_ = 0;
 
-    static uint64_t hash(const char* p, size_t n) {
-        uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xff51afd7ed558ccdull);
-        while (n >= 8) {
-            uint64_t v;
-            std::memcpy(&v, p, 8);
-            h = (h ^ v) * 0xff51afd7ed558ccdull;
-            h ^= h >> 32;
-            p += 8;
-            n -= 8;
-        }
-        if (n) {
-            uint64_t v = 0;
-            std::memcpy(&v, p, n);
-            h = (h ^ v) * 0xc4ceb9fe1a85ec53ull;
-        }
-        h ^= h >> 29;
-        h *= 0x9E3779B97F4A7C15ull;
-        return h ^ (h >> 32);
-    }
     void grow() {
         std::vector<Slot> old(t_.size() * 2, Slot{0, nullptr, 0, 0});
         old.swap(t_);
@@ -381,7 +383,7 @@ class ViewCounter {
   public:
     ViewCounter() : t_(size_t(1) << 12, Slot{0, nullptr, 0, 0}) {}
     void add(std::string_view s) {
-        const uint64_t h = hash(s.data(), s.size());
+        const uint64_t h = pretok_hash(s.data(), s.size());
         const size_t mask = t_.size() - 1;
         for (size_t i = h & mask;; i = (i + 1) & mask) {
             Slot& x = t_[i];
@@ -560,6 +562,64 @@ struct Trainer {
 };
 
 // ------------------------------------------------------------------ encoder
+// Pre-token -> token ids cache: open addressing over (hash, key, ids) slots, keys and ids appended to two
+// arenas (no node or vector allocation per entry; a hit is one probe sequence, one memcmp and a copy of a
+// contiguous id run).
+class PretokCache {
+    struct Slot {
+        uint64_t h;
+        uint32_t koff, klen, ioff, ilen;  // ilen == 0: empty (every pre-token has at least one id)
+    };
+    std::vector<Slot> t_;
+    std::string keys_;
+    std::vector<int32_t> ids_;
+    size_t used_ = 0;
+
+    void grow() {
+        std::vector<Slot> old(t_.size() * 2, Slot{0, 0, 0, 0, 0});
+        old.swap(t_);
+        const size_t mask = t_.size() - 1;
+        for (const Slot& x : old) {
+            if (!x.ilen) continue;
+            size_t i = x.h & mask;
+            while (t_[i].ilen) i = (i + 1) & mask;
+            t_[i] = x;
+        }
+    }
+
+  public:
+    PretokCache() : t_(size_t(1) << 12, Slot{0, 0, 0, 0, 0}) {}
+    size_t size() const { return used_; }
+    void clear() {
+        t_.assign(size_t(1) << 12, Slot{0, 0, 0, 0, 0});
+        keys_.clear();
+        ids_.clear();
+        used_ = 0;
+    }
+    // ids of `s` appended to out; false if absent
+    bool get(std::string_view s, uint64_t h, std::vector<int32_t>& out) const {
+        const size_t mask = t_.size() - 1;
+        for (size_t i = h & mask;; i = (i + 1) & mask) {
+            const Slot& x = t_[i];
+            if (!x.ilen) return false;
+            if (x.h == h && x.klen == s.size() && std::memcmp(keys_.data() + x.koff, s.data(), s.size()) == 0) {
+                out.insert(out.end(), ids_.begin() + x.ioff, ids_.begin() + x.ioff + x.ilen);
+                return true;
+            }
+        }
+    }
+    void put(std::string_view s, uint64_t h, const int32_t* ids, size_t n) {
+        if (n == 0 || keys_.size() + s.size() > UINT32_MAX || ids_.size() + n > UINT32_MAX) return;
+        const size_t mask = t_.size() - 1;
+        size_t i = h & mask;
+        while (t_[i].ilen) i = (i + 1) & mask;
+        t_[i] = Slot{h, (uint32_t)keys_.size(), (uint32_t)s.size(), (uint32_t)ids_.size(), (uint32_t)n};
+        keys_.append(s.data(), s.size());
+        ids_.insert(ids_.end(), ids, ids + n);
+        if (2 * ++used_ > t_.size()) grow();
+    }
+};
+
 struct Encoder {
     std::unordered_map<int32_t, std::string> id2bytes;
     std::unordered_map<std::string, int32_t, SvHash, std::equal_to<>> bytes2id;
@@ -567,7 +627,7 @@ struct Encoder {
     std::unordered_map<uint64_t, std::pair<int32_t, int32_t>> ranks;  // (a,b) -> (rank, merged id)
     SpecialSplitter specials;
     std::vector<int32_t> special_ids;
-    using Cache = std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>>;
+    using Cache = PretokCache;
     Cache cache;  // the calling thread's pre-token cache (worker 0 of every threaded call)
     // persistent caches of workers 1.. of the threaded calls: a 4 MiB encode_iterable batch then starts warm
     // instead of with an empty map per thread per call (the pre-token vocabulary of a corpus is small)
@@ -664,20 +724,19 @@ struct Encoder {
         for (int32_t p = 0; p >= 0; p = nxt[p]) out.push_back(sym[p]);
     }
 
-    void encode_pretoken(std::string_view tok, std::vector<int32_t>& out,
-                         std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>>& c) const {
-        auto it = c.find(tok);
-        if (it != c.end()) {
-            out.insert(out.end(), it->second.begin(), it->second.end());
+    void encode_pretoken(std::string_view tok, std::vector<int32_t>& out, Cache& c) const {
+        if (tok.size() == 1) {  // single byte: one table read, no cache
+            out.push_back(byte_id[(uint8_t)tok[0]]);
             return;
         }
+        const uint64_t h = pretok_hash(tok.data(), tok.size());
+        if (c.get(tok, h, out)) return;
         const size_t start = out.size();
         bpe(tok, out);
-        if (c.size() < cache_limit) c.emplace(std::string(tok), std::vector<int32_t>(out.begin() + start, out.end()));
+        if (c.size() < cache_limit) c.put(tok, h, out.data() + start, out.size() - start);
     }
 
-    void encode_into(std::string_view text, std::vector<int32_t>& out,
-                     std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>>& c) const {
+    void encode_into(std::string_view text, std::vector<int32_t>& out, Cache& c) const {
         specials.split(
             text,
             [&](std::string_view seg) { for_each_pretoken(seg, [&](std::string_view t) { encode_pretoken(t, out, c); }); },

@@ -40,7 +40,7 @@ int main(int argc, char** argv) {
     std::vector<int32_t> par = enc.encode_parallel(clean, nthreads);
     std::vector<int32_t> ser;
     {
-        std::unordered_map<std::string, std::vector<int32_t>, SvHash, std::equal_to<>> c;
+        Encoder::Cache c;
         enc.encode_into(clean, ser, c);
     }
     if (par != ser) {
