@@ -33,7 +33,10 @@ METRIC = "training tokens/sec (whole node), GPT-2-small config at 1/2/4/8 MI355X
 TUNING_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bpe_transformer", "ops", "tuning")
 
 
-DEFAULT_BATCH = {"gpt2-small": 128, "llama-1.1b": 8}
+# per-GPU micro-batch when --batch is not given: GPT-2-small 128 sequences; Llama-1.1B 65 536 tokens (32 x 2048,
+# 16 x 4096: +5-6 % over 16 384 tokens, ~110 GB of the 288 GB HBM; profiles/bench/ab_llama_microbatch_65k_tokens.log)
+DEFAULT_BATCH = {"gpt2-small": 128}
+DEFAULT_TOKENS = {"llama-1.1b": 65536}
 
 
 def load_gemm_tuning(spec: str, model: str, batch: int, seq: int) -> str | None:
@@ -66,7 +69,7 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU micro-batch (sequences); default per model: gpt2-small 128 (128 x 1024 tokens "
                          "uses a fraction of the 288 GB HBM and runs ~2 percent faster than 64; library GEMM tables "
-                         "for both in ops/tuning), llama-1.1b 8, otherwise 8")
+                         "for both in ops/tuning), llama-1.1b 65536 tokens (32 x 2048, 16 x 4096), otherwise 8")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
@@ -93,7 +96,10 @@ def main() -> int:
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = DEFAULT_BATCH.get(args.model, 8)
+        if args.model in DEFAULT_TOKENS:
+            args.batch = max(1, DEFAULT_TOKENS[args.model] // args.seq)
+        else:
+            args.batch = DEFAULT_BATCH.get(args.model, 8)
 
     from bpe_transformer.data import synthetic_tokens
     from bpe_transformer.models import TransformerLM, get_preset

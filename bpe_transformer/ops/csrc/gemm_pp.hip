@@ -504,8 +504,13 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
         }
     }
     if (g == 0 && DIAG != 4) bar();
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    bar();  // every fragment read done: the LDS is free for the epilogue
+    // every fragment read and LDS-DMA done: the LDS is free for the epilogue.  The builtin (not inline asm)
+    // tells the compiler's wait-count model that the DMA has retired; after an asm wait it still counts the
+    // LDS-DMA loads as pending, a second kind of VMEM event beside the epilogue's own loads, and then waits
+    // vmcnt(0) before the first use of any of them (the SwiGLU-backward epilogue's 32 g / u loads drained
+    // completely before the first row's math; now row q waits for its own pair)
+    __builtin_amdgcn_s_waitcnt(0x70);  // vmcnt(0) expcnt(7) lgkmcnt(0)
+    bar();
 
     // DIAG 6 (timing only): the epilogue's global stores are skipped (kept in the code behind a runtime test
     // that is never true, so the MFMAs and the LDS staging stay): prices the store burst at the end of each tile
@@ -547,7 +552,11 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
                 gv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro));  // read once
                 uv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F));
             }
-            __syncthreads();
+            // raw barrier after the staging writes only: __syncthreads() would also wait for all 32 loads
+            // (vmcnt(0)) before the first row's math; this way row q waits for its own pair (in-order vmcnt)
+            // and its math and stores overlap the later rows' loads
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
+            bar();
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int i = q * 16 + (tid >> 5);
