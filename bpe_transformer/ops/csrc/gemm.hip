@@ -421,7 +421,9 @@ __device__ __forceinline__ void for_each_acc(const Acc<16>& acc, int l, F&& f) {
             for (int r = 0; r < 4; ++r) f(a * 16 + 4 * (l >> 4) + r, b * 16 + (l & 15), acc.v[a][b][r]);
 }
 
-template <int MF, bool PRIO, int DSPLIT = 0>
+// NS = LDS stages (4 = 128 KiB, NS - 2 = 2 in flight while one is consumed; 5 = 160 KiB, the whole LDS, 3 in
+// flight: BPE_G256_STAGES=5)
+template <int MF, bool PRIO, int DSPLIT = 0, int NS = NSTAGE>
 __global__ void __launch_bounds__(NT, 1)
 gemm256_tn_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
                   float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int Mo, int No, int R,
@@ -457,23 +459,30 @@ gemm256_tn_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restri
     long oa[2], ob[2];
     dma_offsets(lda, i0, w, l, oa);
     dma_offsets(ldb, j0, w, l, ob);
-    // prologue: stages 0, 1, 2 in flight; retire stage 0
+    // prologue: stages 0 .. NS-2 in flight (4 DMA instructions per wave each); retire stage 0
 #pragma unroll
-    for (int st = 0; st < NSTAGE - 1; ++st) {
+    for (int st = 0; st < NS - 1; ++st) {
         char* d = smem + st * STAGE_BYTES;
         dma_tile(A + (long)(rbeg + st * BK) * lda, oa, d, w);
         dma_tile(B + (long)(rbeg + st * BK) * ldb, ob, d + TILE_BYTES, w);
     }
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if constexpr (NS == 5)
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     for (int kt = 0; kt < nk; ++kt) {
-        char* cur = smem + (kt & (NSTAGE - 1)) * STAGE_BYTES;
-        char* nxt = smem + ((kt + NSTAGE - 1) & (NSTAGE - 1)) * STAGE_BYTES;
+        char* cur = smem + (kt % NS) * STAGE_BYTES;
+        char* nxt = smem + ((kt + NS - 1) % NS) * STAGE_BYTES;
         // every step issues exactly one stage so the counted wait below stays exact; past the end it re-loads
         // the last stage into a buffer nobody reads again
-        const int rn = min(rbeg + (kt + NSTAGE - 1) * BK, rlast);
+        const int rn = min(rbeg + (kt + NS - 1) * BK, rlast);
         kstep<MF, PRIO, DSPLIT>(cur, nxt, A + (long)rn * lda, oa, B + (long)rn * ldb, ob, wr, wc, w, l, acc);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage kt+1 landed; kt+2, kt+3 stay in flight
+        // stage kt+1 landed; the NS - 2 newer stages stay in flight
+        if constexpr (NS == 5)
+            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
     }
@@ -507,17 +516,27 @@ bool gemm_shape_ok(int Mo, int No, int R, int splits, int tile) {
     return Mo % BM == 0 && No % BN == 0 && splits >= 1 && R % BK == 0 && R / BK >= splits;
 }
 
-template <int MF, bool PRIO, int DSPLIT = 0>
+template <int MF, bool PRIO, int DSPLIT = 0, int NS = g256::NSTAGE>
 static void launch_g256_v(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                           float beta, int Mo, int No, int R, int splits, hipStream_t s, int prio) {
     static bool attr = false;  // > 64 KiB dynamic LDS must be opted into once per instantiation
-    auto* k = &g256::gemm256_tn_kernel<MF, PRIO, DSPLIT>;
+    auto* k = &g256::gemm256_tn_kernel<MF, PRIO, DSPLIT, NS>;
+    constexpr int lds = NS * g256::STAGE_BYTES;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, g256::LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
     }
     const int grid = (Mo / 256) * (No / 256) * splits;
-    k<<<grid, g256::NT, g256::LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, prio);
+    k<<<grid, g256::NT, lds, s>>>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, prio);
+}
+
+// BPE_G256_STAGES (read once): 5 = the five-stage form of the default variant (160 KiB LDS, 3 stages in flight)
+static int g256_stages() {
+    static const int n = [] {
+        const char* e = getenv("BPE_G256_STAGES");
+        return (e && atoi(e) == 5) ? 5 : 4;
+    }();
+    return n;
 }
 
 // variant (BPE_G256_VARIANT, read once): bit 0 = 16x16x32 MFMA, bit 1 = setprio'd MFMA cluster, bit 2 / bit 3 =
@@ -531,7 +550,11 @@ static void launch_g256(const __bf16* a, long lda, const __bf16* b, long ldb, fl
     }();
     const int pr = (variant >> 4) & 1;
     if (variant & 8) return launch_g256_v<32, false, 2>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr);
-    if (variant & 4) return launch_g256_v<32, false, 1>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr);
+    if (variant & 4) {
+        if (g256_stages() == 5 && R / g256::BK / splits >= 4)
+            return launch_g256_v<32, false, 1, 5>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr);
+        return launch_g256_v<32, false, 1>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr);
+    }
     switch (variant & 3) {
         case 0: launch_g256_v<32, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;
         case 1: launch_g256_v<16, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;

@@ -121,18 +121,39 @@ static inline int valid_seq(const uint8_t* s, size_t i, size_t n) {
     return 0;
 }
 
-// Python `bytes.decode("utf-8", errors="ignore").encode("utf-8")` (reference pretokenization.py:194).
-static std::string sanitize_utf8(const char* data, size_t n) {
-    const uint8_t* s = reinterpret_cast<const uint8_t*>(data);
-    std::string out;
-    out.reserve(n);
-    size_t i = 0;
+// Python `bytes.decode("utf-8", errors="ignore").encode("utf-8")` (reference pretokenization.py:194), in
+// place: invalid bytes are dropped by compacting the buffer.  ASCII is skipped 8 bytes per step and a valid
+// buffer (the usual case) is never copied; the byte-at-a-time copy this replaces cost ~50 ms per 20 MB.
+static void sanitize_utf8_inplace(std::string& buf) {
+    uint8_t* s = reinterpret_cast<uint8_t*>(buf.data());
+    const size_t n = buf.size();
+    size_t i = 0, o = 0;  // read / write positions (o == i until the first invalid byte)
     while (i < n) {
+        if (i + 8 <= n) {
+            uint64_t v;
+            std::memcpy(&v, s + i, 8);
+            if ((v & 0x8080808080808080ull) == 0) {
+                if (o != i) std::memmove(s + o, s + i, 8);
+                i += 8;
+                o += 8;
+                continue;
+            }
+        }
         const int l = valid_seq(s, i, n);
-        if (l == 0) { ++i; continue; }
-        out.append(data + i, l);
+        if (l == 0) {
+            ++i;
+            continue;
+        }
+        if (o != i) std::memmove(s + o, s + i, (size_t)l);
         i += l;
+        o += l;
     }
+    buf.resize(o);
+}
+
+static std::string sanitize_utf8(const char* data, size_t n) {
+    std::string out(data, n);
+    sanitize_utf8_inplace(out);
     return out;
 }
 
@@ -858,9 +879,8 @@ PYBIND11_MODULE(_bpe_native, m) {
         {
             py::gil_scoped_release nogil;
             std::string raw = read_file(path);
-            std::string s = sanitize_utf8(raw.data(), raw.size());
-            raw.clear();
-            raw.shrink_to_fit();
+            sanitize_utf8_inplace(raw);
+            std::string s = std::move(raw);
             SpecialSplitter sp(std::move(specials));
             cm = count_text_parallel(s, sp, nthreads);
         }
@@ -883,9 +903,8 @@ PYBIND11_MODULE(_bpe_native, m) {
         {
             py::gil_scoped_release nogil;
             std::string raw = read_file(path);
-            std::string s = sanitize_utf8(raw.data(), raw.size());
-            raw.clear();
-            raw.shrink_to_fit();
+            sanitize_utf8_inplace(raw);
+            std::string s = std::move(raw);
             SpecialSplitter sp(specials);
             CountMap cm = count_text_parallel(s, sp, nthreads);
             t.train(cm, vocab_size, specials);
@@ -967,8 +986,8 @@ PYBIND11_MODULE(_bpe_native, m) {
             std::vector<int32_t> out;
             {
                 py::gil_scoped_release nogil;
-                std::string raw = read_file(path);
-                std::string s = sanitize_utf8(raw.data(), raw.size());
+                std::string s = read_file(path);
+                sanitize_utf8_inplace(s);
                 std::lock_guard<std::mutex> lk(e.mu);
                 out = e.encode_parallel(s, nthreads);
             }

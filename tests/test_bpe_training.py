@@ -193,3 +193,17 @@ def test_pretoken_counts_many_unique_tokens(tmp_path):
     assert len(want) > 30000
     for n in (1, 4):
         assert Counter(native.count_pretokens_file(str(path), [], n)) == want, n
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_native_utf8_sanitizer_matches_python(seed):
+    """sanitize_utf8 (in place, 8-byte ASCII skip) == Python's decode(errors="ignore").encode() on byte soup:
+    ASCII runs straddling 8-byte words, valid 2-4 byte sequences, overlongs, surrogates, truncations, stray
+    continuation bytes."""
+    from bpe_transformer.tokenization._native import native
+
+    rng = random.Random(seed)
+    atoms = [b"plain ascii text ", b"abcdefg", b"\xc3\xa9", b"\xe2\x82\xac", b"\xf0\x9f\x98\x80", b"\x80", b"\xbf",
+             b"\xc0\xaf", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xe2\x82", b"\xf0\x9f", b"\xff", b"\n", b"x"]
+    data = b"".join(rng.choice(atoms) for _ in range(rng.randint(500, 3000)))
+    assert native.sanitize_utf8(data) == data.decode("utf-8", errors="ignore").encode("utf-8")
