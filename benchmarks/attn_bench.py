@@ -28,6 +28,9 @@ def main():
                     help="interleaved same-process A/B of the D = 64 forward versions 2 (fa_fwd_kernel) and 4 "
                          "(flash_attn_fwd_v4.hip) (ops.fa_fwd_config)")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--fwd-versions", type=int, nargs="+", default=[2, 4, 5, 6])
+    ap.add_argument("--bwd-arms", nargs="+", default=None,
+                    help="subset of the --bwd-ab arms (names below, or dq,dkv codes like 42,42)")
     ap.add_argument("--mode", choices=["block", "fused"], default="block",
                     help="block = the training path (rope_qk_ in place, then pre-rotated kernels; rope time reported "
                          "separately and included in fwd_ms); fused = RoPE inside the attention kernels")
@@ -63,7 +66,7 @@ def main():
     fl = 4.0 * B * H * S * S * D / 2
     if a.fwd_ab:
         prev = hip.fa_fwd_config(0)
-        times = {2: [], 4: [], 5: []}
+        times = {v: [] for v in a.fwd_versions}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for _ in range(a.rounds):
             for ver in times:
@@ -85,6 +88,8 @@ def main():
     if a.bwd_ab:
         arms = {"fused": (1, 0, 0), "split4x4": (0, 4, 4), "split4x8": (0, 4, 8), "split8x4": (0, 8, 4),
                 "split4_ppdkv": (0, 4, 2), "split_pp_both": (0, 2, 2)}
+        if a.bwd_arms:  # names, or "dq,dkv" wave codes (42 / 43: LDS-DMA staging at 2 / 3 waves per SIMD)
+            arms = {n: (arms[n] if n in arms else (0, *map(int, n.split(",")))) for n in a.bwd_arms}
         prev = hip.fa_bwd_config(-1, 0, 0)
         times = {k: [] for k in arms}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -98,7 +103,7 @@ def main():
                 ev[1].record()
                 torch.cuda.synchronize()
                 times[name].append(ev[0].elapsed_time(ev[1]) / a.iters)
-        hip.fa_bwd_config(prev, 4, 4)
+        hip.fa_bwd_config(prev, 42, 42)
         for name, t in times.items():
             t = sorted(t)
             print(json.dumps({"shape": [B, S, H, Hkv, D], "arm": name, "bwd_ms_median": round(t[len(t) // 2], 4),

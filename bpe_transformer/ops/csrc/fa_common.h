@@ -104,6 +104,28 @@ __device__ __forceinline__ u16x8 rope_u16x8(u16x8 v, const float* cs, const floa
     return pack8(x, mul);
 }
 
+// LDS-DMA staging of a 64-row x 128-byte tile (D = 64) into the swizzled image of swz<128>: the DMA writes lane-
+// linearly (wave-instruction i of wave w fills physical chunks 64 (cpw w + i) + lane), so each lane loads the
+// SOURCE chunk the swizzle puts at its physical slot (c = pc ^ sigma(r)).  Rows past the end are loaded clamped
+// (row S - 1): the kernels mask their scores, so those rows only ever meet a zero P / dS.  No registers hold the
+// tile and no VALU touches it; completion is the issuing wave's vmcnt (the kernels' closing __syncthreads).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+template <int NW>
+__device__ __forceinline__ void dma_tile64(const __bf16* base, long ld, int r0, int S, char* img, int w, int l) {
+    constexpr int CPW = 512 / (NW * 64);  // wave-instructions per wave (512 chunks of 16 bytes per tile)
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+        const int slot = 64 * (CPW * w + i);  // wave-uniform first chunk of this instruction
+        const int e = slot + l, r = e >> 3, pc = e & 7;
+        const int sg = (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+        const long row = min(r0 + r, S - 1);
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + row * ld + ((pc ^ sg) << 3)),
+                                         (lds_void_t*)(img + slot * 16), 16, 0, 0);
+    }
+}
+
 // Launch order of the (block, batch*head) work items: heads are taken in groups of `group` (batch, head) pairs
 // and, inside a group, the `nblk` blocks of every pair run heaviest first (index 0 = heaviest).  All blocks of a
 // pair thus run close together in time, so the K / V (forward) or Q / dO (backward) rows they share are re-read

@@ -40,8 +40,8 @@ constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4;
 // staged 16-byte chunks per thread and tensor for one 64-row tile (512 chunks)
 template <int NW> constexpr int cpt() { return 512 / (NW * 64); }
 
-template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW>
-__global__ void __launch_bounds__(NW * 64, 2)
+template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false>
+__global__ void __launch_bounds__(NW * 64, OCC)
 fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                  long ld_q, long ld_kv, const __bf16* __restrict__ O, long ld_o, const __bf16* __restrict__ dO,
                  long ld_do, const float* __restrict__ LSE, float* __restrict__ DELTA, __bf16* __restrict__ dQ,
@@ -134,58 +134,76 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         }
     };
 
-    load_tile(0);
-    write_tile(0, 0);
+    // DM: K / V tiles by LDS-DMA (no staging registers; rows past the end arrive clamped and are masked below)
+    constexpr bool DM = DMA && !ROPE_IN;
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    if constexpr (DM) {
+        dma_tile64<NW>(kb, ld_kv, 0, S, Ks, wu, l);
+        dma_tile64<NW>(vb, ld_kv, 0, S, Vs, wu, l);
+    } else {
+        load_tile(0);
+        write_tile(0, 0);
+    }
     __syncthreads();
 
     const int trow = 4 * hh + ((l & 15) >> 2);          // tr-read row inside a 16-key step
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);  // tr-read column inside a 32-wide d tile
     for (int it = 0; it < nkt; ++it) {
         const int cur = it & 1, k0 = it * 64;
-        if (it + 1 < nkt) load_tile(it + 1);
-        char* Kc = Ks + cur * TILE;
-        const char* Vc = Vs + cur * TILE;
-        if (!CAUSAL || k0 <= qw + 31) {
-            const bool need_mask = (CAUSAL && k0 + 63 > qw) || (k0 + 64 > S);
-#pragma unroll
-            for (int kh = 0; kh < 2; ++kh) {
-                if (CAUSAL && k0 + 32 * kh > qw + 31) break;  // this 32-key half is past every query of the wave
-                f32x16 sp = ns, dp = nd;
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
-                    sp = mfma(lds_row16(Kc, koff), qf[ks], sp);
-                    dp = mfma(lds_row16(Vc, koff), of[ks], dp);
-                }
-                // P^T = exp2(S^T c - lse), dS^T = P^T (dP^T - delta); key = row of the accumulator, query = lane
-                if (need_mask) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int key = k0 + 32 * kh + acc_row(r, hh);
-                        const float p = fast_exp2(sp[r]);
-                        const bool ok = key < S && (!CAUSAL || key <= q);
-                        dp[r] = ok ? p * dp[r] : 0.f;
-                    }
+        // the current and next buffers as __restrict__ parameters (see fa_bwd_dkv_kernel): no DMA drain mid-tile
+        auto body = [&](char* __restrict__ Kc, const char* __restrict__ Vc, char* __restrict__ Kn,
+                        char* __restrict__ Vn) {
+            if (it + 1 < nkt) {
+                if constexpr (DM) {  // buffer cur ^ 1 was last read in iteration it - 1, before its closing barrier
+                    dma_tile64<NW>(kb, ld_kv, k0 + 64, S, Kn, wu, l);
+                    dma_tile64<NW>(vb, ld_kv, k0 + 64, S, Vn, wu, l);
                 } else {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(sp[r]) * dp[r];
-                }
-                // dQ^T += K^T.dS^T: registers 8s..8s+7 are k-step s (keys 16 s ..) in the MFMA's permuted order
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    bf16x8 db;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) db[j] = (__bf16)dp[8 * s + j];
-                    const int kr = 32 * kh + 16 * s;
-#pragma unroll
-                    for (int dt = 0; dt < 2; ++dt)
-                        acc[dt] = mfma(lds_tr_pair(Kc, tr_off<RB>(kr + trow, 32 * dt + tcol),
-                                                   tr_off<RB>(kr + 8 + trow, 32 * dt + tcol)),
-                                       db, acc[dt]);
+                    load_tile(it + 1);
                 }
             }
-        }
-        if (it + 1 < nkt) write_tile(it + 1, cur ^ 1);
+            if (!CAUSAL || k0 <= qw + 31) {
+                const bool need_mask = (CAUSAL && k0 + 63 > qw) || (k0 + 64 > S);
+    #pragma unroll
+                for (int kh = 0; kh < 2; ++kh) {
+                    if (CAUSAL && k0 + 32 * kh > qw + 31) break;  // this 32-key half is past every query of the wave
+                    f32x16 sp = ns, dp = nd;
+    #pragma unroll
+                    for (int ks = 0; ks < KS; ++ks) {
+                        const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
+                        sp = mfma(lds_row16(Kc, koff), qf[ks], sp);
+                        dp = mfma(lds_row16(Vc, koff), of[ks], dp);
+                    }
+                    // P^T = exp2(S^T c - lse), dS^T = P^T (dP^T - delta); key = row of the accumulator, query = lane
+                    if (need_mask) {
+    #pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int key = k0 + 32 * kh + acc_row(r, hh);
+                            const float p = fast_exp2(sp[r]);
+                            const bool ok = key < S && (!CAUSAL || key <= q);
+                            dp[r] = ok ? p * dp[r] : 0.f;
+                        }
+                    } else {
+    #pragma unroll
+                        for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(sp[r]) * dp[r];
+                    }
+                    // dQ^T += K^T.dS^T: registers 8s..8s+7 are k-step s (keys 16 s ..) in the MFMA's permuted order
+    #pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        bf16x8 db;
+    #pragma unroll
+                        for (int j = 0; j < 8; ++j) db[j] = (__bf16)dp[8 * s + j];
+                        const int kr = 32 * kh + 16 * s;
+    #pragma unroll
+                        for (int dt = 0; dt < 2; ++dt)
+                            acc[dt] = mfma(lds_tr_pair(Kc, tr_off<RB>(kr + trow, 32 * dt + tcol),
+                                                       tr_off<RB>(kr + 8 + trow, 32 * dt + tcol)),
+                                           db, acc[dt]);
+                    }
+                }
+            }
+        };
+        body(Ks + cur * TILE, Vs + cur * TILE, Ks + (cur ^ 1) * TILE, Vs + (cur ^ 1) * TILE);
+        if (!DM && it + 1 < nkt) write_tile(it + 1, cur ^ 1);
         __syncthreads();
     }
 
@@ -214,8 +232,8 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     }
 }
 
-template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW>
-__global__ void __launch_bounds__(NW * 64, 2)
+template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false>
+__global__ void __launch_bounds__(NW * 64, OCC)
 fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                   long ld_q, long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
                   const float* __restrict__ DELTA, __bf16* __restrict__ dK, __bf16* __restrict__ dV, long ld_dkv,
@@ -279,23 +297,28 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     const long sbase = ((long)b * H + h) * S;
     u16x8 qreg[CPT], oreg[CPT];
     float lreg = 0.f, dreg = 0.f;
+    // DM: Q / dO tiles by LDS-DMA (no staging registers); only the row constants go through registers
+    constexpr bool DM = DMA && !ROPE_IN;
+    const int wu = __builtin_amdgcn_readfirstlane(w);
     auto load_tile = [&](int it) {
         const int m0 = m_start + it * 64;
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int e = tid + NT * i, r = e >> 3, c = e & 7;
-            const long qq = min(m0 + r, S - 1);
-            qreg[i] = *reinterpret_cast<const u16x8*>(qb + qq * ld_q + c * 8);
-            oreg[i] = *reinterpret_cast<const u16x8*>(ob + qq * ld_do + c * 8);
-        }
         const long idx = sbase + min(m0 + l, S - 1);  // every wave loads the stats (wave 0 writes them)
         lreg = LSE[idx];
         dreg = DELTA[idx];
+        if constexpr (!DM) {  // DM: the tile itself is DMA'd by the loop body (after these loads)
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int e = tid + NT * i, r = e >> 3, c = e & 7;
+                const long qq = min(m0 + r, S - 1);
+                qreg[i] = *reinterpret_cast<const u16x8*>(qb + qq * ld_q + c * 8);
+                oreg[i] = *reinterpret_cast<const u16x8*>(ob + qq * ld_do + c * 8);
+            }
+        }
     };
     auto write_tile = [&](int it, int buf) {
         const int m0 = m_start + it * 64;
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) {
+        for (int i = 0; i < (DM ? 0 : CPT); ++i) {
             const int e = tid + NT * i, r = e >> 3, c = e & 7;
             const bool ok = m0 + r < S;
             u16x8 qv = ok ? qreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -316,6 +339,10 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
 
     if (nqt > 0) {
         load_tile(0);
+        if constexpr (DM) {
+            dma_tile64<NW>(qb, ld_q, m_start, S, Qs, wu, l);
+            dma_tile64<NW>(ob, ld_do, m_start, S, dOs, wu, l);
+        }
         write_tile(0, 0);
     }
     __syncthreads();
@@ -326,67 +353,77 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     const unsigned span = (unsigned)(S - klim);  // valid query q: (unsigned)(q - klim) < span
     for (int it = 0; it < nqt; ++it) {
         const int cur = it & 1, m0 = m_start + it * 64;
-        if (it + 1 < nqt) load_tile(it + 1);
-        char* Qc = Qs + cur * TILE;
-        char* Oc = dOs + cur * TILE;
-        const float* lc = lseS + cur * 64;
-        const float* dc = dltS + cur * 64;
-        if (!CAUSAL || m0 + 63 >= kw0) {
-            const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + 64 > S) || (kw0 + 32 > S);
-#pragma unroll
-            for (int qt = 0; qt < 2; ++qt) {
-                if (CAUSAL && m0 + 32 * qt + 31 < kw0) continue;  // every query of this half precedes every key
-                f32x16 sp, dp;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int qi = qt * 32 + 8 * i + 4 * hh;  // rows qi..qi+3 of registers 4i..4i+3
-                    const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
-                    const f32x4 dl = *reinterpret_cast<const f32x4*>(dc + qi);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) { sp[4 * i + j] = lv[j]; dp[4 * i + j] = dl[j]; }
+        // One iteration with the current and the next buffers as __restrict__ parameters: the DMA into the next
+        // buffer and the fragment reads of the current one are then provably disjoint to the wait-count pass
+        // (without it hipcc drains the DMA, vmcnt(0), before the first transposed read of every half-tile).
+        auto body = [&](char* __restrict__ Qc, char* __restrict__ Oc, char* __restrict__ Qn, char* __restrict__ On) {
+            if (it + 1 < nqt) {
+                load_tile(it + 1);
+                if constexpr (DM) {  // buffer cur ^ 1 was last read in iteration it - 1, before its closing barrier
+                    dma_tile64<NW>(qb, ld_q, m0 + 64, S, Qn, wu, l);
+                    dma_tile64<NW>(ob, ld_do, m0 + 64, S, On, wu, l);
                 }
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
-                    sp = mfma(lds_row16(Qc, off), kf[ks], sp);
-                    dp = mfma(lds_row16(Oc, off), vf[ks], dp);
-                }
-                if (need_mask) {
-                    const int qoff = m0 + qt * 32 - klim;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const float p = fast_exp2(sp[r]);
-                        const bool ok = (unsigned)(qoff + acc_row(r, hh)) < span;
-                        sp[r] = ok ? p : 0.f;
-                        dp[r] = ok ? p * dp[r] : 0.f;
+            }
+            const float* lc = lseS + cur * 64;
+            const float* dc = dltS + cur * 64;
+            if (!CAUSAL || m0 + 63 >= kw0) {
+                const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + 64 > S) || (kw0 + 32 > S);
+    #pragma unroll
+                for (int qt = 0; qt < 2; ++qt) {
+                    if (CAUSAL && m0 + 32 * qt + 31 < kw0) continue;  // every query of this half precedes every key
+                    f32x16 sp, dp;
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int qi = qt * 32 + 8 * i + 4 * hh;  // rows qi..qi+3 of registers 4i..4i+3
+                        const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
+                        const f32x4 dl = *reinterpret_cast<const f32x4*>(dc + qi);
+    #pragma unroll
+                        for (int j = 0; j < 4; ++j) { sp[4 * i + j] = lv[j]; dp[4 * i + j] = dl[j]; }
                     }
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const float p = fast_exp2(sp[r]);
-                        sp[r] = p;
-                        dp[r] *= p;
+    #pragma unroll
+                    for (int ks = 0; ks < KS; ++ks) {
+                        const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
+                        sp = mfma(lds_row16(Qc, off), kf[ks], sp);
+                        dp = mfma(lds_row16(Oc, off), vf[ks], dp);
                     }
-                }
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    bf16x8 pb, db;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        pb[j] = (__bf16)sp[8 * ss + j];
-                        db[j] = (__bf16)dp[8 * ss + j];
+                    if (need_mask) {
+                        const int qoff = m0 + qt * 32 - klim;
+    #pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const float p = fast_exp2(sp[r]);
+                            const bool ok = (unsigned)(qoff + acc_row(r, hh)) < span;
+                            sp[r] = ok ? p : 0.f;
+                            dp[r] = ok ? p * dp[r] : 0.f;
+                        }
+                    } else {
+    #pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const float p = fast_exp2(sp[r]);
+                            sp[r] = p;
+                            dp[r] *= p;
+                        }
                     }
-                    const int qr = qt * 32 + 16 * ss;
-#pragma unroll
-                    for (int dt = 0; dt < 2; ++dt) {
-                        const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
-                        const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
-                        dv[dt] = mfma(lds_tr_pair(Oc, o0, o1), pb, dv[dt]);
-                        dk[dt] = mfma(lds_tr_pair(Qc, o0, o1), db, dk[dt]);
+    #pragma unroll
+                    for (int ss = 0; ss < 2; ++ss) {
+                        bf16x8 pb, db;
+    #pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            pb[j] = (__bf16)sp[8 * ss + j];
+                            db[j] = (__bf16)dp[8 * ss + j];
+                        }
+                        const int qr = qt * 32 + 16 * ss;
+    #pragma unroll
+                        for (int dt = 0; dt < 2; ++dt) {
+                            const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
+                            const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
+                            dv[dt] = mfma(lds_tr_pair(Oc, o0, o1), pb, dv[dt]);
+                            dk[dt] = mfma(lds_tr_pair(Qc, o0, o1), db, dk[dt]);
+                        }
                     }
                 }
             }
-        }
+        };
+        body(Qs + cur * TILE, dOs + cur * TILE, Qs + (cur ^ 1) * TILE, dOs + (cur ^ 1) * TILE);
         if (it + 1 < nqt) write_tile(it + 1, cur ^ 1);
         __syncthreads();
     }
@@ -908,10 +945,16 @@ using namespace bpe::fa;
 
 // Backward form: 0 = split (default for D = 64), 1 = fused (flash_attn_bwd.hip, the atomics form).  Initial value
 // from BPE_FA_BWD ("fused" / "split"), changeable at run time (fa_bwd_config) for same-process A/B and tests.
-// Waves per workgroup of the two split kernels: BPE_FA_SPLIT_NW="<dq>,<dkv>", each 4 or 8 (the plain kernels) or
-// 2 (the ping-pong kernels: 8 waves in two staggered groups).  Default 4,4: the measured best on MI355X
-// (profiles/bench/ab_attn_pp_b128.log: the ping-pong pair runs at 2 waves per SIMD and loses 13-27 %).
-static int g_mode = -1, g_nw_dq = 4, g_nw_dkv = 4;
+// Waves per workgroup of the two split kernels: BPE_FA_SPLIT_NW="<dq>,<dkv>", each 4 or 8 (the plain kernels with
+// register-staged tiles), 42 / 43 (4 waves, tiles staged by LDS-DMA, 2 / 3 waves per SIMD), 82 (8 waves, LDS-DMA,
+// 2 per SIMD) or 2 (the ping-pong
+// kernels: 8 waves in two staggered groups).  Default 42,42: the LDS-DMA staging frees the 16 staging VGPRs and
+// the VALU / LDS writes of the register path; op-level 1.204 vs 1.277 ms (GPT-2 B 128) and 0.666 vs 0.702 ms
+// (Llama GQA) against 4,4 (profiles/bench/ab_attn_dma_occ.log).  43 spills (27-275 VGPRs at 168) and runs 2.5x
+// slower; the ping-pong pair loses 13-27 % (ab_attn_pp_b128.log).
+static int g_mode = -1, g_nw_dq = 42, g_nw_dkv = 42;
+
+static int nw_code(int v) { return (v == 8 || v == 4 || v == 42 || v == 43 || v == 82) ? v : 2; }
 
 static void config_init() {
     if (g_mode >= 0) return;
@@ -920,8 +963,8 @@ static void config_init() {
     if (const char* n = getenv("BPE_FA_SPLIT_NW")) {
         int a = 4, c = 4;
         if (sscanf(n, "%d,%d", &a, &c) >= 1) {
-            g_nw_dq = a == 8 ? 8 : a == 4 ? 4 : 2;
-            g_nw_dkv = c == 8 ? 8 : c == 4 ? 4 : 2;
+            g_nw_dq = nw_code(a);
+            g_nw_dkv = nw_code(c);
         }
     }
 }
@@ -935,23 +978,23 @@ bool fa_bwd_split_active(int D) {
 int fa_bwd_config(int mode, int nw_dq, int nw_dkv) {
     config_init();
     if (mode >= 0) g_mode = mode ? 1 : 0;
-    if (nw_dq > 0) g_nw_dq = nw_dq == 8 ? 8 : nw_dq == 4 ? 4 : 2;
-    if (nw_dkv > 0) g_nw_dkv = nw_dkv == 8 ? 8 : nw_dkv == 4 ? 4 : 2;
+    if (nw_dq > 0) g_nw_dq = nw_code(nw_dq);
+    if (nw_dkv > 0) g_nw_dkv = nw_code(nw_dkv);
     return g_mode;
 }
 
-template <bool C, bool R, bool RIN, int NW>
+template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false>
 static void dq_launch(const FaArgs& a, hipStream_t s) {
     const int nqb = (a.S + 32 * NW - 1) / (32 * NW);
-    split::fa_bwd_dq_kernel<C, R, RIN, NW><<<nqb * a.B * a.H, NW * 64, 4 * split::TILE, s>>>(
+    split::fa_bwd_dq_kernel<C, R, RIN, NW, OCC, DMA><<<nqb * a.B * a.H, NW * 64, 4 * split::TILE, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do, a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin,
         a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
 }
 
-template <bool C, bool R, bool RIN, int NW>
+template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false>
 static void dkv_launch(const FaArgs& a, hipStream_t s) {
     const int nkb = (a.S + 32 * NW - 1) / (32 * NW);
-    split::fa_bwd_dkv_kernel<C, R, RIN, NW><<<nkb * a.B * a.H, NW * 64, 4 * split::TILE + 1024, s>>>(
+    split::fa_bwd_dkv_kernel<C, R, RIN, NW, OCC, DMA><<<nkb * a.B * a.H, NW * 64, 4 * split::TILE + 1024, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.dkv_part, a.cos,
         a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
 }
@@ -978,9 +1021,15 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
     const int nq = g_nw_dq, nk = g_nw_dkv;
     if (nq == 2) dq_pp_launch<C, R, RIN>(a, s);
     else if (nq == 8) dq_launch<C, R, RIN, 8>(a, s);
+    else if (nq == 42) dq_launch<C, R, RIN, 4, 2, true>(a, s);
+    else if (nq == 43) dq_launch<C, R, RIN, 4, 3, true>(a, s);
+    else if (nq == 82) dq_launch<C, R, RIN, 8, 2, true>(a, s);
     else dq_launch<C, R, RIN, 4>(a, s);
     if (nk == 2) dkv_pp_launch<C, R, RIN>(a, s);
     else if (nk == 8) dkv_launch<C, R, RIN, 8>(a, s);
+    else if (nk == 42) dkv_launch<C, R, RIN, 4, 2, true>(a, s);
+    else if (nk == 43) dkv_launch<C, R, RIN, 4, 3, true>(a, s);
+    else if (nk == 82) dkv_launch<C, R, RIN, 8, 2, true>(a, s);
     else dkv_launch<C, R, RIN, 4>(a, s);
 }
 

@@ -277,8 +277,6 @@ fa_fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
 //   * buffers: K(j) in Ks[j & 1], V(j) in Vs[j & 1]; iteration t waits for K(t+1), V(t) (DMA issued one
 //     iteration earlier) with ONE barrier, then issues K(t+2), V(t+1) into the buffers iteration t-1 read.
 // ---------------------------------------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) const void gbl_void_t;
 
 struct FwdV3 {
     static constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4;

@@ -27,8 +27,8 @@ namespace v4 {
 constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4, SPT = 2;  // SPT: 16-byte chunks per thread and tensor
 constexpr float THR = 8.0f;                                        // deferred-rescale threshold (log2 units)
 
-template <bool CAUSAL>
-__global__ void __launch_bounds__(256, 2)
+template <bool CAUSAL, int OCC = 2>
+__global__ void __launch_bounds__(256, OCC)
 fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                  long ld_q, long ld_kv, __bf16* __restrict__ O, long ld_o, float* __restrict__ LSE, int B, int H,
                  int Hkv, int S, float scale_log2, int group, float* __restrict__ DQZ) {
@@ -402,18 +402,21 @@ fa_fwd_pp_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 using namespace bpe;
 using namespace bpe::fa;
 
-// forward version for D = 64 without in-kernel RoPE: 4 (default, this file) or 2 (fa_fwd_kernel); BPE_FA_FWD
-// sets the initial value, fa_fwd_config changes it at run time (A/B, tests)
+// forward version for D = 64 without in-kernel RoPE: 6 (default: this file's kernel at 3 waves per SIMD), 4 (the
+// same at 2) or 2 (fa_fwd_kernel); BPE_FA_FWD sets the initial value, fa_fwd_config changes it at run time (A/B,
+// tests).  6 vs 4: 0.364 vs 0.371 ms at GPT-2 B 128 (profiles/bench/ab_attn_dma_occ.log)
 static int g_fwd_ver = -1;
 
-// 2 (fa_fwd_kernel), 4 (fa_fwd_v4_kernel, the default) or 5 (fa_fwd_pp_kernel); BPE_FA_FWD sets the initial value
+// 2 (fa_fwd_kernel), 4 (fa_fwd_v4_kernel), 5 (fa_fwd_pp_kernel) or 6 (fa_fwd_v4_kernel at 3 waves per SIMD:
+// 162-168 VGPRs, no spills; the default)
+static int fwd_ver_code(int v) { return (v == 2 || v == 4 || v == 5) ? v : 6; }
+
 int fa_fwd_config(int ver) {
     if (g_fwd_ver < 0) {
         const char* e = getenv("BPE_FA_FWD");
-        const int v = e ? atoi(e) : 4;
-        g_fwd_ver = (v == 2 || v == 5) ? v : 4;
+        g_fwd_ver = fwd_ver_code(e ? atoi(e) : 6);
     }
-    if (ver > 0) g_fwd_ver = (ver == 2 || ver == 5) ? ver : 4;
+    if (ver > 0) g_fwd_ver = fwd_ver_code(ver);
     return g_fwd_ver;
 }
 
@@ -429,7 +432,8 @@ bool launch_fa_fwd_v4(const FaArgs& a, hipStream_t s) {
         return true;
     }
     const int nqb = (a.S + 127) / 128;
-    auto* k = a.causal ? &v4::fa_fwd_v4_kernel<true> : &v4::fa_fwd_v4_kernel<false>;
+    auto* k = ver == 6 ? (a.causal ? &v4::fa_fwd_v4_kernel<true, 3> : &v4::fa_fwd_v4_kernel<false, 3>)
+                       : (a.causal ? &v4::fa_fwd_v4_kernel<true> : &v4::fa_fwd_v4_kernel<false>);
     k<<<nqb * a.B * a.H, 256, 4 * v4::TILE, s>>>(a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.lse, a.B, a.H, a.Hkv,
                                                  a.S, a.scale * LOG2E, fa_group(a.B * a.H), a.dq_acc);
     return true;

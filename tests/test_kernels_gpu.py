@@ -509,6 +509,33 @@ def test_flash_attention_gpt2_shape(gpu_device):
     assert rel(g.cpu(), gr) < 3e-2
 
 
+@pytest.mark.parametrize("S", [1024, 200, 64])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("ver", [2, 6])
+def test_flash_fwd_versions_agree(gpu_device, S, causal, ver):
+    """The D = 64 forward versions on pre-rotated Q / K: v2 (fa_fwd_kernel) and v6 (the v4 kernel at 3 waves per
+    SIMD) against the default v4 -- O within bf16 rounding, v6 bitwise (same code, other register budget)."""
+    h = torch.ops.bpe_hip
+    B, H, D = 2, 4, 64
+    torch.manual_seed(5)
+    x = torch.randn(B * S, 3 * H * D, device=gpu_device, dtype=torch.bfloat16)
+    q, k, v = x[:, : H * D], x[:, H * D : 2 * H * D], x[:, 2 * H * D :]
+    e = torch.empty(0, 0, device=gpu_device)
+    prev = h.fa_fwd_config(0)
+    try:
+        h.fa_fwd_config(4)
+        o4, l4 = h.fa_fwd(q, k, v, e, e, B, S, H, H, D, causal, False, D ** -0.5, False)
+        h.fa_fwd_config(ver)
+        ov, lv = h.fa_fwd(q, k, v, e, e, B, S, H, H, D, causal, False, D ** -0.5, False)
+    finally:
+        h.fa_fwd_config(prev)
+    if ver == 6:
+        assert torch.equal(o4, ov) and torch.equal(l4, lv)
+    else:
+        assert rel(ov.float().cpu(), o4.float().cpu()) < 1e-2
+        assert (lv - l4).abs().max().item() < 1e-2
+
+
 @pytest.fixture
 def fused_bwd():
     """Run the test with the fused (fp32-atomics) attention backward, the one that owns the dQ accumulator and the
@@ -523,10 +550,10 @@ def fused_bwd():
 @pytest.mark.parametrize("H,Hkv", [(4, 4), (8, 2)])
 @pytest.mark.parametrize("rope", ["fused", "prerotated", None])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("nw", [(2, 2), (4, 4), (8, 8)])
+@pytest.mark.parametrize("nw", [(2, 2), (4, 4), (8, 8), (42, 42), (43, 43), (82, 82)])
 def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal, nw):
-    """The split backward (dQ kernel + dK/dV kernel) -- the ping-pong kernels (nw == 2) or the plain ones at 4 / 8
-    waves -- against the fp32 oracle's autograd and against the fused atomics backward on the same
+    """The split backward (dQ kernel + dK/dV kernel) -- the ping-pong kernels (nw == 2), the plain ones at 4 / 8
+    waves, or the 4-wave LDS-DMA-staged ones at 2 / 3 waves per SIMD (42 / 43) -- against the fp32 oracle's autograd and against the fused atomics backward on the same
     forward outputs: dQ, dK, dV each."""
     h = torch.ops.bpe_hip
     B, D = 2, 64
@@ -549,7 +576,7 @@ def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal
         h.fa_bwd_config(1, 0, 0)
         fused = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)
     finally:
-        h.fa_bwd_config(prev, 4, 4)
+        h.fa_bwd_config(prev, 42, 42)
     assert torch.equal(got, again), "split backward is not deterministic"
     qr = qkv.float().cpu().requires_grad_(True)
     orf = ops.attention_qkv_reference(qr, B, S, H, Hkv, D, cos.cpu() if use_rope else None,
@@ -776,7 +803,7 @@ def test_accumulate_weight_grad_fp32_buffer(gpu_device):
     assert e32 < 1e-6 and e16 > 100 * e32, (e32, e16)
 
 
-@pytest.mark.parametrize("ver", [4, 5])
+@pytest.mark.parametrize("ver", [4, 5, 6])
 @pytest.mark.parametrize("S,H,Hkv,causal", [(1024, 4, 4, True), (200, 8, 2, True), (1000, 4, 4, False), (64, 2, 2, True),
                                             (600, 2, 2, True)])
 def test_flash_fwd_v4_matches_v2_and_oracle(gpu_device, S, H, Hkv, causal, ver):
