@@ -27,7 +27,7 @@ namespace v4 {
 constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4, SPT = 2;  // SPT: 16-byte chunks per thread and tensor
 constexpr float THR = 8.0f;                                        // deferred-rescale threshold (log2 units)
 
-template <bool CAUSAL, int OCC = 2>
+template <bool CAUSAL, int OCC = 2, bool DMA = false>
 __global__ void __launch_bounds__(256, OCC)
 fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                  long ld_q, long ld_kv, __bf16* __restrict__ O, long ld_o, float* __restrict__ LSE, int B, int H,
@@ -94,12 +94,26 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     const int trow = 4 * hh + ((l & 15) >> 2);
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
-    load_tile(0);
-    write_tile(0);
+    // DMA: K / V tiles by LDS-DMA (fa_common.h dma_tile64; rows past the end arrive clamped and are masked below)
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    if constexpr (DMA) {
+        dma_tile64<4>(kbase, ld_kv, 0, S, Ks, wu, l);
+        dma_tile64<4>(vbase, ld_kv, 0, S, Vs, wu, l);
+    } else {
+        load_tile(0);
+        write_tile(0);
+    }
     __syncthreads();
     for (int t = 0; t < ntiles; ++t) {
         const int cur = t & 1, n0 = t * 64;
-        if (t + 1 < ntiles) load_tile(t + 1);
+        if (t + 1 < ntiles) {
+            if constexpr (DMA) {  // buffer cur ^ 1 was last read in tile t - 1, before its closing barrier
+                dma_tile64<4>(kbase, ld_kv, n0 + 64, S, Ks + (cur ^ 1) * TILE, wu, l);
+                dma_tile64<4>(vbase, ld_kv, n0 + 64, S, Vs + (cur ^ 1) * TILE, wu, l);
+            } else {
+                load_tile(t + 1);
+            }
+        }
         if (!CAUSAL || n0 <= qw0 + 31) {
             const char* Kc = Ks + cur * TILE;
             char* Vc = Vs + cur * TILE;
@@ -161,7 +175,7 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                 lacc = mfma(ones, pf[kk], lacc);
             }
         }
-        if (t + 1 < ntiles) write_tile(cur ^ 1);
+        if (!DMA && t + 1 < ntiles) write_tile(cur ^ 1);
         __syncthreads();
     }
 
@@ -402,19 +416,21 @@ fa_fwd_pp_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 using namespace bpe;
 using namespace bpe::fa;
 
-// forward version for D = 64 without in-kernel RoPE: 6 (default: this file's kernel at 3 waves per SIMD), 4 (the
-// same at 2) or 2 (fa_fwd_kernel); BPE_FA_FWD sets the initial value, fa_fwd_config changes it at run time (A/B,
-// tests).  6 vs 4: 0.364 vs 0.371 ms at GPT-2 B 128 (profiles/bench/ab_attn_dma_occ.log)
+// forward version for D = 64 without in-kernel RoPE: 7 (default: this file's kernel at 3 waves per SIMD with K / V
+// staged by LDS-DMA), 6 (the same with register staging), 4 (register staging at 2 waves per SIMD) or 2
+// (fa_fwd_kernel); BPE_FA_FWD sets the initial value, fa_fwd_config changes it at run time (A/B, tests).
+// Same box, op-level (profiles/bench/ab_attn_fwd_dma.log): GPT-2 B 128 0.342 / 0.356 / 0.362 ms for 7 / 6 / 4,
+// Llama GQA (8, 2048, 32, 4) 0.178 / 0.196 / 0.193 ms.
 static int g_fwd_ver = -1;
 
-// 2 (fa_fwd_kernel), 4 (fa_fwd_v4_kernel), 5 (fa_fwd_pp_kernel) or 6 (fa_fwd_v4_kernel at 3 waves per SIMD:
-// 162-168 VGPRs, no spills; the default)
-static int fwd_ver_code(int v) { return (v == 2 || v == 4 || v == 5) ? v : 6; }
+// 2 (fa_fwd_kernel), 4 (fa_fwd_v4_kernel), 5 (fa_fwd_pp_kernel), 6 (fa_fwd_v4_kernel at 3 waves per SIMD: 162-168
+// VGPRs, no spills) or 7 (6 with LDS-DMA staging, 164-166 VGPRs; the default)
+static int fwd_ver_code(int v) { return (v == 2 || v == 4 || v == 5 || v == 6) ? v : 7; }
 
 int fa_fwd_config(int ver) {
     if (g_fwd_ver < 0) {
         const char* e = getenv("BPE_FA_FWD");
-        g_fwd_ver = fwd_ver_code(e ? atoi(e) : 6);
+        g_fwd_ver = fwd_ver_code(e ? atoi(e) : 7);
     }
     if (ver > 0) g_fwd_ver = fwd_ver_code(ver);
     return g_fwd_ver;
@@ -432,8 +448,9 @@ bool launch_fa_fwd_v4(const FaArgs& a, hipStream_t s) {
         return true;
     }
     const int nqb = (a.S + 127) / 128;
-    auto* k = ver == 6 ? (a.causal ? &v4::fa_fwd_v4_kernel<true, 3> : &v4::fa_fwd_v4_kernel<false, 3>)
-                       : (a.causal ? &v4::fa_fwd_v4_kernel<true> : &v4::fa_fwd_v4_kernel<false>);
+    auto* k = ver == 6   ? (a.causal ? &v4::fa_fwd_v4_kernel<true, 3> : &v4::fa_fwd_v4_kernel<false, 3>)
+              : ver == 7 ? (a.causal ? &v4::fa_fwd_v4_kernel<true, 3, true> : &v4::fa_fwd_v4_kernel<false, 3, true>)
+                         : (a.causal ? &v4::fa_fwd_v4_kernel<true> : &v4::fa_fwd_v4_kernel<false>);
     k<<<nqb * a.B * a.H, 256, 4 * v4::TILE, s>>>(a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.lse, a.B, a.H, a.Hkv,
                                                  a.S, a.scale * LOG2E, fa_group(a.B * a.H), a.dq_acc);
     return true;
