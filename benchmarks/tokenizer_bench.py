@@ -42,6 +42,27 @@ def timed(fn, reps=1):
     return best, out
 
 
+def effective_cores(n: int = 8, mb: int = 32) -> float:
+    """How many threads actually run at once right now: n GIL-free sha256 threads against one.  On a shared or
+    oversubscribed box this is far below os.cpu_count(), and parallel rows then measure no thread scaling."""
+    import hashlib
+    import threading
+
+    data = b"x" * (mb << 20)
+
+    def run(k: int) -> float:
+        ts = [threading.Thread(target=lambda: hashlib.sha256(data).digest()) for _ in range(k)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        return time.perf_counter() - t0
+
+    one = min(run(1) for _ in range(2))
+    return round(n * one / min(run(n) for _ in range(2)), 2)
+
+
 def emit(name, seconds, **extra):
     ref = REF.get(name)
     row = {"workload": name, "seconds": round(seconds, 4), "reference_seconds": ref,
@@ -55,6 +76,8 @@ def main():
     ap.add_argument("--repeat", type=int, default=150, help="corpus.en copies in the large file (150 = 19.96 MB)")
     ap.add_argument("--workers", type=int, default=8)
     a = ap.parse_args()
+    # printed first, and again last: parallel rows only show thread scaling where this is near --workers
+    print(json.dumps({"cpu_count": os.cpu_count(), "effective_cores_8_threads": effective_cores()}), flush=True)
 
     t, (vocab, merges) = timed(lambda: train_bpe(FIXTURE, 500, SPECIAL), reps=3)
     emit("train_bpe_corpus_en_v500", t, merges=len(merges))
@@ -72,7 +95,7 @@ def main():
                                               n_workers=a.workers), reps=3)
         emit("pretokenize_parallel", t, MB=round(mb, 2), pretokens=sum(counts.values()), unique=len(counts))
         t, counts = timed(lambda: pretokenize(big, special_tokens=SPECIAL, parallel_processing=False,
-                                              n_workers=1))
+                                              n_workers=1), reps=3)
         emit("pretokenize_serial", t, MB=round(mb, 2), pretokens=sum(counts.values()))
 
         t, (vocab, merges) = timed(lambda: train_bpe(big, 10_000, SPECIAL, n_workers=a.workers))
@@ -91,6 +114,7 @@ def main():
         emit("encode_iterable_serial", t, tokens=n, tok_per_s=round(n / t))
         t, n = timed(lambda: run(a.workers))
         emit("encode_iterable_parallel", t, tokens=n, tok_per_s=round(n / t))
+    print(json.dumps({"effective_cores_8_threads_after": effective_cores()}), flush=True)
 
 
 if __name__ == "__main__":
