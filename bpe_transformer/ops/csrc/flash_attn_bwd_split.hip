@@ -40,7 +40,7 @@ constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4;
 // staged 16-byte chunks per thread and tensor for one 64-row tile (512 chunks)
 template <int NW> constexpr int cpt() { return 512 / (NW * 64); }
 
-template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false>
+template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false>
 __global__ void __launch_bounds__(NW * 64, OCC)
 fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                  long ld_q, long ld_kv, const __bf16* __restrict__ O, long ld_o, const __bf16* __restrict__ dO,
@@ -163,19 +163,46 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
             }
             if (!CAUSAL || k0 <= qw + 31) {
                 const bool need_mask = (CAUSAL && k0 + 63 > qw) || (k0 + 64 > S);
-    #pragma unroll
+#pragma unroll
                 for (int kh = 0; kh < 2; ++kh) {
                     if (CAUSAL && k0 + 32 * kh > qw + 31) break;  // this 32-key half is past every query of the wave
                     f32x16 sp = ns, dp = nd;
-    #pragma unroll
-                    for (int ks = 0; ks < KS; ++ks) {
-                        const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
-                        sp = mfma(lds_row16(Kc, koff), qf[ks], sp);
-                        dp = mfma(lds_row16(Vc, koff), of[ks], dp);
+                    bf16x8 tk[2][2];  // SCHED: the transposed K fragments of the dQ products (s, dt)
+                    if constexpr (SCHED) {  // operand reads batched ahead of their uses (see fa_bwd_dkv_kernel)
+                        bf16x8 fk[KS], fv[KS];
+#pragma unroll
+                        for (int ks = 0; ks < KS; ++ks) {
+                            const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
+                            fk[ks] = lds_row16(Kc, koff);
+                            fv[ks] = lds_row16(Vc, koff);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int ks = 0; ks < KS; ++ks) {
+                            sp = mfma(fk[ks], qf[ks], sp);
+                            dp = mfma(fv[ks], of[ks], dp);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int s = 0; s < 2; ++s)
+#pragma unroll
+                            for (int dt = 0; dt < 2; ++dt) {
+                                const int kr = 32 * kh + 16 * s;
+                                tk[s][dt] = lds_tr_pair(Kc, tr_off<RB>(kr + trow, 32 * dt + tcol),
+                                                        tr_off<RB>(kr + 8 + trow, 32 * dt + tcol));
+                            }
+                        __builtin_amdgcn_sched_barrier(0);
+                    } else {
+#pragma unroll
+                        for (int ks = 0; ks < KS; ++ks) {
+                            const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
+                            sp = mfma(lds_row16(Kc, koff), qf[ks], sp);
+                            dp = mfma(lds_row16(Vc, koff), of[ks], dp);
+                        }
                     }
                     // P^T = exp2(S^T c - lse), dS^T = P^T (dP^T - delta); key = row of the accumulator, query = lane
                     if (need_mask) {
-    #pragma unroll
+#pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             const int key = k0 + 32 * kh + acc_row(r, hh);
                             const float p = fast_exp2(sp[r]);
@@ -183,21 +210,25 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                             dp[r] = ok ? p * dp[r] : 0.f;
                         }
                     } else {
-    #pragma unroll
+#pragma unroll
                         for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(sp[r]) * dp[r];
                     }
                     // dQ^T += K^T.dS^T: registers 8s..8s+7 are k-step s (keys 16 s ..) in the MFMA's permuted order
-    #pragma unroll
+#pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         bf16x8 db;
-    #pragma unroll
+#pragma unroll
                         for (int j = 0; j < 8; ++j) db[j] = (__bf16)dp[8 * s + j];
                         const int kr = 32 * kh + 16 * s;
-    #pragma unroll
-                        for (int dt = 0; dt < 2; ++dt)
-                            acc[dt] = mfma(lds_tr_pair(Kc, tr_off<RB>(kr + trow, 32 * dt + tcol),
-                                                       tr_off<RB>(kr + 8 + trow, 32 * dt + tcol)),
-                                           db, acc[dt]);
+#pragma unroll
+                        for (int dt = 0; dt < 2; ++dt) {
+                            if constexpr (SCHED)
+                                acc[dt] = mfma(tk[s][dt], db, acc[dt]);
+                            else
+                                acc[dt] = mfma(lds_tr_pair(Kc, tr_off<RB>(kr + trow, 32 * dt + tcol),
+                                                           tr_off<RB>(kr + 8 + trow, 32 * dt + tcol)),
+                                               db, acc[dt]);
+                        }
                     }
                 }
             }
@@ -232,7 +263,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     }
 }
 
-template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false>
+template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false>
 __global__ void __launch_bounds__(NW * 64, OCC)
 fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                   long ld_q, long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
@@ -368,27 +399,61 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
             const float* dc = dltS + cur * 64;
             if (!CAUSAL || m0 + 63 >= kw0) {
                 const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + 64 > S) || (kw0 + 32 > S);
-    #pragma unroll
+#pragma unroll
                 for (int qt = 0; qt < 2; ++qt) {
                     if (CAUSAL && m0 + 32 * qt + 31 < kw0) continue;  // every query of this half precedes every key
                     f32x16 sp, dp;
-    #pragma unroll
+                    // every operand read of the half is issued before its first use (SCHED): the S / dP row
+                    // fragments before the chains, the transposed dV / dK fragments before the softmax VALU, so
+                    // their LDS latency is paid once per batch instead of once per MFMA (hipcc's own schedule
+                    // waits lgkmcnt(0) in front of every MFMA pair)
+                    bf16x8 fq[KS], fo[KS], tq[2][2], to[2][2];
+                    if constexpr (SCHED) {
+#pragma unroll
+                        for (int ks = 0; ks < KS; ++ks) {
+                            const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
+                            fq[ks] = lds_row16(Qc, off);
+                            fo[ks] = lds_row16(Oc, off);
+                        }
+                    }
+#pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int qi = qt * 32 + 8 * i + 4 * hh;  // rows qi..qi+3 of registers 4i..4i+3
                         const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
                         const f32x4 dl = *reinterpret_cast<const f32x4*>(dc + qi);
-    #pragma unroll
+#pragma unroll
                         for (int j = 0; j < 4; ++j) { sp[4 * i + j] = lv[j]; dp[4 * i + j] = dl[j]; }
                     }
-    #pragma unroll
-                    for (int ks = 0; ks < KS; ++ks) {
-                        const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
-                        sp = mfma(lds_row16(Qc, off), kf[ks], sp);
-                        dp = mfma(lds_row16(Oc, off), vf[ks], dp);
+                    if constexpr (SCHED) {
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int ks = 0; ks < KS; ++ks) {
+                            sp = mfma(fq[ks], kf[ks], sp);
+                            dp = mfma(fo[ks], vf[ks], dp);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+                            for (int dt = 0; dt < 2; ++dt) {
+                                const int qr = qt * 32 + 16 * ss;
+                                const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
+                                const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
+                                to[ss][dt] = lds_tr_pair(Oc, o0, o1);
+                                tq[ss][dt] = lds_tr_pair(Qc, o0, o1);
+                            }
+                        __builtin_amdgcn_sched_barrier(0);
+                    } else {
+#pragma unroll
+                        for (int ks = 0; ks < KS; ++ks) {
+                            const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
+                            sp = mfma(lds_row16(Qc, off), kf[ks], sp);
+                            dp = mfma(lds_row16(Oc, off), vf[ks], dp);
+                        }
                     }
                     if (need_mask) {
                         const int qoff = m0 + qt * 32 - klim;
-    #pragma unroll
+#pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             const float p = fast_exp2(sp[r]);
                             const bool ok = (unsigned)(qoff + acc_row(r, hh)) < span;
@@ -396,28 +461,33 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
                             dp[r] = ok ? p * dp[r] : 0.f;
                         }
                     } else {
-    #pragma unroll
+#pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             const float p = fast_exp2(sp[r]);
                             sp[r] = p;
                             dp[r] *= p;
                         }
                     }
-    #pragma unroll
+#pragma unroll
                     for (int ss = 0; ss < 2; ++ss) {
                         bf16x8 pb, db;
-    #pragma unroll
+#pragma unroll
                         for (int j = 0; j < 8; ++j) {
                             pb[j] = (__bf16)sp[8 * ss + j];
                             db[j] = (__bf16)dp[8 * ss + j];
                         }
                         const int qr = qt * 32 + 16 * ss;
-    #pragma unroll
+#pragma unroll
                         for (int dt = 0; dt < 2; ++dt) {
-                            const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
-                            const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
-                            dv[dt] = mfma(lds_tr_pair(Oc, o0, o1), pb, dv[dt]);
-                            dk[dt] = mfma(lds_tr_pair(Qc, o0, o1), db, dk[dt]);
+                            if constexpr (SCHED) {
+                                dv[dt] = mfma(to[ss][dt], pb, dv[dt]);
+                                dk[dt] = mfma(tq[ss][dt], db, dk[dt]);
+                            } else {
+                                const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
+                                const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
+                                dv[dt] = mfma(lds_tr_pair(Oc, o0, o1), pb, dv[dt]);
+                                dk[dt] = mfma(lds_tr_pair(Qc, o0, o1), db, dk[dt]);
+                            }
                         }
                     }
                 }
@@ -946,15 +1016,17 @@ using namespace bpe::fa;
 // Backward form: 0 = split (default for D = 64), 1 = fused (flash_attn_bwd.hip, the atomics form).  Initial value
 // from BPE_FA_BWD ("fused" / "split"), changeable at run time (fa_bwd_config) for same-process A/B and tests.
 // Waves per workgroup of the two split kernels: BPE_FA_SPLIT_NW="<dq>,<dkv>", each 4 or 8 (the plain kernels with
-// register-staged tiles), 42 / 43 (4 waves, tiles staged by LDS-DMA, 2 / 3 waves per SIMD), 82 (8 waves, LDS-DMA,
-// 2 per SIMD) or 2 (the ping-pong
-// kernels: 8 waves in two staggered groups).  Default 42,42: the LDS-DMA staging frees the 16 staging VGPRs and
-// the VALU / LDS writes of the register path; op-level 1.204 vs 1.277 ms (GPT-2 B 128) and 0.666 vs 0.702 ms
-// (Llama GQA) against 4,4 (profiles/bench/ab_attn_dma_occ.log).  43 spills (27-275 VGPRs at 168) and runs 2.5x
-// slower; the ping-pong pair loses 13-27 % (ab_attn_pp_b128.log).
-static int g_mode = -1, g_nw_dq = 42, g_nw_dkv = 42;
+// register-staged tiles), 42 / 43 (4 waves, tiles staged by LDS-DMA, 2 / 3 waves per SIMD), 44 (42 with every
+// operand read of a half-step issued ahead of its MFMAs, SCHED), 82 (8 waves, LDS-DMA) or 2 (the ping-pong
+// kernels: 8 waves in two staggered groups).  Default 44,44.  Op-level, same box (profiles/bench/ab_attn_dma_occ.log,
+// ab_attn_sched.log): LDS-DMA staging 1.178-1.204 vs 1.207-1.277 ms for 4,4 (GPT-2 B 128) and 0.666 vs 0.702 ms
+// (Llama GQA); the batched reads another -0.4-0.5 % (1.159 vs 1.164, 1.179 vs 1.185; Llama 0.649 vs 0.655).
+// Measured and dropped: 43 (168 VGPRs: 27-275 spilled, 2.5x slower), 82 (+10 %), a two-half software pipeline of
+// the dK/dV kernel (S/dP of half 1 under the softmax of half 0, sched_group_barrier 1 MFMA : 5 VALU; +2.3 %), the
+// ping-pong pair (+13-27 %, ab_attn_pp_b128.log).
+static int g_mode = -1, g_nw_dq = 44, g_nw_dkv = 44;
 
-static int nw_code(int v) { return (v == 8 || v == 4 || v == 42 || v == 43 || v == 82) ? v : 2; }
+static int nw_code(int v) { return (v == 8 || v == 4 || v == 42 || v == 43 || v == 82 || v == 44) ? v : 2; }
 
 static void config_init() {
     if (g_mode >= 0) return;
@@ -983,18 +1055,18 @@ int fa_bwd_config(int mode, int nw_dq, int nw_dkv) {
     return g_mode;
 }
 
-template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false>
+template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false>
 static void dq_launch(const FaArgs& a, hipStream_t s) {
     const int nqb = (a.S + 32 * NW - 1) / (32 * NW);
-    split::fa_bwd_dq_kernel<C, R, RIN, NW, OCC, DMA><<<nqb * a.B * a.H, NW * 64, 4 * split::TILE, s>>>(
+    split::fa_bwd_dq_kernel<C, R, RIN, NW, OCC, DMA, SCHED><<<nqb * a.B * a.H, NW * 64, 4 * split::TILE, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do, a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin,
         a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
 }
 
-template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false>
+template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false>
 static void dkv_launch(const FaArgs& a, hipStream_t s) {
     const int nkb = (a.S + 32 * NW - 1) / (32 * NW);
-    split::fa_bwd_dkv_kernel<C, R, RIN, NW, OCC, DMA><<<nkb * a.B * a.H, NW * 64, 4 * split::TILE + 1024, s>>>(
+    split::fa_bwd_dkv_kernel<C, R, RIN, NW, OCC, DMA, SCHED><<<nkb * a.B * a.H, NW * 64, 4 * split::TILE + 1024, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.dkv_part, a.cos,
         a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
 }
@@ -1024,12 +1096,14 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
     else if (nq == 42) dq_launch<C, R, RIN, 4, 2, true>(a, s);
     else if (nq == 43) dq_launch<C, R, RIN, 4, 3, true>(a, s);
     else if (nq == 82) dq_launch<C, R, RIN, 8, 2, true>(a, s);
+    else if (nq == 44) dq_launch<C, R, RIN, 4, 2, true, true>(a, s);
     else dq_launch<C, R, RIN, 4>(a, s);
     if (nk == 2) dkv_pp_launch<C, R, RIN>(a, s);
     else if (nk == 8) dkv_launch<C, R, RIN, 8>(a, s);
     else if (nk == 42) dkv_launch<C, R, RIN, 4, 2, true>(a, s);
     else if (nk == 43) dkv_launch<C, R, RIN, 4, 3, true>(a, s);
     else if (nk == 82) dkv_launch<C, R, RIN, 8, 2, true>(a, s);
+    else if (nk == 44) dkv_launch<C, R, RIN, 4, 2, true, true>(a, s);
     else dkv_launch<C, R, RIN, 4>(a, s);
 }
 
