@@ -263,7 +263,8 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     }
 }
 
-template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false>
+template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false,
+          bool LOOPG = false>
 __global__ void __launch_bounds__(NW * 64, OCC)
 fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                   long ld_q, long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
@@ -279,9 +280,15 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
     const int nkb = (S + KB - 1) / KB;
+    // LOOPG (GQA): one workgroup per (batch, KV head, key block) sweeps the G query heads of its group one after
+    // the other, summing their dK / dV in the accumulators -- no fp32 partials, no reduce kernel.  Otherwise one
+    // workgroup per (batch, query head, key block).
+    const int G = H / Hkv, GL = LOOPG ? G : 1;
     int kblk, bh;  // causal: key block 0 (the most query tiles) first
-    grouped_order((int)blockIdx.x, nkb, B * H, group, kblk, bh);
-    const int b = bh / H, h = bh % H, G = H / Hkv, hk = h / G;
+    grouped_order((int)blockIdx.x, nkb, B * (LOOPG ? Hkv : H), group, kblk, bh);
+    const int b = LOOPG ? bh / Hkv : bh / H;
+    const int h = LOOPG ? (bh % Hkv) * G : bh % H;  // (first) query head
+    const int hk = h / G;
     const int kb0 = kblk * KB, kw0 = kb0 + 32 * w, key = kw0 + l31;
     const bool key_ok = key < S;
     const long kpos = key_ok ? key : S - 1;
@@ -323,16 +330,21 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
 
     const int m_start = CAUSAL ? kb0 : 0;  // kb0 is a multiple of 64
     const int nqt = m_start < S ? (S - m_start + 63) / 64 : 0;
-    const __bf16* qb = Q + (long)b * S * ld_q + (long)h * D;
-    const __bf16* ob = dO + (long)b * S * ld_do + (long)h * D;
-    const long sbase = ((long)b * H + h) * S;
+    const int nsteps = GL * nqt;  // (query head, query tile) steps, head-major
+    // step j: query head h + j / nqt, query tile j % nqt
+    auto q_of = [&](int j) { return Q + (long)b * S * ld_q + (long)(h + j / nqt) * D; };
+    auto o_of = [&](int j) { return dO + (long)b * S * ld_do + (long)(h + j / nqt) * D; };
+    auto m0_of = [&](int j) { return m_start + (j % nqt) * 64; };
     u16x8 qreg[CPT], oreg[CPT];
     float lreg = 0.f, dreg = 0.f;
     // DM: Q / dO tiles by LDS-DMA (no staging registers); only the row constants go through registers
     constexpr bool DM = DMA && !ROPE_IN;
     const int wu = __builtin_amdgcn_readfirstlane(w);
     auto load_tile = [&](int it) {
-        const int m0 = m_start + it * 64;
+        const int m0 = m0_of(it);
+        const __bf16* qb = q_of(it);
+        const __bf16* ob = o_of(it);
+        const long sbase = ((long)b * H + h + it / nqt) * S;
         const long idx = sbase + min(m0 + l, S - 1);  // every wave loads the stats (wave 0 writes them)
         lreg = LSE[idx];
         dreg = DELTA[idx];
@@ -347,7 +359,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
         }
     };
     auto write_tile = [&](int it, int buf) {
-        const int m0 = m_start + it * 64;
+        const int m0 = m0_of(it);
 #pragma unroll
         for (int i = 0; i < (DM ? 0 : CPT); ++i) {
             const int e = tid + NT * i, r = e >> 3, c = e & 7;
@@ -371,8 +383,8 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     if (nqt > 0) {
         load_tile(0);
         if constexpr (DM) {
-            dma_tile64<NW>(qb, ld_q, m_start, S, Qs, wu, l);
-            dma_tile64<NW>(ob, ld_do, m_start, S, dOs, wu, l);
+            dma_tile64<NW>(q_of(0), ld_q, m_start, S, Qs, wu, l);
+            dma_tile64<NW>(o_of(0), ld_do, m_start, S, dOs, wu, l);
         }
         write_tile(0, 0);
     }
@@ -382,17 +394,17 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
     const int klim = CAUSAL ? (key_ok ? key : S) : (key_ok ? 0 : S);
     const unsigned span = (unsigned)(S - klim);  // valid query q: (unsigned)(q - klim) < span
-    for (int it = 0; it < nqt; ++it) {
-        const int cur = it & 1, m0 = m_start + it * 64;
+    for (int it = 0; it < nsteps; ++it) {
+        const int cur = it & 1, m0 = m0_of(it);
         // One iteration with the current and the next buffers as __restrict__ parameters: the DMA into the next
         // buffer and the fragment reads of the current one are then provably disjoint to the wait-count pass
         // (without it hipcc drains the DMA, vmcnt(0), before the first transposed read of every half-tile).
         auto body = [&](char* __restrict__ Qc, char* __restrict__ Oc, char* __restrict__ Qn, char* __restrict__ On) {
-            if (it + 1 < nqt) {
+            if (it + 1 < nsteps) {
                 load_tile(it + 1);
                 if constexpr (DM) {  // buffer cur ^ 1 was last read in iteration it - 1, before its closing barrier
-                    dma_tile64<NW>(qb, ld_q, m0 + 64, S, Qn, wu, l);
-                    dma_tile64<NW>(ob, ld_do, m0 + 64, S, On, wu, l);
+                    dma_tile64<NW>(q_of(it + 1), ld_q, m0_of(it + 1), S, Qn, wu, l);
+                    dma_tile64<NW>(o_of(it + 1), ld_do, m0_of(it + 1), S, On, wu, l);
                 }
             }
             const float* lc = lseS + cur * 64;
@@ -494,12 +506,12 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
             }
         };
         body(Qs + cur * TILE, dOs + cur * TILE, Qs + (cur ^ 1) * TILE, dOs + (cur ^ 1) * TILE);
-        if (it + 1 < nqt) write_tile(it + 1, cur ^ 1);
+        if (it + 1 < nsteps) write_tile(it + 1, cur ^ 1);
         __syncthreads();
     }
 
     if (!key_ok) return;
-    if (G > 1) {  // GQA: fp32 partials of this query head -> [b, s, h, {dK, dV}, D] for fa_dkv_reduce_kernel
+    if (G > 1 && !LOOPG) {  // GQA: fp32 partials of this query head -> [b, s, h, {dK, dV}, D] for fa_dkv_reduce_kernel
         float* pk = dKVpart + (((long)b * S + key) * H + h) * 2 * D;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
@@ -1025,11 +1037,15 @@ using namespace bpe::fa;
 // the dK/dV kernel (S/dP of half 1 under the softmax of half 0, sched_group_barrier 1 MFMA : 5 VALU; +2.3 %), the
 // ping-pong pair (+13-27 %, ab_attn_pp_b128.log).
 static int g_mode = -1, g_nw_dq = 44, g_nw_dkv = 44;
+// GQA dK / dV: 1 = one workgroup per KV head sweeping its G query heads (the plain split kernels), 0 = one per query
+// head with fp32 partials summed by fa_dkv_reduce_kernel.  BPE_FA_GQA_LOOP sets it, fa_gqa_loop_config at run time.
+static int g_gqa_loop = 1;
 
 static int nw_code(int v) { return (v == 8 || v == 4 || v == 42 || v == 43 || v == 82 || v == 44) ? v : 2; }
 
 static void config_init() {
     if (g_mode >= 0) return;
+    if (const char* e = getenv("BPE_FA_GQA_LOOP")) g_gqa_loop = atoi(e) ? 1 : 0;
     const char* e = getenv("BPE_FA_BWD");
     g_mode = (e && e[0] == 'f') ? 1 : 0;
     if (const char* n = getenv("BPE_FA_SPLIT_NW")) {
@@ -1066,6 +1082,13 @@ static void dq_launch(const FaArgs& a, hipStream_t s) {
 template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false>
 static void dkv_launch(const FaArgs& a, hipStream_t s) {
     const int nkb = (a.S + 32 * NW - 1) / (32 * NW);
+    if (a.Hkv < a.H && g_gqa_loop) {  // GQA: one workgroup per KV head sweeps its query heads (no partials / reduce)
+        split::fa_bwd_dkv_kernel<C, R, RIN, NW, OCC, DMA, SCHED, true>
+            <<<nkb * a.B * a.Hkv, NW * 64, 4 * split::TILE + 1024, s>>>(
+                a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.dkv_part,
+                a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.Hkv));
+        return;
+    }
     split::fa_bwd_dkv_kernel<C, R, RIN, NW, OCC, DMA, SCHED><<<nkb * a.B * a.H, NW * 64, 4 * split::TILE + 1024, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.dkv_part, a.cos,
         a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
@@ -1109,6 +1132,20 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
 
 void launch_fa_dkv_reduce(const FaArgs& a, hipStream_t s);  // flash_attn_bwd.hip
 
+// whether a GQA backward of head size D needs the fp32 dK / dV partials buffer (FaArgs::dkv_part): the fused
+// backward and the ping-pong dK / dV kernel always do, the plain split kernels only with the KV-head sweep off
+bool fa_dkv_partials_needed(int D) {
+    config_init();
+    return !fa_bwd_split_active(D) || !g_gqa_loop || g_nw_dkv == 2;
+}
+
+// set the GQA dK / dV form (v >= 0), return the one in force
+int fa_gqa_loop_config(int v) {
+    config_init();
+    if (v >= 0) g_gqa_loop = v ? 1 : 0;
+    return g_gqa_loop;
+}
+
 bool launch_fa_bwd_split(const FaArgs& a, hipStream_t s) {
     if (!fa_bwd_split_active(a.D)) return false;
     // rope: 0 none, 1 rotate Q / K on load and dQ / dK on output, 2 outputs only (Q / K pre-rotated)
@@ -1121,6 +1158,6 @@ bool launch_fa_bwd_split(const FaArgs& a, hipStream_t s) {
         else if (a.rope == 2) split_launch<false, true, false>(a, s);
         else split_launch<false, false, false>(a, s);
     }
-    if (a.Hkv < a.H) launch_fa_dkv_reduce(a, s);
+    if (a.Hkv < a.H && fa_dkv_partials_needed(a.D)) launch_fa_dkv_reduce(a, s);
     return true;
 }

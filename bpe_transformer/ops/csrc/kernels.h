@@ -154,9 +154,14 @@ size_t fa_bwd_lds_bytes(int D);
 void launch_fa_fwd(const FaArgs& a, hipStream_t s);
 // flash_attn_fwd_v4.hip: the D = 64 forward without in-kernel RoPE; false when not applicable / not selected
 bool launch_fa_fwd_v4(const FaArgs& a, hipStream_t s);
-int fa_fwd_config(int ver);  // forward version for that case: 4 (default), 5 (ping-pong) or 2; ver <= 0 leaves it unchanged
+int fa_fwd_config(int ver);  // forward version for that case: 7 (default), 6, 5 (ping-pong), 4 or 2; ver <= 0 leaves it
+                             // unchanged
 void launch_fa_bwd(const FaArgs& a, hipStream_t s);
 // true when launch_fa_bwd takes the split form for head dim D (no fp32 dQ accumulator, no pre / convert passes)
 bool fa_bwd_split_active(int D);
 // backward form 0 split / 1 fused and the split kernels' waves per workgroup; negative / zero = unchanged
 int fa_bwd_config(int mode, int nw_dq, int nw_dkv);
+// GQA dK / dV of the split form: 1 = one workgroup per KV head sweeps its query heads, 0 = per-query-head fp32 partials
+// + fa_dkv_reduce_kernel; v < 0 leaves it unchanged.  fa_dkv_partials_needed: whether FaArgs::dkv_part must be set.
+int fa_gqa_loop_config(int v);
+bool fa_dkv_partials_needed(int D);

@@ -563,6 +563,7 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
 // whether fa_bwd uses (and fa_fwd should zero) the fp32 dQ accumulator for head dim D
 bool fa_bwd_needs_dq_acc(int64_t D) { return !fa_bwd_split_active((int)D); }
 int64_t fa_fwd_config_op(int64_t ver) { return fa_fwd_config((int)ver); }
+int64_t fa_gqa_loop_config_op(int64_t v) { return fa_gqa_loop_config((int)v); }
 int64_t fa_bwd_config_op(int64_t mode, int64_t nw_dq, int64_t nw_dkv) {
     return fa_bwd_config((int)mode, (int)nw_dq, (int)nw_dkv);
 }
@@ -595,7 +596,8 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     if (!split)
         dq_acc = pre_zeroed ? *dq_acc_in : at::empty({B * ((S + 63) / 64 * 64), H * D}, q.options().dtype(at::kFloat));
     at::Tensor dkv_part;
-    if (Hkv < H) dkv_part = at::empty({B * S, H * 2 * D}, q.options().dtype(at::kFloat));
+    const bool need_part = Hkv < H && fa_dkv_partials_needed((int)D);  // GQA per-query-head partials (+ reduce)
+    if (need_part) dkv_part = at::empty({B * S, H * 2 * D}, q.options().dtype(at::kFloat));
     FaArgs a{};
     a.q = (const __bf16*)q.data_ptr(); a.k = (const __bf16*)k.data_ptr(); a.v = (const __bf16*)v.data_ptr();
     a.ld_q = q.stride(0); a.ld_kv = k.stride(0);
@@ -609,7 +611,7 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     __bf16* base = (__bf16*)dqkv.data_ptr();
     a.dq = base; a.ld_dq = W;
     a.dk = base + H * D; a.dv = base + (H + Hkv) * D; a.ld_dkv = W;
-    a.dkv_part = Hkv < H ? dkv_part.data_ptr<float>() : nullptr;
+    a.dkv_part = need_part ? dkv_part.data_ptr<float>() : nullptr;
     launch_fa_bwd(a, cur_stream());
     return dqkv;
 }
@@ -841,6 +843,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("fa_bwd_needs_dq_acc(int D) -> bool", &fa_bwd_needs_dq_acc);  // no tensors: a catch-all kernel
     m.def("fa_bwd_config(int mode=-1, int nw_dq=0, int nw_dkv=0) -> int", &fa_bwd_config_op);
     m.def("fa_fwd_config(int ver=0) -> int", &fa_fwd_config_op);
+    m.def("fa_gqa_loop_config(int v=-1) -> int", &fa_gqa_loop_config_op);
 }
 
 TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {

@@ -593,6 +593,45 @@ def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal
         assert e < 3e-2 and e < 2.0 * ef + 2e-3, (name, e, ef)
 
 
+@pytest.mark.parametrize("S,H,Hkv", [(1024, 8, 2), (200, 32, 4), (1000, 4, 1)])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("nw", [(44, 44), (4, 4)])
+def test_flash_bwd_gqa_head_sweep(gpu_device, S, H, Hkv, causal, nw):
+    """GQA dK / dV of the split backward: one workgroup per KV head sweeping its G query heads (fa_gqa_loop_config
+    1, the default: no fp32 partials, no reduce kernel) against the per-query-head partials + reduce form (0) and
+    against the fp32 oracle."""
+    h = torch.ops.bpe_hip
+    B, D = 2, 64
+    torch.manual_seed(13)
+    qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device=gpu_device, dtype=torch.bfloat16)
+    cos, sin = R.rope_tables(D, S, 10000.0, device=gpu_device)
+    x = qkv.clone()
+    h.rope_qk_(x, cos, sin, B, S, H, Hkv, D)
+    q, k, v = x[:, : H * D], x[:, H * D : (H + Hkv) * D], x[:, (H + Hkv) * D :]
+    scale = D ** -0.5
+    o, lse = h.fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, causal, True, scale, True)
+    do = torch.randn_like(o)
+    prev_mode = h.fa_bwd_config(0, nw[0], nw[1])
+    prev_loop = h.fa_gqa_loop_config(-1)
+    try:
+        h.fa_gqa_loop_config(1)
+        sweep = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, True, scale, True)
+        h.fa_gqa_loop_config(0)
+        part = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, True, scale, True)
+    finally:
+        h.fa_gqa_loop_config(prev_loop)
+        h.fa_bwd_config(prev_mode, 44, 44)
+    qr = qkv.float().cpu().requires_grad_(True)
+    orf = ops.attention_qkv_reference(qr, B, S, H, Hkv, D, cos.cpu(), sin.cpu(), causal)
+    orf.backward(do.float().cpu())
+    HD, KD = H * D, Hkv * D
+    for name, sl in (("dq", slice(0, HD)), ("dk", slice(HD, HD + KD)), ("dv", slice(HD + KD, HD + 2 * KD))):
+        es = rel(sweep[:, sl].float().cpu(), qr.grad[:, sl])
+        ep = rel(part[:, sl].float().cpu(), qr.grad[:, sl])
+        assert es < 3e-2 and es < 1.5 * ep + 2e-3, (name, es, ep)
+    assert torch.equal(sweep[:, :HD], part[:, :HD])  # dQ does not depend on the dK / dV form
+
+
 @pytest.mark.parametrize("S,D,H,Hkv,fused", [(1000, 64, 4, 4, False), (192, 128, 8, 4, True), (64, 64, 4, 2, True),
                                               (320, 64, 4, 4, True)])
 def test_flash_dq_acc_zeroed_by_forward(gpu_device, S, D, H, Hkv, fused, fused_bwd):
