@@ -126,6 +126,46 @@ __device__ __forceinline__ void dma_tile64(const __bf16* base, long ld, int r0, 
     }
 }
 
+// The same DMA through a buffer resource (guide T8): the resource covers one head's rows [0, S) of a row-major
+// tensor (base = the head's first element, head_bytes = ((S - 1) * ld + D) * 2), the lane's byte offset inside a
+// tile is fixed for the kernel (dma_voff, once) and the tile's row offset is the wave-uniform soffset -- no per-tile
+// vector address arithmetic (the 64-bit clamped addresses of dma_tile64 cost ~30 VALU per tile).  Rows at or past S
+// are out of range and read as zeros; the kernels mask their scores.  The resource is built inside the helper from
+// wave-uniform values (scalar instructions only); its type exists for the device target alone, so the body is
+// compiled in the device pass only.
+__device__ __forceinline__ int head_bytes(long ld, int S, int D) { return (int)(((long)(S - 1) * ld + D) * 2); }
+
+template <int NW>
+struct DmaVoff {
+    static constexpr int CPW = 512 / (NW * 64);
+    unsigned v[CPW];
+};
+
+template <int NW>
+__device__ __forceinline__ DmaVoff<NW> dma_voff(long ld, int w, int l) {
+    DmaVoff<NW> o;
+#pragma unroll
+    for (int i = 0; i < DmaVoff<NW>::CPW; ++i) {
+        const int e = 64 * (DmaVoff<NW>::CPW * w + i) + l, r = e >> 3, pc = e & 7;
+        const int sg = (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+        o.v[i] = (unsigned)((r * ld + ((pc ^ sg) << 3)) * 2);
+    }
+    return o;
+}
+
+template <int NW>
+__device__ __forceinline__ void dma_tile64_buf(const __bf16* base, int nbytes, const DmaVoff<NW>& vo, int r0, long ld,
+                                               char* img, int w) {
+#if defined(__HIP_DEVICE_COMPILE__)  // device pass only: the host pass cannot instantiate the resource type
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nbytes, 0x00020000);
+    const unsigned soff = (unsigned)((long)r0 * ld * 2);
+#pragma unroll
+    for (int i = 0; i < DmaVoff<NW>::CPW; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + 64 * (DmaVoff<NW>::CPW * w + i) * 16), 16,
+                                                 vo.v[i], soff, 0, 0);
+#endif
+}
+
 // Launch order of the (block, batch*head) work items: heads are taken in groups of `group` (batch, head) pairs
 // and, inside a group, the `nblk` blocks of every pair run heaviest first (index 0 = heaviest).  All blocks of a
 // pair thus run close together in time, so the K / V (forward) or Q / dO (backward) rows they share are re-read

@@ -134,12 +134,15 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         }
     };
 
-    // DM: K / V tiles by LDS-DMA (no staging registers; rows past the end arrive clamped and are masked below)
+    // DM: K / V tiles by LDS-DMA through buffer resources (no staging registers, no per-tile address VALU; rows
+    // past the end read as 0 and are masked below)
     constexpr bool DM = DMA && !ROPE_IN;
     const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int hbytes = head_bytes(ld_kv, S, D);
+    const DmaVoff<NW> kvo = dma_voff<NW>(ld_kv, wu, l);
     if constexpr (DM) {
-        dma_tile64<NW>(kb, ld_kv, 0, S, Ks, wu, l);
-        dma_tile64<NW>(vb, ld_kv, 0, S, Vs, wu, l);
+        dma_tile64_buf(kb, hbytes, kvo, 0, ld_kv, Ks, wu);
+        dma_tile64_buf(vb, hbytes, kvo, 0, ld_kv, Vs, wu);
     } else {
         load_tile(0);
         write_tile(0, 0);
@@ -155,8 +158,8 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                         char* __restrict__ Vn) {
             if (it + 1 < nkt) {
                 if constexpr (DM) {  // buffer cur ^ 1 was last read in iteration it - 1, before its closing barrier
-                    dma_tile64<NW>(kb, ld_kv, k0 + 64, S, Kn, wu, l);
-                    dma_tile64<NW>(vb, ld_kv, k0 + 64, S, Vn, wu, l);
+                    dma_tile64_buf(kb, hbytes, kvo, k0 + 64, ld_kv, Kn, wu);
+                    dma_tile64_buf(vb, hbytes, kvo, k0 + 64, ld_kv, Vn, wu);
                 } else {
                     load_tile(it + 1);
                 }
@@ -337,9 +340,11 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     auto m0_of = [&](int j) { return m_start + (j % nqt) * 64; };
     u16x8 qreg[CPT], oreg[CPT];
     float lreg = 0.f, dreg = 0.f;
-    // DM: Q / dO tiles by LDS-DMA (no staging registers); only the row constants go through registers
+    // DM: Q / dO tiles by LDS-DMA through per-head buffer resources (no staging registers, no per-tile address
+    // VALU); only the row constants go through registers
     constexpr bool DM = DMA && !ROPE_IN;
     const int wu = __builtin_amdgcn_readfirstlane(w);
+    const DmaVoff<NW> qvo = dma_voff<NW>(ld_q, wu, l), ovo = dma_voff<NW>(ld_do, wu, l);
     auto load_tile = [&](int it) {
         const int m0 = m0_of(it);
         const __bf16* qb = q_of(it);
@@ -383,8 +388,8 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     if (nqt > 0) {
         load_tile(0);
         if constexpr (DM) {
-            dma_tile64<NW>(q_of(0), ld_q, m_start, S, Qs, wu, l);
-            dma_tile64<NW>(o_of(0), ld_do, m_start, S, dOs, wu, l);
+            dma_tile64_buf(q_of(0), head_bytes(ld_q, S, D), qvo, m_start, ld_q, Qs, wu);
+            dma_tile64_buf(o_of(0), head_bytes(ld_do, S, D), ovo, m_start, ld_do, dOs, wu);
         }
         write_tile(0, 0);
     }
@@ -403,8 +408,8 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
             if (it + 1 < nsteps) {
                 load_tile(it + 1);
                 if constexpr (DM) {  // buffer cur ^ 1 was last read in iteration it - 1, before its closing barrier
-                    dma_tile64<NW>(q_of(it + 1), ld_q, m0_of(it + 1), S, Qn, wu, l);
-                    dma_tile64<NW>(o_of(it + 1), ld_do, m0_of(it + 1), S, On, wu, l);
+                    dma_tile64_buf(q_of(it + 1), head_bytes(ld_q, S, D), qvo, m0_of(it + 1), ld_q, Qn, wu);
+                    dma_tile64_buf(o_of(it + 1), head_bytes(ld_do, S, D), ovo, m0_of(it + 1), ld_do, On, wu);
                 }
             }
             const float* lc = lseS + cur * 64;

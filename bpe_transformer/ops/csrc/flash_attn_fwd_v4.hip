@@ -94,11 +94,15 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     const int trow = 4 * hh + ((l & 15) >> 2);
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
-    // DMA: K / V tiles by LDS-DMA (fa_common.h dma_tile64; rows past the end arrive clamped and are masked below)
+    // DMA: K / V tiles by LDS-DMA through buffer resources (fa_common.h dma_tile64_buf; rows past the end read as 0
+    // and are masked below)
     const int wu = __builtin_amdgcn_readfirstlane(w);
+    // K and V share the row stride: one set of lane offsets and one extent serve both buffer resources
+    const int hbytes = head_bytes(ld_kv, S, D);
+    const DmaVoff<4> vo = dma_voff<4>(ld_kv, wu, l);
     if constexpr (DMA) {
-        dma_tile64<4>(kbase, ld_kv, 0, S, Ks, wu, l);
-        dma_tile64<4>(vbase, ld_kv, 0, S, Vs, wu, l);
+        dma_tile64_buf(kbase, hbytes, vo, 0, ld_kv, Ks, wu);
+        dma_tile64_buf(vbase, hbytes, vo, 0, ld_kv, Vs, wu);
     } else {
         load_tile(0);
         write_tile(0);
@@ -108,8 +112,8 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         const int cur = t & 1, n0 = t * 64;
         if (t + 1 < ntiles) {
             if constexpr (DMA) {  // buffer cur ^ 1 was last read in tile t - 1, before its closing barrier
-                dma_tile64<4>(kbase, ld_kv, n0 + 64, S, Ks + (cur ^ 1) * TILE, wu, l);
-                dma_tile64<4>(vbase, ld_kv, n0 + 64, S, Vs + (cur ^ 1) * TILE, wu, l);
+                dma_tile64_buf(kbase, hbytes, vo, n0 + 64, ld_kv, Ks + (cur ^ 1) * TILE, wu);
+                dma_tile64_buf(vbase, hbytes, vo, n0 + 64, ld_kv, Vs + (cur ^ 1) * TILE, wu);
             } else {
                 load_tile(t + 1);
             }

@@ -1,0 +1,10 @@
+# buffer-resource DMA (no per-tile address VALU) in the forward v7 and the split backward 44: tests + op-level A/B
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "flash" > gpurun_out/ab_tests.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/ab_tests.log; exit 1; }
+tail -1 gpurun_out/ab_tests.log
+timeout -k 10 300 python benchmarks/attn_bench.py --batch 128 --fwd-ab --fwd-versions 6 7 --rounds 7 2>&1 | grep shape | tee gpurun_out/ab_buf.log
+timeout -k 10 300 python benchmarks/attn_bench.py --batch 128 --bwd-ab --bwd-arms 4,4 44,44 --rounds 7 2>&1 | grep shape | tee -a gpurun_out/ab_buf.log
+timeout -k 10 300 python benchmarks/attn_bench.py --batch 32 --seq 2048 --heads 32 --kv-heads 4 --fwd-ab --fwd-versions 6 7 --bwd-ab --bwd-arms 4,4 44,44 --rounds 5 2>&1 | grep shape | tee -a gpurun_out/ab_buf.log
