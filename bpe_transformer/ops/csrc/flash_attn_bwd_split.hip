@@ -205,11 +205,13 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                     }
                     // P^T = exp2(S^T c - lse), dS^T = P^T (dP^T - delta); key = row of the accumulator, query = lane
                     if (need_mask) {
+                        // key k0 + 32 kh + acc_row(r, hh) is valid iff <= min(q, S - 1) (causal) / S - 1: the
+                        // per-lane limit against the register's compile-time row offset, one compare per score
+                        const int klim = (CAUSAL ? min(q, S - 1) : S - 1) - k0 - 32 * kh - 4 * hh;
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
-                            const int key = k0 + 32 * kh + acc_row(r, hh);
                             const float p = fast_exp2(sp[r]);
-                            const bool ok = key < S && (!CAUSAL || key <= q);
+                            const bool ok = (r & 3) + 8 * (r >> 2) <= klim;
                             dp[r] = ok ? p * dp[r] : 0.f;
                         }
                     } else {

@@ -130,13 +130,15 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                     s[kt] = mfma(lds_row16(Kc, swz<RB>(kt * 32 + l31, 2 * ks + hh)), qf[ks], s[kt]);
             }
             if ((CAUSAL && n0 + 63 > qw0) || (n0 + 64 > S)) {  // diagonal / ragged tile (wave-uniform)
+                // key n0 + 32 kt + acc_row(r, hh) is valid iff it is <= min(qrow, S - 1) (causal) / S - 1: one
+                // compare of the per-lane limit against the register's compile-time row offset (acc_row minus its
+                // lane-half term) and one select per score
+                const int qlim = (CAUSAL ? min(qrow, S - 1) : S - 1) - n0 - 4 * hh;
 #pragma unroll
                 for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int key = n0 + kt * 32 + acc_row(r, hh);
-                        if ((CAUSAL && key > qrow) || key >= S) s[kt][r] = -INFINITY;
-                    }
+                    for (int r = 0; r < 16; ++r)
+                        if ((r & 3) + 8 * (r >> 2) > qlim - 32 * kt) s[kt][r] = -INFINITY;
             }
             float mt = s[0][0];
 #pragma unroll
