@@ -26,8 +26,9 @@ namespace v4 {
 
 constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4, SPT = 2;  // SPT: 16-byte chunks per thread and tensor
 constexpr float THR = 8.0f;                                        // deferred-rescale threshold (log2 units)
+constexpr float TSUM = 256.0f;                                     // 2^THR: the MAXLESS form's P-sum threshold
 
-template <bool CAUSAL, int OCC = 2, bool DMA = false>
+template <bool CAUSAL, int OCC = 2, bool DMA = false, bool MAXLESS = false>
 __global__ void __launch_bounds__(256, OCC)
 fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                  long ld_q, long ld_kv, __bf16* __restrict__ O, long ld_o, float* __restrict__ LSE, int B, int H,
@@ -86,7 +87,7 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         lacc[r] = 0.f;
         nm[r] = 0.f;
     }
-    float m_run = 0.f;
+    float m_run = 0.f, lsum_t = 0.f;  // lsum_t: the row sum (MAXLESS)
     bf16x8 ones;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
@@ -140,6 +141,66 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                     for (int r = 0; r < 16; ++r)
                         if ((r & 3) + 8 * (r >> 2) > qlim - 32 * kt) s[kt][r] = -INFINITY;
             }
+            if constexpr (MAXLESS) {
+                // No tile max on the common path: P = exp2(S') is formed at once and its row sum taken by MFMA into
+                // a fresh accumulator; only a tile whose P sum exceeds 2^THR (some score more than ~THR above the
+                // running max, or inf / NaN) -- and the first tile -- takes the max, rescales, and forms P and its
+                // sum again, before any of this tile's P reaches O (guide T13 hazard).  Every P that reaches O is
+                // <= 2^THR, as with the max test.  Saves the ~20 max instructions and the lane exchange per tile.
+                bf16x8 pf[4];
+                auto exp_tile = [&]() {
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const int kt = kk >> 1, ss = kk & 1;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) pf[kk][j] = (__bf16)fast_exp2(s[kt][8 * ss + j]);
+                    }
+                };
+                auto tile_sum = [&]() {  // every register of the result holds the lane's row sum
+                    f32x16 lt = mfma(ones, pf[0], f32x16{});
+#pragma unroll
+                    for (int kk = 1; kk < 4; ++kk) lt = mfma(ones, pf[kk], lt);
+                    return lt[0];
+                };
+                float lt = 0.f;
+                if (t > 0) {
+                    exp_tile();
+                    lt = tile_sum();
+                }
+                const bool grow = t == 0 || !(lt <= TSUM);
+                if (!__all(!grow)) {
+                    float mt = s[0][0];
+#pragma unroll
+                    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kt][r]);
+                    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+                    const float d = grow ? mt : 0.f;
+                    const float alpha = t == 0 ? 0.f : fast_exp2(-d);
+                    m_run += d;
+                    lsum_t *= alpha;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        o[0][r] *= alpha;
+                        o[1][r] *= alpha;
+                        nm[r] = -m_run;
+                        s[0][r] -= d;
+                        s[1][r] -= d;
+                    }
+                    exp_tile();
+                    lt = tile_sum();
+                }
+                lsum_t += lt;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int kb = (kk >> 1) * 32 + 16 * (kk & 1);
+#pragma unroll
+                    for (int dt = 0; dt < 2; ++dt)
+                        o[dt] = mfma(lds_tr_pair(Vc, tr_off<RB>(kb + trow, dt * 32 + tcol),
+                                                 tr_off<RB>(kb + 8 + trow, dt * 32 + tcol)),
+                                     pf[kk], o[dt]);
+                }
+            } else {
             float mt = s[0][0];
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
@@ -180,6 +241,7 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                                  pf[kk], o[dt]);
                 lacc = mfma(ones, pf[kk], lacc);
             }
+            }
         }
         if (!DMA && t + 1 < ntiles) write_tile(cur ^ 1);
         __syncthreads();
@@ -187,7 +249,7 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 
     // ---- epilogue: O = O^T / l (query on the lane, 4 consecutive d per register group), LSE = m + log2 l
     if (qrow < S) {
-        const float lsum = lacc[0];
+        const float lsum = MAXLESS ? lsum_t : lacc[0];
         const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
         __bf16* op = O + ((long)b * S + qrow) * ld_o + (long)h * D;
 #pragma unroll
@@ -422,21 +484,22 @@ fa_fwd_pp_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 using namespace bpe;
 using namespace bpe::fa;
 
-// forward version for D = 64 without in-kernel RoPE: 7 (default: this file's kernel at 3 waves per SIMD with K / V
-// staged by LDS-DMA), 6 (the same with register staging), 4 (register staging at 2 waves per SIMD) or 2
-// (fa_fwd_kernel); BPE_FA_FWD sets the initial value, fa_fwd_config changes it at run time (A/B, tests).
-// Same box, op-level (profiles/bench/ab_attn_fwd_dma.log): GPT-2 B 128 0.342 / 0.356 / 0.362 ms for 7 / 6 / 4,
-// Llama GQA (8, 2048, 32, 4) 0.178 / 0.196 / 0.193 ms.
+// forward version for D = 64 without in-kernel RoPE: 8 (default: this file's kernel at 3 waves per SIMD, K / V
+// staged by LDS-DMA, no tile max on the common path), 7 (with the tile max), 6 (register staging), 4 (register
+// staging at 2 waves per SIMD) or 2 (fa_fwd_kernel); BPE_FA_FWD sets the initial value, fa_fwd_config changes it at
+// run time (A/B, tests).  Same box, op-level: GPT-2 B 128 0.342 / 0.356 / 0.362 ms for 7 / 6 / 4, Llama GQA
+// (8, 2048, 32, 4) 0.178 / 0.196 / 0.193 ms (profiles/bench/ab_attn_fwd_dma.log); 8 vs 7 0.314 vs 0.324 ms
+// (ab_attn_mask_maxless.log).
 static int g_fwd_ver = -1;
 
 // 2 (fa_fwd_kernel), 4 (fa_fwd_v4_kernel), 5 (fa_fwd_pp_kernel), 6 (fa_fwd_v4_kernel at 3 waves per SIMD: 162-168
-// VGPRs, no spills) or 7 (6 with LDS-DMA staging, 164-166 VGPRs; the default)
-static int fwd_ver_code(int v) { return (v == 2 || v == 4 || v == 5 || v == 6) ? v : 7; }
+// VGPRs, no spills), 7 (6 with LDS-DMA staging) or 8 (7 with the P-sum rescale test, MAXLESS; the default)
+static int fwd_ver_code(int v) { return (v == 2 || v == 4 || v == 5 || v == 6 || v == 7) ? v : 8; }
 
 int fa_fwd_config(int ver) {
     if (g_fwd_ver < 0) {
         const char* e = getenv("BPE_FA_FWD");
-        g_fwd_ver = fwd_ver_code(e ? atoi(e) : 7);
+        g_fwd_ver = fwd_ver_code(e ? atoi(e) : 8);
     }
     if (ver > 0) g_fwd_ver = fwd_ver_code(ver);
     return g_fwd_ver;
@@ -456,6 +519,8 @@ bool launch_fa_fwd_v4(const FaArgs& a, hipStream_t s) {
     const int nqb = (a.S + 127) / 128;
     auto* k = ver == 6   ? (a.causal ? &v4::fa_fwd_v4_kernel<true, 3> : &v4::fa_fwd_v4_kernel<false, 3>)
               : ver == 7 ? (a.causal ? &v4::fa_fwd_v4_kernel<true, 3, true> : &v4::fa_fwd_v4_kernel<false, 3, true>)
+              : ver == 8 ? (a.causal ? &v4::fa_fwd_v4_kernel<true, 3, true, true>
+                                     : &v4::fa_fwd_v4_kernel<false, 3, true, true>)
                          : (a.causal ? &v4::fa_fwd_v4_kernel<true> : &v4::fa_fwd_v4_kernel<false>);
     k<<<nqb * a.B * a.H, 256, 4 * v4::TILE, s>>>(a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.lse, a.B, a.H, a.Hkv,
                                                  a.S, a.scale * LOG2E, fa_group(a.B * a.H), a.dq_acc);

@@ -154,8 +154,8 @@ size_t fa_bwd_lds_bytes(int D);
 void launch_fa_fwd(const FaArgs& a, hipStream_t s);
 // flash_attn_fwd_v4.hip: the D = 64 forward without in-kernel RoPE; false when not applicable / not selected
 bool launch_fa_fwd_v4(const FaArgs& a, hipStream_t s);
-int fa_fwd_config(int ver);  // forward version for that case: 7 (default), 6, 5 (ping-pong), 4 or 2; ver <= 0 leaves it
-                             // unchanged
+int fa_fwd_config(int ver);  // forward version for that case: 8 (default), 7, 6, 5 (ping-pong), 4 or 2; ver <= 0 leaves
+                             // it unchanged
 void launch_fa_bwd(const FaArgs& a, hipStream_t s);
 // true when launch_fa_bwd takes the split form for head dim D (no fp32 dQ accumulator, no pre / convert passes)
 bool fa_bwd_split_active(int D);

@@ -511,11 +511,11 @@ def test_flash_attention_gpt2_shape(gpu_device):
 
 @pytest.mark.parametrize("S", [1024, 200, 64])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("ver", [2, 6, 7])
+@pytest.mark.parametrize("ver", [2, 6, 7, 8])
 def test_flash_fwd_versions_agree(gpu_device, S, causal, ver):
     """The D = 64 forward versions on pre-rotated Q / K: v2 (fa_fwd_kernel) and v6 (the v4 kernel at 3 waves per
-    SIMD) and v7 (the same with LDS-DMA K / V staging) against v4 -- O within bf16 rounding, v6 / v7 bitwise
-    (same math, other register budget / staging)."""
+    SIMD), v7 (the same with LDS-DMA K / V staging) and v8 (v7 without the tile max on the common path) against v4
+    -- O within bf16 rounding, v6 / v7 bitwise (same math, other register budget / staging)."""
     h = torch.ops.bpe_hip
     B, H, D = 2, 4, 64
     torch.manual_seed(5)
@@ -843,7 +843,7 @@ def test_accumulate_weight_grad_fp32_buffer(gpu_device):
     assert e32 < 1e-6 and e16 > 100 * e32, (e32, e16)
 
 
-@pytest.mark.parametrize("ver", [4, 5, 6, 7])
+@pytest.mark.parametrize("ver", [4, 5, 6, 7, 8])
 @pytest.mark.parametrize("S,H,Hkv,causal", [(1024, 4, 4, True), (200, 8, 2, True), (1000, 4, 4, False), (64, 2, 2, True),
                                             (600, 2, 2, True)])
 def test_flash_fwd_v4_matches_v2_and_oracle(gpu_device, S, H, Hkv, causal, ver):
