@@ -22,7 +22,6 @@ namespace fa {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef short v8s __attribute__((ext_vector_type(8)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 constexpr float LOG2E = 1.4426950408889634f;

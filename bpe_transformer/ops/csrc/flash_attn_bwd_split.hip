@@ -40,7 +40,8 @@ constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4;
 // staged 16-byte chunks per thread and tensor for one 64-row tile (512 chunks)
 template <int NW> constexpr int cpt() { return 512 / (NW * 64); }
 
-template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false>
+template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false,
+          int KTT = 64>
 __global__ void __launch_bounds__(NW * 64, OCC)
 fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                  long ld_q, long ld_kv, const __bf16* __restrict__ O, long ld_o, const __bf16* __restrict__ dO,
@@ -48,9 +49,13 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                  long ld_dq, const float* __restrict__ cosT, const float* __restrict__ sinT, int B, int H, int Hkv,
                  int S, float scale_log2, float scale, int group) {
     constexpr int NT = NW * 64, QB = 32 * NW, CPT = cpt<NW>();
+    // keys per K / V tile (one barrier each): KTT (64 or 128) with LDS-DMA staging, 64 with register staging; a
+    // 128-key tile is two 64-row images side by side
+    constexpr bool DM = DMA && !ROPE_IN;
+    constexpr int KT = DM ? KTT : 64, NSUB = KT / 64, BUF = NSUB * TILE;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* Ks = smem;             // [2][64 keys][128 B]  (roped K)
-    char* Vs = smem + 2 * TILE;  // [2][64 keys][128 B]
+    char* Ks = smem;            // [2][KT keys][128 B]  (roped K)
+    char* Vs = smem + 2 * BUF;  // [2][KT keys][128 B]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
     const int nqb = (S + QB - 1) / QB;
@@ -105,7 +110,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
 
     const int kend = CAUSAL ? min(S, q0 + QB) : S;
-    const int nkt = (kend + 63) / 64;
+    const int nkt = (kend + KT - 1) / KT;
     const __bf16* kb = K + (long)b * S * ld_kv + (long)hk * D;
     const __bf16* vb = Vv + (long)b * S * ld_kv + (long)hk * D;
     u16x8 kreg[CPT], vreg[CPT];
@@ -136,13 +141,15 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 
     // DM: K / V tiles by LDS-DMA through buffer resources (no staging registers, no per-tile address VALU; rows
     // past the end read as 0 and are masked below)
-    constexpr bool DM = DMA && !ROPE_IN;
     const int wu = __builtin_amdgcn_readfirstlane(w);
     const int hbytes = head_bytes(ld_kv, S, D);
     const DmaVoff<NW> kvo = dma_voff<NW>(ld_kv, wu, l);
     if constexpr (DM) {
-        dma_tile64_buf(kb, hbytes, kvo, 0, ld_kv, Ks, wu);
-        dma_tile64_buf(vb, hbytes, kvo, 0, ld_kv, Vs, wu);
+#pragma unroll
+        for (int sb = 0; sb < NSUB; ++sb) {
+            dma_tile64_buf(kb, hbytes, kvo, 64 * sb, ld_kv, Ks + sb * TILE, wu);
+            dma_tile64_buf(vb, hbytes, kvo, 64 * sb, ld_kv, Vs + sb * TILE, wu);
+        }
     } else {
         load_tile(0);
         write_tile(0, 0);
@@ -152,23 +159,30 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     const int trow = 4 * hh + ((l & 15) >> 2);          // tr-read row inside a 16-key step
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);  // tr-read column inside a 32-wide d tile
     for (int it = 0; it < nkt; ++it) {
-        const int cur = it & 1, k0 = it * 64;
+        const int cur = it & 1, k0 = it * KT;
         // the current and next buffers as __restrict__ parameters (see fa_bwd_dkv_kernel): no DMA drain mid-tile
         auto body = [&](char* __restrict__ Kc, const char* __restrict__ Vc, char* __restrict__ Kn,
                         char* __restrict__ Vn) {
             if (it + 1 < nkt) {
                 if constexpr (DM) {  // buffer cur ^ 1 was last read in iteration it - 1, before its closing barrier
-                    dma_tile64_buf(kb, hbytes, kvo, k0 + 64, ld_kv, Kn, wu);
-                    dma_tile64_buf(vb, hbytes, kvo, k0 + 64, ld_kv, Vn, wu);
+#pragma unroll
+                    for (int sb = 0; sb < NSUB; ++sb) {
+                        dma_tile64_buf(kb, hbytes, kvo, k0 + KT + 64 * sb, ld_kv, Kn + sb * TILE, wu);
+                        dma_tile64_buf(vb, hbytes, kvo, k0 + KT + 64 * sb, ld_kv, Vn + sb * TILE, wu);
+                    }
                 } else {
                     load_tile(it + 1);
                 }
             }
             if (!CAUSAL || k0 <= qw + 31) {
-                const bool need_mask = (CAUSAL && k0 + 63 > qw) || (k0 + 64 > S);
+                const bool need_mask = (CAUSAL && k0 + KT - 1 > qw) || (k0 + KT > S);
 #pragma unroll
-                for (int kh = 0; kh < 2; ++kh) {
-                    if (CAUSAL && k0 + 32 * kh > qw + 31) break;  // this 32-key half is past every query of the wave
+                for (int kq = 0; kq < KT / 32; ++kq) {
+                    if (CAUSAL && k0 + 32 * kq > qw + 31) break;  // this 32-key step is past every query of the wave
+                    // step kq: image kq / 2 of the tile, its 32-key half kh
+                    char* Kh = Kc + (kq >> 1) * TILE;
+                    const char* Vh = Vc + (kq >> 1) * TILE;
+                    const int kh = kq & 1;
                     f32x16 sp = ns, dp = nd;
                     bf16x8 tk[2][2];  // SCHED: the transposed K fragments of the dQ products (s, dt)
                     if constexpr (SCHED) {  // operand reads batched ahead of their uses (see fa_bwd_dkv_kernel)
@@ -176,8 +190,8 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 #pragma unroll
                         for (int ks = 0; ks < KS; ++ks) {
                             const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
-                            fk[ks] = lds_row16(Kc, koff);
-                            fv[ks] = lds_row16(Vc, koff);
+                            fk[ks] = lds_row16(Kh, koff);
+                            fv[ks] = lds_row16(Vh, koff);
                         }
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -191,7 +205,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 #pragma unroll
                             for (int dt = 0; dt < 2; ++dt) {
                                 const int kr = 32 * kh + 16 * s;
-                                tk[s][dt] = lds_tr_pair(Kc, tr_off<RB>(kr + trow, 32 * dt + tcol),
+                                tk[s][dt] = lds_tr_pair(Kh, tr_off<RB>(kr + trow, 32 * dt + tcol),
                                                         tr_off<RB>(kr + 8 + trow, 32 * dt + tcol));
                             }
                         __builtin_amdgcn_sched_barrier(0);
@@ -199,15 +213,15 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 #pragma unroll
                         for (int ks = 0; ks < KS; ++ks) {
                             const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
-                            sp = mfma(lds_row16(Kc, koff), qf[ks], sp);
-                            dp = mfma(lds_row16(Vc, koff), of[ks], dp);
+                            sp = mfma(lds_row16(Kh, koff), qf[ks], sp);
+                            dp = mfma(lds_row16(Vh, koff), of[ks], dp);
                         }
                     }
                     // P^T = exp2(S^T c - lse), dS^T = P^T (dP^T - delta); key = row of the accumulator, query = lane
                     if (need_mask) {
-                        // key k0 + 32 kh + acc_row(r, hh) is valid iff <= min(q, S - 1) (causal) / S - 1: the
+                        // key k0 + 32 kq + acc_row(r, hh) is valid iff <= min(q, S - 1) (causal) / S - 1: the
                         // per-lane limit against the register's compile-time row offset, one compare per score
-                        const int klim = (CAUSAL ? min(q, S - 1) : S - 1) - k0 - 32 * kh - 4 * hh;
+                        const int klim = (CAUSAL ? min(q, S - 1) : S - 1) - k0 - 32 * kq - 4 * hh;
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             const float p = fast_exp2(sp[r]);
@@ -230,7 +244,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                             if constexpr (SCHED)
                                 acc[dt] = mfma(tk[s][dt], db, acc[dt]);
                             else
-                                acc[dt] = mfma(lds_tr_pair(Kc, tr_off<RB>(kr + trow, 32 * dt + tcol),
+                                acc[dt] = mfma(lds_tr_pair(Kh, tr_off<RB>(kr + trow, 32 * dt + tcol),
                                                            tr_off<RB>(kr + 8 + trow, 32 * dt + tcol)),
                                                db, acc[dt]);
                         }
@@ -238,7 +252,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                 }
             }
         };
-        body(Ks + cur * TILE, Vs + cur * TILE, Ks + (cur ^ 1) * TILE, Vs + (cur ^ 1) * TILE);
+        body(Ks + cur * BUF, Vs + cur * BUF, Ks + (cur ^ 1) * BUF, Vs + (cur ^ 1) * BUF);
         if (!DM && it + 1 < nkt) write_tile(it + 1, cur ^ 1);
         __syncthreads();
     }
@@ -1036,19 +1050,20 @@ using namespace bpe::fa;
 // from BPE_FA_BWD ("fused" / "split"), changeable at run time (fa_bwd_config) for same-process A/B and tests.
 // Waves per workgroup of the two split kernels: BPE_FA_SPLIT_NW="<dq>,<dkv>", each 4 or 8 (the plain kernels with
 // register-staged tiles), 42 / 43 (4 waves, tiles staged by LDS-DMA, 2 / 3 waves per SIMD), 44 (42 with every
-// operand read of a half-step issued ahead of its MFMAs, SCHED), 82 (8 waves, LDS-DMA) or 2 (the ping-pong
-// kernels: 8 waves in two staggered groups).  Default 44,44.  Op-level, same box (profiles/bench/ab_attn_dma_occ.log,
+// operand read of a half-step issued ahead of its MFMAs, SCHED), 48 (dQ only: 44 with 128-key tiles, one barrier
+// per 128 keys), 82 (8 waves, LDS-DMA) or 2 (the ping-pong kernels: 8 waves in two staggered groups).  Default
+// 48,44 (48 vs 44: 1.159 vs 1.162 ms, Llama B 32 2.155 vs 2.173 ms; profiles/bench/ab_attn_dq128.log).  Op-level, same box (profiles/bench/ab_attn_dma_occ.log,
 // ab_attn_sched.log): LDS-DMA staging 1.178-1.204 vs 1.207-1.277 ms for 4,4 (GPT-2 B 128) and 0.666 vs 0.702 ms
 // (Llama GQA); the batched reads another -0.4-0.5 % (1.159 vs 1.164, 1.179 vs 1.185; Llama 0.649 vs 0.655).
 // Measured and dropped: 43 (168 VGPRs: 27-275 spilled, 2.5x slower), 82 (+10 %), a two-half software pipeline of
 // the dK/dV kernel (S/dP of half 1 under the softmax of half 0, sched_group_barrier 1 MFMA : 5 VALU; +2.3 %), the
 // ping-pong pair (+13-27 %, ab_attn_pp_b128.log).
-static int g_mode = -1, g_nw_dq = 44, g_nw_dkv = 44;
+static int g_mode = -1, g_nw_dq = 48, g_nw_dkv = 44;
 // GQA dK / dV: 1 = one workgroup per KV head sweeping its G query heads (the plain split kernels), 0 = one per query
 // head with fp32 partials summed by fa_dkv_reduce_kernel.  BPE_FA_GQA_LOOP sets it, fa_gqa_loop_config at run time.
 static int g_gqa_loop = 1;
 
-static int nw_code(int v) { return (v == 8 || v == 4 || v == 42 || v == 43 || v == 82 || v == 44) ? v : 2; }
+static int nw_code(int v) { return (v == 8 || v == 4 || v == 42 || v == 43 || v == 82 || v == 44 || v == 48) ? v : 2; }
 
 static void config_init() {
     if (g_mode >= 0) return;
@@ -1078,10 +1093,11 @@ int fa_bwd_config(int mode, int nw_dq, int nw_dkv) {
     return g_mode;
 }
 
-template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false>
+template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false, int KT = 64>
 static void dq_launch(const FaArgs& a, hipStream_t s) {
     const int nqb = (a.S + 32 * NW - 1) / (32 * NW);
-    split::fa_bwd_dq_kernel<C, R, RIN, NW, OCC, DMA, SCHED><<<nqb * a.B * a.H, NW * 64, 4 * split::TILE, s>>>(
+    const int lds = 4 * split::TILE * ((DMA && !RIN) ? KT / 64 : 1);
+    split::fa_bwd_dq_kernel<C, R, RIN, NW, OCC, DMA, SCHED, KT><<<nqb * a.B * a.H, NW * 64, lds, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do, a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin,
         a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
 }
@@ -1127,6 +1143,7 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
     else if (nq == 43) dq_launch<C, R, RIN, 4, 3, true>(a, s);
     else if (nq == 82) dq_launch<C, R, RIN, 8, 2, true>(a, s);
     else if (nq == 44) dq_launch<C, R, RIN, 4, 2, true, true>(a, s);
+    else if (nq == 48) dq_launch<C, R, RIN, 4, 2, true, true, 128>(a, s);
     else dq_launch<C, R, RIN, 4>(a, s);
     if (nk == 2) dkv_pp_launch<C, R, RIN>(a, s);
     else if (nk == 8) dkv_launch<C, R, RIN, 8>(a, s);
