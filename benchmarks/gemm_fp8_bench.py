@@ -23,9 +23,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--tokens", type=int, default=16384,
+                    help="M of the Llama shapes (16384 = s4096 B4; 65536 = s4096 B16, the bench default)")
     a = ap.parse_args()
     h = ops()
     for name, (M, N, K) in SHAPES.items():
+        if not name.startswith("gpt2"):
+            M = a.tokens
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
         fa = torch.float8_e5m2 if name.endswith("_dx") else torch.float8_e4m3fn  # dgrad: e5m2 gradient
