@@ -283,7 +283,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 }
 
 template <bool CAUSAL, bool ROPE, bool ROPE_IN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false,
-          bool LOOPG = false>
+          bool LOOPG = false, int QTT = 64>
 __global__ void __launch_bounds__(NW * 64, OCC)
 fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                   long ld_q, long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
@@ -291,11 +291,14 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
                   float* __restrict__ dKVpart, const float* __restrict__ cosT, const float* __restrict__ sinT, int B,
                   int H, int Hkv, int S, float scale_log2, float scale, int group) {
     constexpr int NT = NW * 64, KB = 32 * NW, CPT = cpt<NW>();
+    // queries per Q / dO tile (one barrier each): QTT (64 or 128) with LDS-DMA staging, 64 with register staging;
+    // a 128-query tile is two 64-row images side by side
+    constexpr int QT = (DMA && !ROPE_IN) ? QTT : 64, NSUB = QT / 64, BUF = NSUB * TILE;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* Qs = smem;                                             // [2][64 q][128 B]  (roped Q)
-    char* dOs = smem + 2 * TILE;                                 // [2][64 q][128 B]
-    float* lseS = reinterpret_cast<float*>(smem + 4 * TILE);     // [2][64]  -lse / c
-    float* dltS = lseS + 128;                                    // [2][64]  -delta
+    char* Qs = smem;                                            // [2][QT q][128 B]  (roped Q)
+    char* dOs = smem + 2 * BUF;                                 // [2][QT q][128 B]
+    float* lseS = reinterpret_cast<float*>(smem + 4 * BUF);     // [2][QT]  -lse / c
+    float* dltS = lseS + 2 * QT;                                // [2][QT]  -delta
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
     const int nkb = (S + KB - 1) / KB;
@@ -348,12 +351,12 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
         for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
 
     const int m_start = CAUSAL ? kb0 : 0;  // kb0 is a multiple of 64
-    const int nqt = m_start < S ? (S - m_start + 63) / 64 : 0;
+    const int nqt = m_start < S ? (S - m_start + QT - 1) / QT : 0;
     const int nsteps = GL * nqt;  // (query head, query tile) steps, head-major
     // step j: query head h + j / nqt, query tile j % nqt
     auto q_of = [&](int j) { return Q + (long)b * S * ld_q + (long)(h + j / nqt) * D; };
     auto o_of = [&](int j) { return dO + (long)b * S * ld_do + (long)(h + j / nqt) * D; };
-    auto m0_of = [&](int j) { return m_start + (j % nqt) * 64; };
+    auto m0_of = [&](int j) { return m_start + (j % nqt) * QT; };
     u16x8 qreg[CPT], oreg[CPT];
     float lreg = 0.f, dreg = 0.f;
     // DM: Q / dO tiles by LDS-DMA through per-head buffer resources (no staging registers, no per-tile address
@@ -366,7 +369,8 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
         const __bf16* qb = q_of(it);
         const __bf16* ob = o_of(it);
         const long sbase = ((long)b * H + h + it / nqt) * S;
-        const long idx = sbase + min(m0 + l, S - 1);  // every wave loads the stats (wave 0 writes them)
+        // every wave loads the stats of tile rows 64 (w & 1) + lane (waves 0 .. QT / 64 - 1 write them)
+        const long idx = sbase + min(m0 + (QT == 128 ? 64 * (w & 1) : 0) + l, S - 1);
         lreg = LSE[idx];
         dreg = DELTA[idx];
         if constexpr (!DM) {  // DM: the tile itself is DMA'd by the loop body (after these loads)
@@ -394,18 +398,21 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
             *reinterpret_cast<u16x8*>(Qs + buf * TILE + swz<RB>(r, c)) = qv;
             *reinterpret_cast<u16x8*>(dOs + buf * TILE + swz<RB>(r, c)) = ov;
         }
-        if (tid < 64) {  // the S / dP accumulators' starting values: -lse and -delta
+        if (tid < QT) {  // the S / dP accumulators' starting values: -lse and -delta
             const bool ok = m0 + tid < S;
-            lseS[buf * 64 + tid] = (!ok || lreg == INFINITY) ? -INFINITY : -lreg;
-            dltS[buf * 64 + tid] = ok ? -dreg : 0.f;
+            lseS[buf * QT + tid] = (!ok || lreg == INFINITY) ? -INFINITY : -lreg;
+            dltS[buf * QT + tid] = ok ? -dreg : 0.f;
         }
     };
 
     if (nqt > 0) {
         load_tile(0);
         if constexpr (DM) {
-            dma_tile64_buf(q_of(0), head_bytes(ld_q, S, D), qvo, m_start, ld_q, Qs, wu);
-            dma_tile64_buf(o_of(0), head_bytes(ld_do, S, D), ovo, m_start, ld_do, dOs, wu);
+#pragma unroll
+            for (int sb = 0; sb < NSUB; ++sb) {
+                dma_tile64_buf(q_of(0), head_bytes(ld_q, S, D), qvo, m_start + 64 * sb, ld_q, Qs + sb * TILE, wu);
+                dma_tile64_buf(o_of(0), head_bytes(ld_do, S, D), ovo, m_start + 64 * sb, ld_do, dOs + sb * TILE, wu);
+            }
         }
         write_tile(0, 0);
     }
@@ -424,17 +431,26 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
             if (it + 1 < nsteps) {
                 load_tile(it + 1);
                 if constexpr (DM) {  // buffer cur ^ 1 was last read in iteration it - 1, before its closing barrier
-                    dma_tile64_buf(q_of(it + 1), head_bytes(ld_q, S, D), qvo, m0_of(it + 1), ld_q, Qn, wu);
-                    dma_tile64_buf(o_of(it + 1), head_bytes(ld_do, S, D), ovo, m0_of(it + 1), ld_do, On, wu);
+#pragma unroll
+                    for (int sb = 0; sb < NSUB; ++sb) {
+                        dma_tile64_buf(q_of(it + 1), head_bytes(ld_q, S, D), qvo, m0_of(it + 1) + 64 * sb, ld_q,
+                                       Qn + sb * TILE, wu);
+                        dma_tile64_buf(o_of(it + 1), head_bytes(ld_do, S, D), ovo, m0_of(it + 1) + 64 * sb, ld_do,
+                                       On + sb * TILE, wu);
+                    }
                 }
             }
-            const float* lc = lseS + cur * 64;
-            const float* dc = dltS + cur * 64;
-            if (!CAUSAL || m0 + 63 >= kw0) {
-                const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + 64 > S) || (kw0 + 32 > S);
+            const float* lc = lseS + cur * QT;
+            const float* dc = dltS + cur * QT;
+            if (!CAUSAL || m0 + QT - 1 >= kw0) {
+                const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + QT > S) || (kw0 + 32 > S);
 #pragma unroll
-                for (int qt = 0; qt < 2; ++qt) {
-                    if (CAUSAL && m0 + 32 * qt + 31 < kw0) continue;  // every query of this half precedes every key
+                for (int qq = 0; qq < QT / 32; ++qq) {
+                    if (CAUSAL && m0 + 32 * qq + 31 < kw0) continue;  // every query of this step precedes every key
+                    // step qq: image qq / 2 of the tile, its 32-query half qt
+                    char* Qh = Qc + (qq >> 1) * TILE;
+                    char* Oh = Oc + (qq >> 1) * TILE;
+                    const int qt = qq & 1;
                     f32x16 sp, dp;
                     // every operand read of the half is issued before its first use (SCHED): the S / dP row
                     // fragments before the chains, the transposed dV / dK fragments before the softmax VALU, so
@@ -445,13 +461,13 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
 #pragma unroll
                         for (int ks = 0; ks < KS; ++ks) {
                             const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
-                            fq[ks] = lds_row16(Qc, off);
-                            fo[ks] = lds_row16(Oc, off);
+                            fq[ks] = lds_row16(Qh, off);
+                            fo[ks] = lds_row16(Oh, off);
                         }
                     }
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const int qi = qt * 32 + 8 * i + 4 * hh;  // rows qi..qi+3 of registers 4i..4i+3
+                        const int qi = qq * 32 + 8 * i + 4 * hh;  // rows qi..qi+3 of registers 4i..4i+3
                         const f32x4 lv = *reinterpret_cast<const f32x4*>(lc + qi);
                         const f32x4 dl = *reinterpret_cast<const f32x4*>(dc + qi);
 #pragma unroll
@@ -472,20 +488,20 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
                                 const int qr = qt * 32 + 16 * ss;
                                 const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
                                 const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
-                                to[ss][dt] = lds_tr_pair(Oc, o0, o1);
-                                tq[ss][dt] = lds_tr_pair(Qc, o0, o1);
+                                to[ss][dt] = lds_tr_pair(Oh, o0, o1);
+                                tq[ss][dt] = lds_tr_pair(Qh, o0, o1);
                             }
                         __builtin_amdgcn_sched_barrier(0);
                     } else {
 #pragma unroll
                         for (int ks = 0; ks < KS; ++ks) {
                             const int off = swz<RB>(qt * 32 + l31, 2 * ks + hh);
-                            sp = mfma(lds_row16(Qc, off), kf[ks], sp);
-                            dp = mfma(lds_row16(Oc, off), vf[ks], dp);
+                            sp = mfma(lds_row16(Qh, off), kf[ks], sp);
+                            dp = mfma(lds_row16(Oh, off), vf[ks], dp);
                         }
                     }
                     if (need_mask) {
-                        const int qoff = m0 + qt * 32 - klim;
+                        const int qoff = m0 + qq * 32 - klim;
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             const float p = fast_exp2(sp[r]);
@@ -518,15 +534,15 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
                             } else {
                                 const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
                                 const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
-                                dv[dt] = mfma(lds_tr_pair(Oc, o0, o1), pb, dv[dt]);
-                                dk[dt] = mfma(lds_tr_pair(Qc, o0, o1), db, dk[dt]);
+                                dv[dt] = mfma(lds_tr_pair(Oh, o0, o1), pb, dv[dt]);
+                                dk[dt] = mfma(lds_tr_pair(Qh, o0, o1), db, dk[dt]);
                             }
                         }
                     }
                 }
             }
         };
-        body(Qs + cur * TILE, dOs + cur * TILE, Qs + (cur ^ 1) * TILE, dOs + (cur ^ 1) * TILE);
+        body(Qs + cur * BUF, dOs + cur * BUF, Qs + (cur ^ 1) * BUF, dOs + (cur ^ 1) * BUF);
         if (it + 1 < nsteps) write_tile(it + 1, cur ^ 1);
         __syncthreads();
     }
@@ -1050,15 +1066,16 @@ using namespace bpe::fa;
 // from BPE_FA_BWD ("fused" / "split"), changeable at run time (fa_bwd_config) for same-process A/B and tests.
 // Waves per workgroup of the two split kernels: BPE_FA_SPLIT_NW="<dq>,<dkv>", each 4 or 8 (the plain kernels with
 // register-staged tiles), 42 / 43 (4 waves, tiles staged by LDS-DMA, 2 / 3 waves per SIMD), 44 (42 with every
-// operand read of a half-step issued ahead of its MFMAs, SCHED), 48 (dQ only: 44 with 128-key tiles, one barrier
-// per 128 keys), 82 (8 waves, LDS-DMA) or 2 (the ping-pong kernels: 8 waves in two staggered groups).  Default
-// 48,44 (48 vs 44: 1.159 vs 1.162 ms, Llama B 32 2.155 vs 2.173 ms; profiles/bench/ab_attn_dq128.log).  Op-level, same box (profiles/bench/ab_attn_dma_occ.log,
-// ab_attn_sched.log): LDS-DMA staging 1.178-1.204 vs 1.207-1.277 ms for 4,4 (GPT-2 B 128) and 0.666 vs 0.702 ms
-// (Llama GQA); the batched reads another -0.4-0.5 % (1.159 vs 1.164, 1.179 vs 1.185; Llama 0.649 vs 0.655).
+// operand read of a half-step issued ahead of its MFMAs, SCHED), 48 (44 with 128-key / 128-query tiles, one
+// barrier per 128 rows), 82 (8 waves, LDS-DMA) or 2 (the ping-pong kernels: 8 waves in two staggered groups).
+// Default 48,48.  Op-level, same box each: LDS-DMA staging 1.178-1.204 vs 1.207-1.277 ms for 4,4 (GPT-2 B 128)
+// and 0.666 vs 0.702 ms (Llama GQA) (profiles/bench/ab_attn_dma_occ.log); the batched reads another -0.4-0.5 %
+// (ab_attn_sched.log); 128-row tiles: dQ 1.159 vs 1.162 ms (ab_attn_dq128.log), dK/dV 1.168 vs 1.179 ms, Llama
+// B 32 2.159 vs 2.208 ms (ab_attn_dkv128.log).
 // Measured and dropped: 43 (168 VGPRs: 27-275 spilled, 2.5x slower), 82 (+10 %), a two-half software pipeline of
 // the dK/dV kernel (S/dP of half 1 under the softmax of half 0, sched_group_barrier 1 MFMA : 5 VALU; +2.3 %), the
 // ping-pong pair (+13-27 %, ab_attn_pp_b128.log).
-static int g_mode = -1, g_nw_dq = 48, g_nw_dkv = 44;
+static int g_mode = -1, g_nw_dq = 48, g_nw_dkv = 48;
 // GQA dK / dV: 1 = one workgroup per KV head sweeping its G query heads (the plain split kernels), 0 = one per query
 // head with fp32 partials summed by fa_dkv_reduce_kernel.  BPE_FA_GQA_LOOP sets it, fa_gqa_loop_config at run time.
 static int g_gqa_loop = 1;
@@ -1102,17 +1119,19 @@ static void dq_launch(const FaArgs& a, hipStream_t s) {
         a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
 }
 
-template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false>
+template <bool C, bool R, bool RIN, int NW, int OCC = 2, bool DMA = false, bool SCHED = false, int QT = 64>
 static void dkv_launch(const FaArgs& a, hipStream_t s) {
     const int nkb = (a.S + 32 * NW - 1) / (32 * NW);
+    const int qt = (DMA && !RIN) ? QT : 64;
+    const int lds = 4 * split::TILE * (qt / 64) + 16 * qt;  // Q / dO buffers + the -lse / -delta rows
     if (a.Hkv < a.H && g_gqa_loop) {  // GQA: one workgroup per KV head sweeps its query heads (no partials / reduce)
-        split::fa_bwd_dkv_kernel<C, R, RIN, NW, OCC, DMA, SCHED, true>
-            <<<nkb * a.B * a.Hkv, NW * 64, 4 * split::TILE + 1024, s>>>(
+        split::fa_bwd_dkv_kernel<C, R, RIN, NW, OCC, DMA, SCHED, true, QT>
+            <<<nkb * a.B * a.Hkv, NW * 64, lds, s>>>(
                 a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.dkv_part,
                 a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.Hkv));
         return;
     }
-    split::fa_bwd_dkv_kernel<C, R, RIN, NW, OCC, DMA, SCHED><<<nkb * a.B * a.H, NW * 64, 4 * split::TILE + 1024, s>>>(
+    split::fa_bwd_dkv_kernel<C, R, RIN, NW, OCC, DMA, SCHED, false, QT><<<nkb * a.B * a.H, NW * 64, lds, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.dkv_part, a.cos,
         a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
 }
@@ -1151,6 +1170,7 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
     else if (nk == 43) dkv_launch<C, R, RIN, 4, 3, true>(a, s);
     else if (nk == 82) dkv_launch<C, R, RIN, 8, 2, true>(a, s);
     else if (nk == 44) dkv_launch<C, R, RIN, 4, 2, true, true>(a, s);
+    else if (nk == 48) dkv_launch<C, R, RIN, 4, 2, true, true, 128>(a, s);
     else dkv_launch<C, R, RIN, 4>(a, s);
 }
 
