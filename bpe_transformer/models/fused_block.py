@@ -77,15 +77,18 @@ def _fuse_swiglu_bwd(dy: Tensor, w2: Tensor, gu: Tensor) -> bool:
 
 
 _FUSE_SWIGLU_FWD = os.environ.get("BPE_FUSE_SWIGLU_FWD", "1") == "1"
+_FUSE_SWIGLU_FWD_MAX_D = int(os.environ.get("BPE_FUSE_SWIGLU_FWD_MAX_D", "1024"))  # d_model cap (A/B knob)
 
 
 def _fuse_swiglu_fwd(x: Tensor, w13: Tensor) -> bool:
     """The W13 GEMM with a = silu(g) * u in its epilogue (csrc/gemm_pp.hip EPI_SWIGLU_FWD): tokens in multiples
     of 256, d_ff of 128, d_model of 64 up to 1024.  Past that the library GEMM's lead over the ping-pong kernel
-    outgrows the saved gate pass: GPT-2 (d 768) +0.7 % end to end, Llama-1.1B (d 2048) -1.2 %
-    (profiles/bench/ab_e2e_swiglu_fwd_fused_b128.log, ab_llama_swiglu_fwd_fused.log)."""
+    outgrows the saved gate pass: GPT-2 (d 768) +0.7 % end to end, Llama-1.1B (d 2048) -1.2 % at B 8 and -0.9 % at
+    B 32 (profiles/bench/ab_e2e_swiglu_fwd_fused_b128.log, ab_llama_swiglu_fwd_fused.log,
+    ab_llama_swiglu_fused_b32.log; ``BPE_FUSE_SWIGLU_FWD_MAX_D`` moves the cap for such A/Bs)."""
     return (_FUSE_SWIGLU_FWD and x.dtype == torch.bfloat16 and x.shape[0] % 256 == 0 and x.shape[1] % 64 == 0
-            and x.shape[1] <= 1024 and w13.shape[0] % 256 == 0 and x.stride(1) == 1 and w13.stride(1) == 1)
+            and x.shape[1] <= _FUSE_SWIGLU_FWD_MAX_D and w13.shape[0] % 256 == 0 and x.stride(1) == 1
+            and w13.stride(1) == 1)
 
 
 _DX_TN = os.environ.get("BPE_DX_TN", "1") == "1"
