@@ -103,7 +103,7 @@ def main():
                 ev[1].record()
                 torch.cuda.synchronize()
                 times[name].append(ev[0].elapsed_time(ev[1]) / a.iters)
-        hip.fa_bwd_config(prev, 48, 48)
+        hip.fa_bwd_config(prev, 48, 47)
         for name, t in times.items():
             t = sorted(t)
             print(json.dumps({"shape": [B, S, H, Hkv, D], "arm": name, "bwd_ms_median": round(t[len(t) // 2], 4),

@@ -1066,21 +1066,24 @@ using namespace bpe::fa;
 // from BPE_FA_BWD ("fused" / "split"), changeable at run time (fa_bwd_config) for same-process A/B and tests.
 // Waves per workgroup of the two split kernels: BPE_FA_SPLIT_NW="<dq>,<dkv>", each 4 or 8 (the plain kernels with
 // register-staged tiles), 42 / 43 (4 waves, tiles staged by LDS-DMA, 2 / 3 waves per SIMD), 44 (42 with every
-// operand read of a half-step issued ahead of its MFMAs, SCHED), 48 (44 with 128-key / 128-query tiles, one
-// barrier per 128 rows), 82 (8 waves, LDS-DMA) or 2 (the ping-pong kernels: 8 waves in two staggered groups).
-// Default 48,48.  Op-level, same box each: LDS-DMA staging 1.178-1.204 vs 1.207-1.277 ms for 4,4 (GPT-2 B 128)
-// and 0.666 vs 0.702 ms (Llama GQA) (profiles/bench/ab_attn_dma_occ.log); the batched reads another -0.4-0.5 %
-// (ab_attn_sched.log); 128-row tiles: dQ 1.159 vs 1.162 ms (ab_attn_dq128.log), dK/dV 1.168 vs 1.179 ms, Llama
-// B 32 2.159 vs 2.208 ms (ab_attn_dkv128.log).
+// operand read of a half-step issued ahead of its MFMAs, SCHED), 47 / 48 (42 / 44 with 128-key / 128-query tiles,
+// one barrier per 128 rows), 82 (8 waves, LDS-DMA) or 2 (the ping-pong kernels: 8 waves in two staggered groups).
+// Default 48,47 (the dK/dV kernel without the batched reads: 215 VGPRs instead of 256 with 2 spilled, and
+// 1.1437 vs 1.1465 ms for 48,48; ab_attn_sched128.log).  Op-level, same box each: LDS-DMA staging 1.178-1.204 vs
+// 1.207-1.277 ms for 4,4 (GPT-2 B 128) and 0.666 vs 0.702 ms (Llama GQA) (profiles/bench/ab_attn_dma_occ.log); the
+// batched reads another -0.4-0.5 % (ab_attn_sched.log); 128-row tiles: dQ 1.159 vs 1.162 ms (ab_attn_dq128.log),
+// dK/dV 1.168 vs 1.179 ms, Llama B 32 2.159 vs 2.208 ms (ab_attn_dkv128.log).
 // Measured and dropped: 43 (168 VGPRs: 27-275 spilled, 2.5x slower), 82 (+10 %), a two-half software pipeline of
 // the dK/dV kernel (S/dP of half 1 under the softmax of half 0, sched_group_barrier 1 MFMA : 5 VALU; +2.3 %), the
 // ping-pong pair (+13-27 %, ab_attn_pp_b128.log).
-static int g_mode = -1, g_nw_dq = 48, g_nw_dkv = 48;
+static int g_mode = -1, g_nw_dq = 48, g_nw_dkv = 47;
 // GQA dK / dV: 1 = one workgroup per KV head sweeping its G query heads (the plain split kernels), 0 = one per query
 // head with fp32 partials summed by fa_dkv_reduce_kernel.  BPE_FA_GQA_LOOP sets it, fa_gqa_loop_config at run time.
 static int g_gqa_loop = 1;
 
-static int nw_code(int v) { return (v == 8 || v == 4 || v == 42 || v == 43 || v == 82 || v == 44 || v == 48) ? v : 2; }
+static int nw_code(int v) {
+    return (v == 8 || v == 4 || v == 42 || v == 43 || v == 82 || v == 44 || v == 48 || v == 47) ? v : 2;
+}
 
 static void config_init() {
     if (g_mode >= 0) return;
@@ -1163,6 +1166,7 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
     else if (nq == 82) dq_launch<C, R, RIN, 8, 2, true>(a, s);
     else if (nq == 44) dq_launch<C, R, RIN, 4, 2, true, true>(a, s);
     else if (nq == 48) dq_launch<C, R, RIN, 4, 2, true, true, 128>(a, s);
+    else if (nq == 47) dq_launch<C, R, RIN, 4, 2, true, false, 128>(a, s);
     else dq_launch<C, R, RIN, 4>(a, s);
     if (nk == 2) dkv_pp_launch<C, R, RIN>(a, s);
     else if (nk == 8) dkv_launch<C, R, RIN, 8>(a, s);
@@ -1171,6 +1175,7 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
     else if (nk == 82) dkv_launch<C, R, RIN, 8, 2, true>(a, s);
     else if (nk == 44) dkv_launch<C, R, RIN, 4, 2, true, true>(a, s);
     else if (nk == 48) dkv_launch<C, R, RIN, 4, 2, true, true, 128>(a, s);
+    else if (nk == 47) dkv_launch<C, R, RIN, 4, 2, true, false, 128>(a, s);
     else dkv_launch<C, R, RIN, 4>(a, s);
 }
 
