@@ -22,15 +22,14 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-rope", action="store_true", help="plain attention (isolates the fused-RoPE cost)")
     ap.add_argument("--bwd-ab", action="store_true",
-                    help="interleaved same-process A/B of the backward forms: fused (atomics) and split at 4/8 "
-                         "waves per workgroup (ops.fa_bwd_config)")
+                    help="interleaved same-process A/B of the backward forms (ops.fa_bwd_config): fused (atomics) "
+                         "and split")
     ap.add_argument("--fwd-ab", action="store_true",
-                    help="interleaved same-process A/B of the D = 64 forward versions 2 (fa_fwd_kernel) and 4 "
+                    help="interleaved same-process A/B of the D = 64 forward versions 2 (fa_fwd_kernel) and 8 "
                          "(flash_attn_fwd_v4.hip) (ops.fa_fwd_config)")
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--fwd-versions", type=int, nargs="+", default=[2, 4, 5, 6])
-    ap.add_argument("--bwd-arms", nargs="+", default=None,
-                    help="subset of the --bwd-ab arms (names below, or dq,dkv codes like 42,42)")
+    ap.add_argument("--fwd-versions", type=int, nargs="+", default=[2, 8])
+    ap.add_argument("--bwd-arms", nargs="+", default=None, help="subset of the --bwd-ab arms (names below)")
     ap.add_argument("--mode", choices=["block", "fused"], default="block",
                     help="block = the training path (rope_qk_ in place, then pre-rotated kernels; rope time reported "
                          "separately and included in fwd_ms); fused = RoPE inside the attention kernels")
@@ -86,16 +85,15 @@ def main():
         if not a.bwd_ab:
             return
     if a.bwd_ab:
-        arms = {"fused": (1, 0, 0), "split4x4": (0, 4, 4), "split4x8": (0, 4, 8), "split8x4": (0, 8, 4),
-                "split4_ppdkv": (0, 4, 2), "split_pp_both": (0, 2, 2)}
-        if a.bwd_arms:  # names, or "dq,dkv" wave codes (42 / 43: LDS-DMA staging at 2 / 3 waves per SIMD)
-            arms = {n: (arms[n] if n in arms else (0, *map(int, n.split(",")))) for n in a.bwd_arms}
-        prev = hip.fa_bwd_config(-1, 0, 0)
+        arms = {"fused": 1, "split": 0}
+        if a.bwd_arms:
+            arms = {n: arms[n] for n in a.bwd_arms}
+        prev = hip.fa_bwd_config(-1)
         times = {k: [] for k in arms}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for _ in range(a.rounds):
             for name, cfg in arms.items():
-                hip.fa_bwd_config(*cfg)
+                hip.fa_bwd_config(cfg)
                 bwd(o, lse)
                 ev[0].record()
                 for _ in range(a.iters):
@@ -103,7 +101,7 @@ def main():
                 ev[1].record()
                 torch.cuda.synchronize()
                 times[name].append(ev[0].elapsed_time(ev[1]) / a.iters)
-        hip.fa_bwd_config(prev, 48, 47)
+        hip.fa_bwd_config(prev)
         for name, t in times.items():
             t = sorted(t)
             print(json.dumps({"shape": [B, S, H, Hkv, D], "arm": name, "bwd_ms_median": round(t[len(t) // 2], 4),

@@ -2,17 +2,17 @@
 
 One ``autograd.Function`` per transformer block instead of ~10 autograd nodes:
 
-forward::
+forward (x = xr + xd: the previous block's residual and its not-yet-added FFN output)::
 
-    h1 = rmsnorm(x; ln1)              HIP
-    qkv = h1 @ [Wq;Wk;Wv]^T           hipBLASLt (one GEMM)
+    x, h1 = add_rmsnorm(xr, xd; ln1)  HIP (the residual add fused into the norm)
+    qkv = h1 @ [Wq;Wk;Wv]^T           hipBLASLt (one GEMM; fp8: ops/fp8.py)
     rope_qk_(qkv)                     HIP, in place on Q / K (D = 64; D = 128 rotates inside attention)
-    o = flash_attn(qkv)               HIP
-    xm = x + o @ Wo^T                 hipBLASLt addmm (residual folded into the GEMM)
-    h2 = rmsnorm(xm; ln2)             HIP
-    gu = h2 @ [W1;W3]^T               hipBLASLt (one GEMM)
-    a = silu(g) * u                   HIP
-    y = xm + a @ W2^T                 hipBLASLt addmm
+    o = flash_attn(qkv)               HIP (csrc/flash_attn_fwd_v4.hip)
+    g1 = o @ Wo^T                     hipBLASLt
+    xm, h2 = add_rmsnorm(x, g1; ln2)  HIP
+    gu, a = h2 @ [W1;W3]^T, silu(g)*u our ping-pong GEMM with the gate in its epilogue (csrc/gemm_pp.hip,
+                                      d_model <= 1024; else hipBLASLt + the HIP gate kernel)
+    g2 = a @ W2^T                     hipBLASLt; the block returns (xm, g2), added by the next norm
 
 backward: the mirror image, with
   * the SwiGLU backward fused into the epilogue of the dY @ W2 GEMM (our
@@ -26,9 +26,11 @@ backward: the mirror image, with
   * both residual-gradient additions folded into the RMSNorm backward kernel;
   * a data-parallel "gradient ready" notification per parameter right after
     its gradient lands, so bucketed all-reduces start while the rest of the
-    backward runs;
-  * the weight-gradient GEMMs issued on a side stream (ops/streams.py), so
-    they overlap the serial input-gradient chain.
+    backward runs.
+
+Everything runs on the current stream.  (Weight-gradient GEMMs on a side stream were measured and removed:
+912 k vs 1 006 k tok/s at GPT-2 B 128, ``profiles/bench/ab_lmhead_chunk_dwstream_b128.log`` -- the chip is
+already full, so the two streams only compete for the same CUs.)
 
 Without ``main_grad`` (e.g. a plain module, tests) the same function returns
 ordinary per-parameter gradients.
@@ -42,7 +44,6 @@ import os
 import torch
 from torch import Tensor
 
-from ..ops import streams
 from ..ops._ext import ops as hip
 from ..ops.attention import prerotate_default
 from ..ops.gemm import accumulate_weight_grad
@@ -67,16 +68,13 @@ def _cat_weights(ts: list[Tensor]) -> Tensor:
     return v if v is not None else torch.cat([t.detach() for t in ts], 0)
 
 
-_FUSE_SWIGLU_BWD = os.environ.get("BPE_FUSE_SWIGLU_BWD", "1") == "1"
-
-
 def _fuse_swiglu_bwd(dy: Tensor, w2: Tensor, gu: Tensor) -> bool:
     """The fused dX-GEMM + SwiGLU-backward kernel covers tokens and d_ff in multiples of 256, d_model of 64."""
-    return (_FUSE_SWIGLU_BWD and dy.shape[0] % 256 == 0 and w2.shape[1] % 256 == 0 and dy.shape[1] % 64 == 0
+    return (dy.shape[0] % 256 == 0 and w2.shape[1] % 256 == 0 and dy.shape[1] % 64 == 0
             and gu.is_contiguous() and dy.stride(1) == 1 and w2.stride(1) == 1)
 
 
-_FUSE_SWIGLU_FWD = os.environ.get("BPE_FUSE_SWIGLU_FWD", "1") == "1"
+_FUSE_SWIGLU_FWD = True  # module flag (tests compare the unfused path)
 _FUSE_SWIGLU_FWD_MAX_D = int(os.environ.get("BPE_FUSE_SWIGLU_FWD_MAX_D", "1024"))  # d_model cap (A/B knob)
 
 
@@ -91,20 +89,13 @@ def _fuse_swiglu_fwd(x: Tensor, w13: Tensor) -> bool:
             and w13.stride(1) == 1)
 
 
-_DX_TN = os.environ.get("BPE_DX_TN", "1") == "1"
-
-# the attention forward zeroes the backward's fp32 dQ accumulator in its epilogue instead of the backward
-# pre-pass doing it (``BPE_FA_DQ_FWD_ZERO=0`` restores the pre-pass; docs/performance.md, attention)
-_DQ_FWD_ZERO = os.environ.get("BPE_FA_DQ_FWD_ZERO", "1") == "1"
-
-
 def _dx_tn(w: Tensor) -> bool:
     """Run dX = dY . W as dY . (W^T)^T with W^T materialised (``ops.transpose_bf16``): hipBLASLt's TN layout
     (both operands contiguous along the reduction) beats the NN layout of the stored weight by 10-20 % at the
     GPT-2 B 128 shapes, measured with tuned solutions on random data (benchmarks/gemm_layouts.py,
     profiles/bench/gemm_layouts_b128.log: qkv 0.359 vs 0.407 ms, o 0.138 vs 0.176, w13 0.606 vs 0.689); the
-    transpose is ~3-7 us per weight.  ``BPE_DX_TN=0`` keeps the NN call."""
-    return (_DX_TN and w.dtype == torch.bfloat16 and w.stride(1) == 1 and w.stride(0) % 8 == 0
+    transpose is ~3-7 us per weight."""
+    return (w.dtype == torch.bfloat16 and w.stride(1) == 1 and w.stride(0) % 8 == 0
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0)
 
 
@@ -119,7 +110,8 @@ class FusedBlockFn(torch.autograd.Function):
     def forward(ctx, xr, xd, ln1, wq, wk, wv, wo, ln2, w1, w3, w2, cos, sin, meta):
         B, S, H, Hkv, D, eps, use_rope = meta[:7]
         # fp8: (e4m3 Fp8State, first slot, e5m2 gradient Fp8State or None, first gradient slot) or None
-        fp8 = meta[7] if len(meta) > 7 else None
+        fp8 = meta[7]
+        train = meta[8]  # a backward will run (decided by the caller: grad mode is off inside forward)
         scale = 1.0 / math.sqrt(D)
         w_qkv = _cat_weights([wq, wk, wv])
         w_13 = _cat_weights([w1, w3])
@@ -151,12 +143,10 @@ class FusedBlockFn(torch.autograd.Function):
             hip().rope_qk_(qkv, cos, sin, B, S, H, Hkv, D)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         # training: the forward kernel zeroes the backward's fp32 dQ accumulator in its epilogue (hidden under
-        # its compute; the backward pre-pass then only reads O / dO)
-        # (only the fused atomics backward has that accumulator: D != 64 or BPE_FA_BWD=fused), and only when a
-        # backward will run
+        # its compute; the backward pre-pass then only reads O / dO).  Only the fused atomics backward has that
+        # accumulator (D != 64), and only when a backward will run.
         dq_acc = (torch.empty(B * ((S + 63) // 64 * 64), H * D, device=q.device, dtype=torch.float32)
-                  if _DQ_FWD_ZERO and torch.is_grad_enabled() and any(ctx.needs_input_grad)
-                  and hip().fa_bwd_needs_dq_acc(D) else None)
+                  if train and hip().fa_bwd_needs_dq_acc(D) else None)
         o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, pre, dq_acc)
         ctx.dq_acc = dq_acc
         g1 = mm(o, wo.detach(), 1) if fp8 is not None else torch.matmul(o, wo.t())
@@ -188,26 +178,19 @@ class FusedBlockFn(torch.autograd.Function):
         grads: dict[int, Tensor] = {}
 
         def acc_weight(ps: list[Tensor], g_out: Tensor, x_in: Tensor) -> None:
-            """dW = g_out^T x_in for the row-stacked weights ``ps`` (on the side stream: ops/streams.py)."""
+            """dW = g_out^T x_in for the row-stacked weights ``ps``, accumulated into their flat gradient slices."""
             if main:
-                def run():
-                    view = _adjacent_view([p.main_grad for p in ps])
-                    if view is not None:
-                        accumulate_weight_grad(view, g_out, x_in)
-                    else:
-                        off = 0
-                        for p in ps:
-                            n = p.shape[0]
-                            accumulate_weight_grad(p.main_grad, g_out[:, off : off + n], x_in)
-                            off += n
-                    for p in ps:
-                        _notify(p)
-
-                if streams.enabled(g_out):
-                    with streams.after_compute(g_out.device, keep=(g_out, x_in)):
-                        run()
+                view = _adjacent_view([p.main_grad for p in ps])
+                if view is not None:
+                    accumulate_weight_grad(view, g_out, x_in)
                 else:
-                    run()
+                    off = 0
+                    for p in ps:
+                        n = p.shape[0]
+                        accumulate_weight_grad(p.main_grad, g_out[:, off : off + n], x_in)
+                        off += n
+                for p in ps:
+                    _notify(p)
             else:
                 dw = torch.matmul(g_out.t(), x_in)
                 off = 0
@@ -216,7 +199,7 @@ class FusedBlockFn(torch.autograd.Function):
                     grads[id(p)] = dw[off : off + n]
                     off += n
 
-        fp8 = ctx.meta[7] if len(ctx.meta) > 7 else None
+        fp8 = ctx.meta[7]
         w8s = getattr(ctx, "w8s", None)
 
         def dx(g_out: Tensor, ws: list[Tensor], i: int) -> Tensor:
@@ -296,10 +279,9 @@ def fused_block_pair(block, xr: Tensor, xd: Tensor | None, B: int, S: int) -> tu
             _EMPTY[key] = torch.empty(0, 0, device=key, dtype=torch.float32)
         cos = sin = _EMPTY[key]
         use_rope = False
-    meta = (B, S, attn.num_heads, attn.num_kv_heads, attn.d_k, block.ln1.eps, use_rope)
-    fp8 = getattr(block, "fp8", None)
-    if fp8 is not None:
-        meta = meta + (fp8,)
+    train = torch.is_grad_enabled() and (xr.requires_grad or any(p.requires_grad for p in block.parameters()))
+    meta = (B, S, attn.num_heads, attn.num_kv_heads, attn.d_k, block.ln1.eps, use_rope, getattr(block, "fp8", None),
+            train)
     return FusedBlockFn.apply(xr, xd, block.ln1.weight, attn.q_proj.weight, attn.k_proj.weight,
                               attn.v_proj.weight, attn.output_proj.weight, block.ln2.weight, ffn.w1.weight,
                               ffn.w3.weight, ffn.w2.weight, cos, sin, meta)

@@ -10,7 +10,6 @@ their gradient.
 
 from __future__ import annotations
 
-import os
 
 import torch
 from torch import Tensor, nn
@@ -19,12 +18,9 @@ from .. import ops
 from .config import ModelConfig
 from .layers import Embedding, Linear, RMSNorm, TransformerBlock
 
-# GPU path: residual adds fused into the following RMSNorm across block boundaries (0 = per-block fallback,
-# for A/B measurements)
-_FUSED_STACK = os.environ.get("BPE_FUSED_STACK", "1") == "1"
 # LM-head rows padded (with zero rows, inside the flat parameter buffer) to a multiple of this, so the vocab
-# dimension of the head GEMMs and the logits row stride are aligned (0 = off)
-_VOCAB_PAD = int(os.environ.get("BPE_VOCAB_PAD", "256"))
+# dimension of the head GEMMs and the logits row stride are aligned (profiles/bench/lm_head_vocab_pad.log)
+_VOCAB_PAD = 256
 
 
 class TransformerLM(nn.Module):
@@ -115,7 +111,7 @@ class TransformerLM(nn.Module):
         if fence is not None:
             fence(self.token_embeddings)
         x = self.token_embeddings(in_indices)
-        if (_FUSED_STACK and len(self.layers) and x.dim() == 3
+        if (len(self.layers) and x.dim() == 3
                 and all(layer._fused_ok(x) for layer in self.layers)):
             from .fused_block import fused_stack_forward
 

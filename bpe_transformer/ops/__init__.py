@@ -10,7 +10,7 @@ training step is here.
 
 from ._ext import is_built, library_path, load
 from .activations import gelu, silu, swiglu_gate
-from .attention import attention_qkv_reference, flash_attention_qkv, flash_supported
+from .attention import attention_qkv_reference, flash_attention_qkv, flash_supported, scaled_dot_product_attention
 from .decode import decode_attention, kv_append
 from .embedding import embedding
 from .loss import IGNORE_INDEX, cross_entropy, lm_head_cross_entropy
@@ -38,6 +38,7 @@ __all__ = [
     "lm_head_cross_entropy",
     "load",
     "rmsnorm",
+    "scaled_dot_product_attention",
     "silu",
     "softmax",
     "swiglu_gate",

@@ -1,6 +1,9 @@
-"""Flash attention with fused RoPE (``csrc/flash_attn.hip``).
+"""Attention ops.
 
-``flash_attention_qkv`` consumes the output of the fused QKV projection
+``scaled_dot_product_attention``: the generic contract (K7, ``tests/adapters.py:92-110``) -- any leading dims, an
+arbitrary boolean mask -- on ``csrc/masked_sdpa.hip`` for GPU tensors (fp32 math), the oracle on the CPU.
+
+``flash_attention_qkv`` (the training path, ``csrc/flash_attn_*.hip``) consumes the output of the fused QKV projection
 ``[B*S, (H + 2*Hkv) * D]`` directly (no transposes, no separate RoPE pass) and
 returns ``[B*S, H*D]`` ready for the output projection; its backward returns
 the gradient in the same fused layout, feeding the QKV weight-gradient GEMM
@@ -31,9 +34,56 @@ def _empty(dev: torch.device) -> Tensor:
     return t
 
 
+class _MaskedSDPAFn(torch.autograd.Function):
+    """Forward on the HIP kernel; the backward (not on the training path: the model's attention is the flash
+    kernels') differentiates the oracle formula on the saved inputs."""
+
+    @staticmethod
+    def forward(ctx, q: Tensor, k: Tensor, v: Tensor, mask: Tensor | None, scale: float):
+        ctx.save_for_backward(q, k, v, mask)
+        ctx.scale = scale
+        return ops().masked_sdpa(q, k, v, mask, scale)
+
+    @staticmethod
+    def backward(ctx, do: Tensor):
+        q, k, v, mask = ctx.saved_tensors
+        with torch.enable_grad():
+            qf, kf, vf = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+            s = torch.matmul(qf, kf.transpose(-1, -2)) * ctx.scale
+            if mask is not None:
+                s = s.masked_fill(mask == 0, float("-inf"))
+            o = torch.matmul(torch.softmax(s, -1), vf)
+            dq, dk, dv = torch.autograd.grad(o, (qf, kf, vf), do.float())
+        return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), None, None
+
+
+def scaled_dot_product_attention(Q: Tensor, K: Tensor, V: Tensor, mask: Tensor | None = None,
+                                 scale: float | None = None) -> Tensor:
+    """``softmax(Q K^T * scale + (mask ? 0 : -inf)) V`` (scale 1/sqrt(d_k) by default) with any leading dims and a
+    boolean mask (True = attend) broadcastable to ``[..., q, k]``.  GPU fp32 / bf16 tensors run
+    ``csrc/masked_sdpa.hip`` (fp32 math, head dims up to 128); anything else the oracle formula."""
+    d_k = Q.shape[-1]
+    if not (Q.is_cuda and Q.dtype in (torch.float32, torch.bfloat16) and K.dtype == Q.dtype and V.dtype == Q.dtype
+            and d_k <= 128 and V.shape[-1] <= 128 and Q.shape[:-2] == K.shape[:-2] == V.shape[:-2]):
+        if scale is None:
+            return F.scaled_dot_product_attention(Q, K, V, mask)
+        s = torch.matmul(Q, K.transpose(-1, -2)) * scale
+        if mask is not None:
+            s = s.masked_fill(~mask, float("-inf"))
+        return torch.matmul(F.softmax(s, -1), V)
+    lead = Q.shape[:-2]
+    Sq, Sk = Q.shape[-2], K.shape[-2]
+    q, k, v = (t.reshape(-1, t.shape[-2], t.shape[-1]) for t in (Q, K, V))
+    m = None
+    if mask is not None:  # a view where the broadcast allows it (stride 0), else a copy
+        m = mask.to(device=Q.device).expand(*lead, Sq, Sk).reshape(-1, Sq, Sk)
+    o = _MaskedSDPAFn.apply(q, k, v, m, 1.0 / math.sqrt(d_k) if scale is None else scale)
+    return o.reshape(*lead, Sq, V.shape[-1])
+
+
 def prerotate_default(head_dim: int) -> bool:
     """Rotate Q / K once in the QKV activation (``rope_qk_``) instead of inside the attention kernels: the
-    D = 64 forward (v3) then stages K by LDS-DMA with no per-tile rotation.  ``BPE_ROPE_PREROTATE=0`` keeps the
+    D = 64 forward (v8) then stages K by LDS-DMA with no per-tile rotation.  ``BPE_ROPE_PREROTATE=0`` keeps the
     fused-RoPE kernels."""
     return head_dim == 64 and os.environ.get("BPE_ROPE_PREROTATE", "1") == "1"
 

@@ -8,8 +8,8 @@ with the source tree (no JIT cache, no site-packages install).
 
 Staleness is decided by CONTENT, not mtimes: every object records the sha256 of
 its compile command, its source and every header (``<obj>.sha``), and the linked
-library carries a stamp (``_bpe_hip.so.stamp``) with the digest of all sources,
-headers and flags.  ``_ext.load()`` recomputes that digest and refuses a library
+library carries a stamp (``_bpe_hip.so.stamp``, never committed) with the digest of all sources,
+headers and flags AND the sha256 of the library bytes it was written for.  ``_ext.load()`` recomputes that digest and refuses a library
 whose stamp does not match the tree (or rebuilds it with ``BPE_AUTOBUILD=1``), so a
 newer-but-stale ``.so`` shipped with a snapshot can never run in place of the
 sources next to it.
@@ -72,9 +72,16 @@ def stamp_path(lib: Path) -> Path:
     return lib.with_name(lib.name + ".stamp")
 
 
+def lib_sha(lib: Path) -> str:
+    return hashlib.sha256(lib.read_bytes()).hexdigest()
+
+
 def read_stamp(lib: Path) -> str | None:
+    """The source digest the library was built from, or None when there is no stamp or the stamp was written for
+    other library bytes (a stamp and a library that did not come out of one build)."""
     try:
-        return json.loads(stamp_path(lib).read_text())["digest"]
+        st = json.loads(stamp_path(lib).read_text())
+        return st["digest"] if st.get("lib_sha256") == lib_sha(lib) else None
     except (OSError, ValueError, KeyError):
         return None
 
@@ -147,15 +154,15 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False, v
         with cf.ThreadPoolExecutor(n) as ex:
             list(ex.map(compile_one, jobs_list))
     digest = source_digest(csrc, defines)
-    if force or jobs_list or not lib.exists() or read_stamp(lib) != digest:
+    if force or jobs_list or not lib.exists() or read_stamp(lib) != digest:  # (read_stamp checks the lib bytes)
         stamp_path(lib).unlink(missing_ok=True)
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(lib), *map(str, objs)]
         for d in libdirs:
             link += ["-L", d, f"-Wl,-rpath,{d}"]
         link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip"]
         _run(link, verbose)
-        stamp_path(lib).write_text(json.dumps({"digest": digest, "arch": ARCH, "defines": defines or [],
-                                               "src": str(csrc)}) + "\n")
+        stamp_path(lib).write_text(json.dumps({"digest": digest, "lib_sha256": lib_sha(lib), "arch": ARCH,
+                                               "defines": defines or [], "src": str(csrc)}) + "\n")
     return lib
 
 

@@ -117,18 +117,16 @@ __device__ __forceinline__ void softmax_ds(f32x16& sp, f32x16& dp, int hh, float
     }
 }
 
-// DBG (timing diagnostics, numerically wrong; built only with -DBPE_FA_DIAG): bit 1 = no dQ phase,
-// bit 2 = no softmax (P = S), bit 3 = no next-tile global loads, bit 4 = no dQ atomics.
 // ROPE: dK is un-rotated on output (and dQ by the convert kernel); ROPE_IN: Q / K are rotated on load too
 // (false when ops.rope_qk_ rotated them in the QKV activation already, rope mode 2).
-template <int D, bool CAUSAL, bool ROPE, int DBG = 0, bool ROPE_IN = ROPE>
+template <int D, bool CAUSAL, bool ROPE, bool ROPE_IN = ROPE>
 __global__ void __launch_bounds__(BwdCfg<D>::NW * 64, BwdCfg<D>::WGS)
 fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv, long ld_q,
               long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
               const float* __restrict__ DELTA, float* __restrict__ dQacc, __bf16* __restrict__ dK,
               __bf16* __restrict__ dV, long ld_dkv, float* __restrict__ dKVpart, const float* __restrict__ cosT,
               const float* __restrict__ sinT, int B, int H, int Hkv, int S, float scale_log2, float scale,
-              int flags, int group) {
+              int group) {
     using C = BwdCfg<D>;
     constexpr int NW = C::NW, NT = NW * 64, RB = C::RB, CPR = D / 8, QT = C::QT;
     constexpr int SPT = (64 * CPR + NT - 1) / NT;  // staged chunks per thread per tile (Q and dO each)
@@ -143,8 +141,6 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     float* dltS = lseS + 128;                                              // [2][64]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
-    // flags bit 0: static s_setprio 1 for the younger half of the waves (guide T5 static form; wave-uniform test)
-    if ((flags & 1) && __builtin_amdgcn_readfirstlane(tid >> 6) >= NW / 2) __builtin_amdgcn_s_setprio(1);
     // one workgroup per (key block, batch, QUERY head): with GQA the G query heads of a kv head run in
     // parallel (their dK / dV partials are summed by fa_dkv_reduce_kernel) instead of one workgroup sweeping
     // all G heads -- with causal masking that serial sweep left most CUs idle behind the key-block-0 groups.
@@ -243,7 +239,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
     auto body = [&](int it) {
         const int cur = C::QBUF == 2 ? (it & 1) : 0;
         const int m0 = m_start + it * 64;
-        if (it + 1 < total_it && !(DBG & 8)) load_tile(it + 1);
+        if (it + 1 < total_it) load_tile(it + 1);
         char* Qc = Qs + cur * QT;
         char* Oc = dOs + cur * QT;
         const float* lc = lseS + cur * 64;
@@ -274,8 +270,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
                 }
                 // P = exp2(S * scale*log2e - LSE2), dS = P * (dP - delta); diagonal / ragged tiles (wave-uniform
                 // test, scalar branch) zero P where (unsigned)(q - klim) >= span
-                if (DBG & 4) {
-                } else if (need_mask)
+                if (need_mask)
                     softmax_ds<true>(sp, dp, hh, scale_log2, m0 + qt * 32 - klim, span);
                 else
                     softmax_ds<false>(sp, dp, hh, scale_log2, 0, 0u);
@@ -316,7 +311,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
         //      of a wave share their query block, so the dS^T fragments are read once per 32-key step.
         //      dQacc rows are padded to a multiple of 64 per batch: rows q >= S of the last tile land in
         //      padding (carrying zeros: P = 0 there), so the atomics need no per-element guard.
-        if (!(DBG & 2)) {
+        {
             constexpr int DB = D / 16, TPW = 4 * DB / NW;
             const int t0 = w * TPW, qb = t0 / DB;
             f32x4 acc[TPW];
@@ -337,7 +332,7 @@ fa_bwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const 
             // unconditional (no runtime skip flag): a conditional atomic block makes the wait-count pass take
             // the count of the path WITHOUT the atomics at the join, i.e. vmcnt(1) / vmcnt(0) before the next
             // tile's LDS writes -- which drains these atomics (~600-3000 cycles) every query tile
-            if (!(DBG & 16)) {
+            {
                 const long HD = (long)H * D;
                 const int Spad = (S + 63) & ~63;
                 float* dqp = dQacc + ((long)b * Spad + m0 + qb * 16 + 4 * (l >> 4)) * HD + (long)h * D + (l & 15);
@@ -478,36 +473,18 @@ using namespace bpe::fa;
 
 size_t fa_bwd_lds_bytes(int D) { return D == 64 ? BwdCfg<64>::LDS : BwdCfg<128>::LDS; }
 
-// BPE_FA_BWD_PRIO (read once, default 0): static s_setprio 1 for waves NW/2.. of the backward kernel
-static int bwd_prio() {
-    static const int p = [] {
-        const char* e = getenv("BPE_FA_BWD_PRIO");
-        return e ? atoi(e) : 0;
-    }();
-    return p;
-}
-
-template <int D, bool C, bool R, int DBG, bool RIN>
-static void bwd_main_k(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
+template <int D, bool C, bool R, bool RIN>
+static void bwd_main_k(const FaArgs& a, hipStream_t s, int nkb) {
     using Cfg = BwdCfg<D>;
     static bool lds_attr = false;  // > 64 KiB of dynamic LDS: opt in once (before any graph capture)
     if (!lds_attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fa_bwd_kernel<D, C, R, DBG, RIN>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fa_bwd_kernel<D, C, R, RIN>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
         lds_attr = true;
     }
-    fa_bwd_kernel<D, C, R, DBG, RIN><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
+    fa_bwd_kernel<D, C, R, RIN><<<nkb * a.B * a.H, Cfg::NW * 64, Cfg::LDS, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dq_acc, a.dk, a.dv, a.ld_dkv,
-        a.dkv_part, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, (dbg << 1) | (bwd_prio() & 1),
-        fa_group(a.B * a.H));
-}
-
-template <int D, bool C, bool R, int DBG>
-static void bwd_main(const FaArgs& a, hipStream_t s, int nkb, int dbg) {
-    if (R && a.rope == 2)
-        bwd_main_k<D, C, R, DBG, false>(a, s, nkb, dbg);  // Q / K pre-rotated: only the outputs are rotated back
-    else
-        bwd_main_k<D, C, R, DBG, R>(a, s, nkb, dbg);
+        a.dkv_part, a.cos, a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
 }
 
 // stream non-temporally when a [tokens, H * D] bf16 activation is past 128 MB: GPT-2 B 128 (201 MB; its fp32 dQ
@@ -527,25 +504,12 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
         pre<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
             a.o, a.ld_o, a.dout, a.ld_do, a.delta, a.dq_zeroed ? nullptr : a.dq_acc, a.B, a.H, a.S, spad);
     }
-    constexpr int dbg = 0;
     {
         const int nkb = (a.S + Cfg::KB - 1) / Cfg::KB;
-#ifdef BPE_FA_DIAG
-        static const int diag = [] {
-            const char* e = getenv("BPE_FA_DIAG");
-            return e ? atoi(e) : 0;
-        }();
-        switch (diag) {
-            case 2: bwd_main<D, C, R, 2>(a, s, nkb, dbg); break;
-            case 4: bwd_main<D, C, R, 4>(a, s, nkb, dbg); break;
-            case 8: bwd_main<D, C, R, 8>(a, s, nkb, dbg); break;
-            case 14: bwd_main<D, C, R, 14>(a, s, nkb, dbg); break;
-            case 16: bwd_main<D, C, R, 16>(a, s, nkb, dbg); break;
-            default: bwd_main<D, C, R, 0>(a, s, nkb, dbg); break;
-        }
-#else
-        bwd_main<D, C, R, 0>(a, s, nkb, dbg);
-#endif
+        if (R && a.rope == 2)
+            bwd_main_k<D, C, R, false>(a, s, nkb);  // Q / K pre-rotated: only the outputs are rotated back
+        else
+            bwd_main_k<D, C, R, R>(a, s, nkb);
     }
     if (a.Hkv < a.H) {
         const long tkv = (long)a.B * a.S * a.Hkv * (D / 4);
@@ -557,18 +521,6 @@ static void bwd_launch(const FaArgs& a, hipStream_t s) {
     const int grid = (int)std::min<long>((total + 255) / 256, 4096);
     auto* conv = big_stream(a) ? &fa_dq_convert_kernel<D, R, true> : &fa_dq_convert_kernel<D, R, false>;
     conv<<<grid, 256, 0, s>>>(a.dq_acc, a.dq, a.ld_dq, a.cos, a.sin, a.B, a.H, a.S, a.scale);
-}
-
-void launch_fa_dkv_reduce(const FaArgs& a, hipStream_t s) {
-    const long tkv = (long)a.B * a.S * a.Hkv * (a.D / 4);
-    const int g2 = (int)std::min<long>((tkv + 255) / 256, 4096);
-    if (a.D != 64) return;
-    if (a.rope)
-        fa_dkv_reduce_kernel<64, true><<<g2, 256, 0, s>>>(a.dkv_part, a.dk, a.dv, a.ld_dkv, a.cos, a.sin, a.B, a.H,
-                                                            a.Hkv, a.S, a.scale);
-    else
-        fa_dkv_reduce_kernel<64, false><<<g2, 256, 0, s>>>(a.dkv_part, a.dk, a.dv, a.ld_dkv, a.cos, a.sin, a.B, a.H,
-                                                             a.Hkv, a.S, a.scale);
 }
 
 bool launch_fa_bwd_split(const FaArgs& a, hipStream_t s);  // flash_attn_bwd_split.hip

@@ -422,7 +422,7 @@ __device__ __forceinline__ void for_each_acc(const Acc<16>& acc, int l, F&& f) {
 }
 
 // NS = LDS stages (4 = 128 KiB, NS - 2 = 2 in flight while one is consumed; 5 = 160 KiB, the whole LDS, 3 in
-// flight: BPE_G256_STAGES=5)
+// flight; measured no faster)
 template <int MF, bool PRIO, int DSPLIT = 0, int NS = NSTAGE>
 __global__ void __launch_bounds__(NT, 1)
 gemm256_tn_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
@@ -530,37 +530,12 @@ static void launch_g256_v(const __bf16* a, long lda, const __bf16* b, long ldb, 
     k<<<grid, g256::NT, lds, s>>>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, prio);
 }
 
-// BPE_G256_STAGES (read once): 5 = the five-stage form of the default variant (160 KiB LDS, 3 stages in flight)
-static int g256_stages() {
-    static const int n = [] {
-        const char* e = getenv("BPE_G256_STAGES");
-        return (e && atoi(e) == 5) ? 5 : 4;
-    }();
-    return n;
-}
-
-// variant (BPE_G256_VARIANT, read once): bit 0 = 16x16x32 MFMA, bit 1 = setprio'd MFMA cluster, bit 2 / bit 3 =
-// the DMA split over the step in 2 / 4 places (32x32x16, overrides bits 0-1), bit 4 = static s_setprio 1 for
-// waves 4-7
+// The dW configuration: 32x32x16 MFMA, the DMA of a stage split over the 16-deep k-step in 2 places (+3-4 % over
+// one burst, profiles/bench/ab_dw_dma_split.log), 4 stages.  Measured and not kept: 16x16x32 MFMA and a setprio'd
+// MFMA cluster (+-3 %), the DMA split in 4 places (-7 %), a static s_setprio for waves 4-7 (+-0.3 %), 5 stages.
 static void launch_g256(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                         float beta, int Mo, int No, int R, int splits, hipStream_t s) {
-    static int variant = [] {  // default 4: +3-4 % over the one-burst DMA (profiles/bench/ab_dw_dma_split.log)
-        const char* e = getenv("BPE_G256_VARIANT");
-        return e ? atoi(e) : 4;
-    }();
-    const int pr = (variant >> 4) & 1;
-    if (variant & 8) return launch_g256_v<32, false, 2>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr);
-    if (variant & 4) {
-        if (g256_stages() == 5 && R / g256::BK / splits >= 4)
-            return launch_g256_v<32, false, 1, 5>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr);
-        return launch_g256_v<32, false, 1>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr);
-    }
-    switch (variant & 3) {
-        case 0: launch_g256_v<32, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;
-        case 1: launch_g256_v<16, false>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;
-        case 2: launch_g256_v<32, true>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;
-        default: launch_g256_v<16, true>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, pr); break;
-    }
+    launch_g256_v<32, false, 1>(a, lda, b, ldb, slab, c, ldc, beta, Mo, No, R, splits, s, 0);
 }
 
 void splitk_reduce(const float* slab, void* C, long ldc, float beta, int M, int N, int splits, int c_f32,

@@ -337,7 +337,7 @@ __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2
                                          0, 0);
 }
 
-// SPLIT (spread mode 2, BPE_GPP_SPREAD; the default for the weight-gradient layout): the second piece of each
+// SPLIT (spread mode 2, the weight-gradient layout): the second piece of each
 // pair is issued by the same wave in its MFMA section,
 // between the two halves of the quadrant, so a load section carries one piece; the waits become vmcnt(3).
 template <bool AK, bool BKM, int DIAG, bool SPLIT = false, int F8 = 0>
@@ -615,247 +615,28 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
 }
 
 
-// ---------------------------------------------------------------------------------------------------------
-// Persistent form (the default).  A/B builds showed where the one-tile-per-workgroup kernel loses to the
-// library on short reductions (K = 768: 12 K-tiles per tile): every workgroup waits for its first K-tile with
-// an empty pipeline, then all CUs store their 128 KiB tiles at the same moment (an HBM-bound burst that no
-// MFMA work overlaps).  Here one workgroup per CU walks its work items (tile, k-split) with stride gridDim.x;
-// the K-tile prefetch runs on across item boundaries (the next tile's first K-tile is DMA'd during the last
-// K-tile of the current one), and each group stores its finished accumulators straight from registers
-// (8-byte bf16 / 16-byte fp32 stores, merged into lines by the L2) at the start of its next load section, so
-// the stores drain while the next tile computes.  The K loop is the ping-pong loop above, unchanged.
-// (A 5-slot ring of 32-deep half-stages was also tried: 15-25 % slower.)
-// Measured (benchmarks/gemm_pp_bench.py --quick): without its output stores this form runs the K = 768 forward
-// GEMMs at 1.19-1.37 PF/s (one-tile-per-workgroup: 0.85-1.04); with them, 0.74-0.89 -- the 8-byte stores of
-// 32 accumulators per lane cost more than the overlap gains, so BPE_GPP_VER=2 selects it and 1 (the
-// one-tile-per-workgroup kernel with the LDS-staged 512-byte-row epilogue) is the default.
-namespace pers {
-
-struct Item {
-    int i0, j0, kb, nk, split;
-};
-
-__device__ __forceinline__ Item item_info(int it, int tiles_n, int ntiles, int nkt, int splits) {
-    Item r;
-    r.split = it / ntiles;
-    const int tile = it - r.split * ntiles;
-    const int ti = tile / tiles_n;
-    r.i0 = ti * BT;
-    r.j0 = (tile - ti * tiles_n) * BT;
-    r.kb = r.split * nkt / splits;  // split < 64, nkt < 2^20: 32-bit products
-    r.nk = (r.split + 1) * nkt / splits - r.kb;
-    return r;
-}
-
-struct Out {
-    __bf16* C;
-    float* slab;
-    long ldc;
-    int M, N;
-    float beta;
-};
-
-// Store accumulator quadrant (m, n) of item `it` -- row i = 128 g + 16 a + (l & 15), columns
-// 64 wl + 16 b + 4 (l >> 4) + r of register r (a = 4 m + ib, b = 2 n + jb).  Addresses: one wave-uniform
-// 64-bit tile base + a 32-bit per-lane offset (few live VGPRs: this runs beside a full accumulator file).
-template <bool SLAB>
-__device__ __forceinline__ void store_q(const f32x4 (&acc)[8][4], int m, int n, const Item& it, const Out& o, int g,
-                                        int wl, int l) {
-    const int ld = SLAB ? o.N : (int)o.ldc;
-    const int lane = (128 * g + (l & 15)) * ld + 64 * wl + 4 * (l >> 4);
-#pragma unroll
-    for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            const int a = 4 * m + ib, b = 2 * n + jb;
-            const int off = lane + a * 16 * ld + 16 * b;
-            f32x4 v = acc[a][b];
-            if constexpr (SLAB) {
-                float* base = o.slab + ((long)it.split * o.M + it.i0) * o.N + it.j0;
-                *reinterpret_cast<f32x4*>(base + off) = v;
-            } else {
-                __bf16* base = o.C + (long)it.i0 * o.ldc + it.j0;
-                // beta == 0 here: beta != 0 launches the one-tile-per-workgroup kernel
-                *reinterpret_cast<u16x4*>(base + off) = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-            }
-        }
-}
-
-// First K-tile of an item: MFMAs start from zero (no accumulator reset).  Phase 0 issues both halves of the next
-// K-tile's DMA FIRST and then stores the previous item's accumulators (32 stores per lane) before its MFMAs
-// overwrite them; phase 3 then waits for the DMA with vmcnt(32), leaving the 32 younger stores in flight
-// (vmcnt counts stores too, in issue order -- waiting on a DMA issued after the stores would wait for them).
-// (Spreading the stores over the four phases, one quadrant each, keeps old and new accumulators live together:
-// 60-150 spilled VGPRs.)
-__device__ __forceinline__ void mma_q_first(f32x4 (&acc)[8][4], const Frags& f, int m, int n) {
-#pragma unroll
-    for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            f32x4& c = acc[4 * m + ib][2 * n + jb];
-            c = mfma16(f.b[jb][0], f.a[ib][0], f32x4{0.f, 0.f, 0.f, 0.f});
-            c = mfma16(f.b[jb][1], f.a[ib][1], c);
-        }
-}
-
-template <bool AK, bool BKM, bool SLAB>
-__device__ __forceinline__ void ktile_first(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
-                                            const __bf16* an, const __bf16* bn, const int (&oa)[4],
-                                            const int (&ob)[4], int g, int wl, int l, f32x4 (&acc)[8][4],
-                                            bool has_prev, const Item& prev, const Out& o) {
-    Frags f;
-    char* Ac = cur;
-    char* Bc = cur + OPB;
-    if (dma) {
-        dma_half(an, oa, nxt, g, wl);
-        dma_half(bn, ob, nxt + OPB, g, wl);
-    }
-    if (has_prev) {
-        store_q<SLAB>(acc, 0, 0, prev, o, g, wl, l);
-        __builtin_amdgcn_sched_barrier(0);
-        store_q<SLAB>(acc, 0, 1, prev, o, g, wl, l);
-        __builtin_amdgcn_sched_barrier(0);
-        store_q<SLAB>(acc, 1, 1, prev, o, g, wl, l);
-        __builtin_amdgcn_sched_barrier(0);
-        store_q<SLAB>(acc, 1, 0, prev, o, g, wl, l);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    load_a<AK, BKM>(f, Ac, g, 0, l);
-    load_b<AK, BKM>(f, Bc, wl, 0, l);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    mma_q_first(acc, f, 0, 0);
-    bar();
-    load_b<AK, BKM>(f, Bc, wl, 1, l);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    mma_q_first(acc, f, 0, 1);
-    bar();
-    load_a<AK, BKM>(f, Ac, g, 1, l);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    mma_q_first(acc, f, 1, 1);
-    bar();
-    load_b<AK, BKM>(f, Bc, wl, 0, l);
-    if (has_prev)
-        asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    bar();
-    mma_q_first(acc, f, 1, 0);
-    bar();
-}
-
-template <bool AK, bool BKM, bool SLAB>
-__global__ void __launch_bounds__(NT, 1)
-gemm_pp_pers_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
-                    float* __restrict__ slab, __bf16* __restrict__ C, long ldc, float beta, int M, int N, int R,
-                    int splits) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, l = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = w >> 2, wl = w & 3;
-    const int G = gridDim.x;
-    // the workgroups of one XCD (blockIdx % 8) take consecutive work items in every round (T1)
-    const int wid = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);  // G % 8 == 0 (host)
-    const int tiles_n = N / BT;
-    const int ntiles = (M / BT) * tiles_n;
-    const int nitems = ntiles * splits;
-    const int nkt = R / BK;
-    if (wid >= nitems) return;  // wave-uniform: the whole workgroup
-    const Out o{C, slab, ldc, M, N, beta};
-
-    int oa[4], ob[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int e = g * 1024 + (wl * 4 + j) * 64 + l;
-        oa[j] = src_off<AK>(e, (int)lda);
-        ob[j] = src_off<BKM>(e, (int)ldb);
-    }
-    f32x4 acc[8][4];
-
-    int c = wid, st = 0;
-    Item ci = item_info(c, tiles_n, ntiles, nkt, splits);
-    Item prev = ci;
-    bool has_prev = false;
-    {
-        const long k0 = (long)ci.kb * BK;
-        dma_half(tile_ptr<AK>(A, lda, ci.i0, k0), oa, smem, g, wl);
-        dma_half(tile_ptr<BKM>(B, ldb, ci.j0, k0), ob, smem + OPB, g, wl);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bar();
-    }
-    if (g == 1) bar();  // the stagger
-    while (true) {
-        // the item's K-tiles; each prefetches its successor in this workgroup's sequence (across items)
-        const int nc = c + G;
-        const bool more = nc < nitems;
-        const Item ni = more ? item_info(nc, tiles_n, ntiles, nkt, splits) : ci;
-        for (int kt = 0; kt < ci.nk; ++kt) {
-            const bool last = kt + 1 == ci.nk;
-            const Item& di = last ? ni : ci;
-            const long k1 = (long)(di.kb + (last ? 0 : kt + 1)) * BK;
-            const bool dma = !last || more;
-            char* cur = smem + st * STAGE;
-            char* nxt = smem + (st ^ 1) * STAGE;
-            const __bf16* an = tile_ptr<AK>(A, lda, di.i0, k1);
-            const __bf16* bn = tile_ptr<BKM>(B, ldb, di.j0, k1);
-            if (kt == 0)
-                ktile_first<AK, BKM, SLAB>(cur, nxt, dma, an, bn, oa, ob, g, wl, l, acc, has_prev, prev, o);
-            else
-                ktile<AK, BKM, 0>(cur, nxt, dma, an, bn, oa, ob, g, wl, l, acc);
-            st ^= 1;
-        }
-        if (!more) break;
-        prev = ci;  // its tile is stored during the next item's first K-tile
-        has_prev = true;
-        c = nc;
-        ci = ni;
-    }
-    // the last item: all four quadrants
-    store_q<SLAB>(acc, 0, 0, ci, o, g, wl, l);
-    store_q<SLAB>(acc, 0, 1, ci, o, g, wl, l);
-    store_q<SLAB>(acc, 1, 1, ci, o, g, wl, l);
-    store_q<SLAB>(acc, 1, 0, ci, o, g, wl, l);
-    if (g == 0) bar();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-}  // namespace pers
+// (A persistent form -- one workgroup per CU walking its tiles with the K-tile prefetch running across tile seams
+// and the previous tile's accumulators stored from registers during the next tile -- ran the K = 768 forward GEMMs
+// at 1.19-1.37 PF/s without its output stores but 0.74-0.89 with them: the 8-byte stores of 32 accumulators per lane
+// cost more than the overlap gained.  It was removed; docs/performance.md, ping-pong GEMM.)
 }  // namespace gpp
 }  // namespace bpe
 
 using namespace bpe::gpp;
 
-// BPE_GPP_PRIO (read once, default 1): static s_setprio 1 for the younger wave group (end to end +0.1-0.6 %,
-// profiles/bench/ab_e2e_gpp_prio.log)
-static int prio_mode() {
-    static const int m = [] {
-        const char* e = getenv("BPE_GPP_PRIO");
-        return e ? atoi(e) : 1;
-    }();
-    return m;
-}
+// Static s_setprio 1 for the younger wave group: end to end +0.1-0.6 % (profiles/bench/ab_e2e_gpp_prio.log).
+static int prio_mode() { return 1; }
 
-// BPE_GPP_SPREAD (read once): 1 = the spread DMA schedule, 2 = spread with one piece per section moved into
-// the MFMA section, 0 = the burst schedule of ktile.  Unset: 2 for the weight gradient (both operands MN-major:
-// +1-3 %), 1 for the rest (2 is 3 % slower there; profiles/bench/ab_gpp_dma_split.log).
-static int spread_mode(bool weight_grad = false) {
-    static const int m = [] {
-        const char* e = getenv("BPE_GPP_SPREAD");
-        return e ? atoi(e) : -1;
-    }();
-    return m >= 0 ? m : (weight_grad ? 2 : 1);
-}
+// DMA schedule: 1 = the spread schedule (ktile_spread), 2 = spread with one piece per section moved into the MFMA
+// section: 2 for the weight gradient (both operands MN-major: +1-3 %), 1 for the rest (2 is 3 % slower there;
+// profiles/bench/ab_gpp_dma_split.log).  0, the burst schedule of ktile, serves the DIAG 5 build only.
+static int spread_mode(bool weight_grad = false) { return weight_grad ? 2 : 1; }
 
 // dgu = swiglu_bwd(dY . W2, gu): A = dY [M][R] (K-major), B = W2 [R][F] (MN-major)
 void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,
                                long ldg, int M, int F, int R, hipStream_t s) {
     static bool attr = false;
-    const int sm = spread_mode();
-    auto* k = sm == 2   ? &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, 2>
-              : sm == 1 ? &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, 1>
-                        : &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, 0>;
+    auto* k = &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, 1>;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr = true;
@@ -871,8 +652,7 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
 void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ldw, void* gu, long ldg, void* act,
                                long lda_, int M, int F, int R, hipStream_t s) {
     static bool attr = false;
-    auto* k = spread_mode() == 2 ? &gemm_pp_kernel<true, true, false, 0, EPI_SWIGLU_FWD, 2>
-                                 : &gemm_pp_kernel<true, true, false, 0, EPI_SWIGLU_FWD, 1>;
+    auto* k = &gemm_pp_kernel<true, true, false, 0, EPI_SWIGLU_FWD, 1>;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr = true;
@@ -935,53 +715,15 @@ static void launch_pp1(const __bf16* a, long lda, const __bf16* b, long ldb, flo
     launch_pp1s<AK, BKM, SLAB, DIAG, 0>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
 }
 
-template <bool AK, bool BKM, bool SLAB>
-static void launch_pers(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
-                        float beta, int M, int N, int R, int splits, hipStream_t s) {
-    static bool attr = false;
-    static int cus = 256;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)pers::gemm_pp_pers_kernel<AK, BKM, SLAB>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        int dev = 0, n = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        if (n >= 8) cus = n / 8 * 8;
-        attr = true;
-    }
-    const int items = (M / BT) * (N / BT) * splits;
-    const int grid = items < cus ? (items + 7) / 8 * 8 : cus;
-    pers::gemm_pp_pers_kernel<AK, BKM, SLAB><<<grid, NT, LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N,
-                                                                          R, splits);
-}
-
+// BPE_GPP_DIAG (a build define, ``python -m bpe_transformer.ops.build --variant diag -D BPE_GPP_DIAG=<n>``): the
+// timing diagnostics of ktile / ktile_spread (numerically wrong) in an A/B copy of the library
+#ifndef BPE_GPP_DIAG
+#define BPE_GPP_DIAG 0
+#endif
 template <bool AK, bool BKM, bool SLAB>
 static void launch_pp(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                       float beta, int M, int N, int R, int splits, hipStream_t s) {
-#ifdef BPE_GPP_DIAG
-    static int diag = [] {
-        const char* e = getenv("BPE_GPP_DIAG");
-        return e ? atoi(e) : 0;
-    }();
-#else
-    constexpr int diag = 0;
-#endif
-    static int ver = [] {
-        const char* e = getenv("BPE_GPP_VER");
-        return e ? atoi(e) : 1;
-    }();
-    if (ver == 2 && (SLAB || beta == 0.f)) return launch_pers<AK, BKM, SLAB>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
-    switch (diag) {
-#ifdef BPE_GPP_DIAG
-        case 1: launch_pp1<AK, BKM, SLAB, 1>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
-        case 2: launch_pp1<AK, BKM, SLAB, 2>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
-        case 3: launch_pp1<AK, BKM, SLAB, 3>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
-        case 4: launch_pp1<AK, BKM, SLAB, 4>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
-        case 5: launch_pp1<AK, BKM, SLAB, 5>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
-        case 6: launch_pp1<AK, BKM, SLAB, 6>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
-#endif
-        default: launch_pp1<AK, BKM, SLAB, 0>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s); break;
-    }
+    launch_pp1<AK, BKM, SLAB, BPE_GPP_DIAG>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
 }
 
 void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,

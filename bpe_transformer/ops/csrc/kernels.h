@@ -44,6 +44,11 @@ void launch_norm_finalize(const float* partial, int np, float max_norm, float* o
 void launch_scale(int dtype, void* x, size_t n, const float* coef, hipStream_t s);
 
 // softmax.hip
+// masked_sdpa.hip: the generic masked SDPA contract path (dtype: DT_F32 / DT_BF16; mask uint8, strides in bytes per
+// (batch-head, query, key), null = no mask)
+void launch_masked_sdpa(int dtype, const void* q, const void* k, const void* v, const uint8_t* mask, long msb,
+                        long msq, long msk, void* o, int BH, int Sq, int Sk, int D, int Dv, float scale,
+                        hipStream_t s);
 void launch_softmax_fwd(int dtype, const void* x, void* y, int M, int N, hipStream_t s);
 void launch_softmax_bwd(int dtype, const void* dy, const void* y, void* dx, int M, int N, hipStream_t s);
 
@@ -154,14 +159,12 @@ size_t fa_bwd_lds_bytes(int D);
 void launch_fa_fwd(const FaArgs& a, hipStream_t s);
 // flash_attn_fwd_v4.hip: the D = 64 forward without in-kernel RoPE; false when not applicable / not selected
 bool launch_fa_fwd_v4(const FaArgs& a, hipStream_t s);
-int fa_fwd_config(int ver);  // forward version for that case: 8 (default), 7, 6, 5 (ping-pong), 4 or 2; ver <= 0 leaves
-                             // it unchanged
+int fa_fwd_config(int ver);  // the D = 64 forward: 8 (default) or 2 (fa_fwd_kernel); ver <= 0 leaves it unchanged;
+                             // returns the version in force before the call
 void launch_fa_bwd(const FaArgs& a, hipStream_t s);
 // true when launch_fa_bwd takes the split form for head dim D (no fp32 dQ accumulator, no pre / convert passes)
 bool fa_bwd_split_active(int D);
-// backward form 0 split / 1 fused and the split kernels' waves per workgroup; negative / zero = unchanged
-int fa_bwd_config(int mode, int nw_dq, int nw_dkv);
-// GQA dK / dV of the split form: 1 = one workgroup per KV head sweeps its query heads, 0 = per-query-head fp32 partials
-// + fa_dkv_reduce_kernel; v < 0 leaves it unchanged.  fa_dkv_partials_needed: whether FaArgs::dkv_part must be set.
-int fa_gqa_loop_config(int v);
+// D = 64 backward form 0 split / 1 fused; negative = unchanged; returns the form in force before the call
+int fa_bwd_config(int mode);
+// whether FaArgs::dkv_part (GQA fp32 dK / dV partials of the fused backward) must be set
 bool fa_dkv_partials_needed(int D);

@@ -275,6 +275,42 @@ void scale_(at::Tensor x, const at::Tensor& coef) {
     launch_scale(dt_code(x), x.data_ptr(), x.numel(), coef.data_ptr<float>(), cur_stream());
 }
 
+// ---------------------------------------------------------------- generic masked SDPA (contract K7)
+// q [BH, Sq, D], k [BH, Sk, D], v [BH, Sk, Dv] (fp32 or bf16, one dtype); mask: bool / uint8 viewable as
+// [BH, Sq, Sk] with any strides (0 for broadcast dims), or None.  fp32 math; returns [BH, Sq, Dv] in q's dtype.
+at::Tensor masked_sdpa(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                       const c10::optional<at::Tensor>& mask, double scale) {
+    check_cuda(q, "q");
+    TORCH_CHECK(q.dim() == 3 && k.dim() == 3 && v.dim() == 3, "masked_sdpa: q / k / v must be [BH, S, D]");
+    TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type(),
+                "masked_sdpa: q, k, v must share a dtype");
+    const int64_t BH = q.size(0), Sq = q.size(1), D = q.size(2), Sk = k.size(1), Dv = v.size(2);
+    TORCH_CHECK(k.size(0) == BH && v.size(0) == BH && k.size(2) == D && v.size(1) == Sk,
+                "masked_sdpa: shape mismatch");
+    TORCH_CHECK(D >= 1 && D <= 128 && Dv >= 1 && Dv <= 128, "masked_sdpa: head dims must be 1..128");
+    TORCH_CHECK(BH <= 65535 && Sk >= 1, "masked_sdpa: at most 65535 batch-heads, at least one key");
+    auto qc = q.contiguous(), kc = k.contiguous(), vc = v.contiguous();
+    const uint8_t* mp = nullptr;
+    long msb = 0, msq = 0, msk = 0;
+    at::Tensor m;
+    if (mask.has_value() && mask->defined()) {
+        m = *mask;
+        TORCH_CHECK(m.dim() == 3 && m.size(0) == BH && m.size(1) == Sq && m.size(2) == Sk,
+                    "masked_sdpa: mask must be viewable as [BH, Sq, Sk]");
+        TORCH_CHECK(m.is_cuda() && m.device() == q.device(), "masked_sdpa: mask must be on q's device");
+        if (m.scalar_type() != at::kBool && m.scalar_type() != at::kByte) m = m.ne(0);
+        mp = reinterpret_cast<const uint8_t*>(m.data_ptr());
+        msb = m.stride(0);
+        msq = m.stride(1);
+        msk = m.stride(2);
+    }
+    DevGuard g(q.device());
+    auto o = at::empty({BH, Sq, Dv}, q.options());
+    launch_masked_sdpa(dt_code(qc), qc.data_ptr(), kc.data_ptr(), vc.data_ptr(), mp, msb, msq, msk, o.data_ptr(),
+                       (int)BH, (int)Sq, (int)Sk, (int)D, (int)Dv, (float)scale, cur_stream());
+    return o;
+}
+
 // ---------------------------------------------------------------- softmax
 at::Tensor softmax_fwd(const at::Tensor& x) {
     check_cuda(x, "x");
@@ -563,10 +599,7 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
 // whether fa_bwd uses (and fa_fwd should zero) the fp32 dQ accumulator for head dim D
 bool fa_bwd_needs_dq_acc(int64_t D) { return !fa_bwd_split_active((int)D); }
 int64_t fa_fwd_config_op(int64_t ver) { return fa_fwd_config((int)ver); }
-int64_t fa_gqa_loop_config_op(int64_t v) { return fa_gqa_loop_config((int)v); }
-int64_t fa_bwd_config_op(int64_t mode, int64_t nw_dq, int64_t nw_dkv) {
-    return fa_bwd_config((int)mode, (int)nw_dq, (int)nw_dkv);
-}
+int64_t fa_bwd_config_op(int64_t mode) { return fa_bwd_config((int)mode); }
 
 // Returns dqkv = [B*S, (H + 2*Hkv) * D]: dq | dk | dv in the fused QKV-projection layout.
 at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
@@ -831,6 +864,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("cast_fp8_t(Tensor w, Tensor scale, Tensor(a!) w8, Tensor(b!) w8t, Tensor(c!) amax_bits) -> ()");
     m.def("update_scales(Tensor(a!) amax_bits, Tensor(b!) hist, Tensor(c!) scale, Tensor(d!) inv_scale, int pos, "
           "float margin, int fmt=0) -> ()");
+    m.def("masked_sdpa(Tensor q, Tensor k, Tensor v, Tensor? mask, float scale) -> Tensor");
     m.def("softmax_fwd(Tensor x) -> Tensor");
     m.def("softmax_bwd(Tensor dy, Tensor y) -> Tensor");
     m.def("rope(Tensor x, Tensor pos, Tensor cos, Tensor sin, bool inverse) -> Tensor");
@@ -841,9 +875,8 @@ TORCH_LIBRARY(bpe_hip, m) {
           "Tensor? dq_acc=None) -> Tensor");
     m.def("rope_qk_(Tensor(a!) qkv, Tensor cos, Tensor sin, int B, int S, int H, int Hkv, int D) -> ()");
     m.def("fa_bwd_needs_dq_acc(int D) -> bool", &fa_bwd_needs_dq_acc);  // no tensors: a catch-all kernel
-    m.def("fa_bwd_config(int mode=-1, int nw_dq=0, int nw_dkv=0) -> int", &fa_bwd_config_op);
+    m.def("fa_bwd_config(int mode=-1) -> int", &fa_bwd_config_op);
     m.def("fa_fwd_config(int ver=0) -> int", &fa_fwd_config_op);
-    m.def("fa_gqa_loop_config(int v=-1) -> int", &fa_gqa_loop_config_op);
 }
 
 TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
@@ -870,6 +903,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("transpose_bf16", &transpose_bf16);
     m.impl("cast_fp8_t", &cast_fp8_t);
     m.impl("update_scales", &update_scales);
+    m.impl("masked_sdpa", &masked_sdpa);
     m.impl("softmax_fwd", &softmax_fwd);
     m.impl("softmax_bwd", &softmax_bwd);
     m.impl("rope", &rope);

@@ -22,8 +22,9 @@ from torch import Tensor
 
 from ._ext import ops
 
-_TARGET_WGS = int(os.environ.get("BPE_GEMM_TARGET_WGS", "512"))
-_ENABLED = os.environ.get("BPE_DW_GEMM", "1") == "1"
+# split-K target workgroups of the 128-tile kernel (256 / 768 / 1024 measured within noise of 512:
+# profiles/bench/ab_gemm_target_wgs_b128.log)
+_TARGET_WGS = 512
 
 
 def choose_splits(n: int, k: int, t: int, target: int = _TARGET_WGS, min_iters: int = 8) -> int:
@@ -39,8 +40,7 @@ def choose_splits(n: int, k: int, t: int, target: int = _TARGET_WGS, min_iters: 
     return best
 
 
-_MAX_TILES = int(os.environ.get("BPE_DW_GEMM_MAX_TILES", "160"))
-_TILE256 = os.environ.get("BPE_GEMM_TILE256", "1") == "1"
+_MAX_TILES = 160  # the 128-tile kernel's output-tile cap (256 measured the same: ab_gemm_target_wgs_b128.log)
 _CUS = 256
 
 
@@ -67,7 +67,7 @@ def choose_splits_256(n: int, k: int, t: int) -> int:
 
 
 def use_tile256(n: int, k: int, t: int) -> bool:
-    return _TILE256 and n % 256 == 0 and k % 256 == 0 and t % 256 == 0
+    return n % 256 == 0 and k % 256 == 0 and t % 256 == 0
 
 
 def supported(n: int, k: int, t: int) -> bool:
@@ -117,10 +117,7 @@ def choose_splits_pp(n: int, k: int, t: int, cus: int = _CUS) -> int:
 
 
 def use_pp(n: int, k: int, t: int) -> bool:
-    return _PP and n % 256 == 0 and k % 256 == 0 and t % 64 == 0
-
-
-_PP = os.environ.get("BPE_GEMM_PP", "1") == "1"
+    return n % 256 == 0 and k % 256 == 0 and t % 64 == 0
 
 
 def _candidates(n: int, k: int, t: int) -> list[str]:
@@ -213,7 +210,7 @@ def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
     """
     n, k = g.shape
     t = dy.shape[0]
-    ok = (_ENABLED and g.is_cuda and g.dtype in (torch.bfloat16, torch.float32) and dy.dtype == torch.bfloat16
+    ok = (g.is_cuda and g.dtype in (torch.bfloat16, torch.float32) and dy.dtype == torch.bfloat16
           and x.dtype == torch.bfloat16 and g.stride(1) == 1 and dy.stride(1) == 1 and x.stride(1) == 1)
     if not ok:
         _blas_acc(g, dy, x)

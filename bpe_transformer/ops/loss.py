@@ -52,13 +52,13 @@ def default_lmhead_mode() -> str:
 
 STREAMED_DEFAULT_CHUNK = 16384
 
-_HEAD_DX_TN = os.environ.get("BPE_HEAD_DX_TN", "1") == "1"
+_HEAD_DX_TN = True  # module flag (tests compare the NN call)
 
 
 def _head_dx(dlogits: Tensor, w: Tensor) -> Tensor:
     """dh = dlogits @ W in hipBLASLt's TN layout through a transposed copy of W (``ops.transpose_bf16``, as the
     blocks' input gradients do: models/fused_block.py ``_dx_tn``): 7.24 vs 8.27 ms at GPT-2 B 128 with tuned
-    solutions (profiles/bench/head_dx_layouts_b128.log), +0.65 % end to end.  ``BPE_HEAD_DX_TN=0`` keeps NN."""
+    solutions (profiles/bench/head_dx_layouts_b128.log), +0.65 % end to end."""
     if (_HEAD_DX_TN and w.dtype == torch.bfloat16 and dlogits.is_cuda and w.stride(1) == 1
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0):
         return torch.matmul(dlogits, ops().transpose_bf16(w).t())
@@ -109,20 +109,12 @@ class _LMHeadCEFn(torch.autograd.Function):
             return dh, torch.matmul(dlogits.t(), hs)[: ctx.w_param.shape[0]], None, None, None
         if mg is not None:
             # weight gradient accumulated in place into the flat gradient buffer (no temporary, no grad add)
-            from . import streams
             from .gemm import accumulate_weight_grad
 
-            def run():
-                accumulate_weight_grad(mg, dlogits, hs)
-                cb = getattr(ctx.w_param, "_bpe_grad_ready", None)
-                if cb is not None:
-                    cb(ctx.w_param)
-
-            if streams.enabled(hs):  # overlaps the blocks' backward (side stream, ordered: ops/streams.py)
-                with streams.after_compute(hs.device, keep=(dlogits, hs)):
-                    run()
-            else:
-                run()
+            accumulate_weight_grad(mg, dlogits, hs)
+            cb = getattr(ctx.w_param, "_bpe_grad_ready", None)
+            if cb is not None:
+                cb(ctx.w_param)
             return dh, None, None, None, None
         return dh, torch.matmul(dlogits.t(), hs), None, None, None
 
@@ -202,6 +194,25 @@ def cross_entropy(logits: Tensor, targets: Tensor, ignore_index: int = IGNORE_IN
     return F.cross_entropy(x[valid], t[valid])
 
 
+@torch.no_grad()
+def _lm_head_ce_loss_only(h: Tensor, w: Tensor, targets: Tensor, ignore_index: int, chunk: int) -> Tensor:
+    V = w.shape[0]
+    wp = getattr(w, "_bpe_padded", None)
+    if wp is None or wp.data_ptr() != w.data_ptr():
+        wp = w
+    M = h.shape[0]
+    chunk = min(chunk, M)
+    nvalid = (targets != ignore_index).sum().clamp_min(1).to(torch.float32)
+    buf = h.new_empty(chunk, wp.shape[0])
+    total = torch.zeros((), device=h.device, dtype=torch.float32)
+    for c0 in range(0, M, chunk):
+        c1 = min(M, c0 + chunk)
+        lg = buf[: c1 - c0]
+        torch.matmul(h[c0:c1], wp.t(), out=lg)
+        total += ops().ce_fwd_bwd(lg[:, :V], targets[c0:c1], ignore_index, False, nvalid)[0].sum()
+    return total / nvalid
+
+
 def lm_head_cross_entropy(h: Tensor, weight: Tensor, targets: Tensor, ignore_index: int = IGNORE_INDEX,
                           chunk: int | None = None, mode: str | None = None) -> Tensor:
     """``cross_entropy(h @ weight.T, targets)`` without keeping separate logits/probs/grad buffers.
@@ -215,6 +226,11 @@ def lm_head_cross_entropy(h: Tensor, weight: Tensor, targets: Tensor, ignore_ind
     d = h.shape[-1]
     h2 = h.reshape(-1, d)
     t = targets.reshape(-1).long().contiguous()
+    if h.is_cuda and h.dtype == torch.bfloat16 and not (
+            torch.is_grad_enabled() and (h.requires_grad or weight.requires_grad)):
+        # no backward will run (evaluation / validation loss): loss only, chunk by chunk through one reused
+        # buffer -- neither the full logits of "logits" mode nor the dh / dW work of "streamed" mode
+        return _lm_head_ce_loss_only(h2, weight, t, ignore_index, int(chunk or STREAMED_DEFAULT_CHUNK))
     if h.is_cuda and h.dtype == torch.bfloat16 and mode == "streamed":
         return _LMHeadCEStreamedFn.apply(h2, weight, t, ignore_index, int(chunk or STREAMED_DEFAULT_CHUNK))
     if chunk is None:

@@ -30,7 +30,6 @@ from contextlib import contextmanager
 import torch
 import torch.distributed as dist
 
-from ..ops import streams
 from ..optim.flat import FlatParameters
 
 
@@ -100,16 +99,12 @@ class BucketedAllReduce:
         s, e = self.buckets[b]
         view = self.flat.grad[s:e]
         if self._cbuf is not None:
-            self._cbuf[s:e].copy_(view)  # on the stream that produced the gradients: ordered after them
+            # every gradient is produced on the current (compute) stream, so this copy -- and the collective,
+            # which RCCL orders after the current stream -- follow all writes to the bucket
+            self._cbuf[s:e].copy_(view)
             view = self._cbuf[s:e]
         op = dist.ReduceOp.AVG if (self.average and self._use_avg) else dist.ReduceOp.SUM
-        if view.is_cuda and streams.enabled(view):
-            # weight gradients may be written on the side stream (ops/streams.py): issue the collective from
-            # there, after it waited for the compute stream, so it is ordered after both streams' writes
-            with streams.after_compute(view.device):
-                self._works[b] = dist.all_reduce(view, op=op, group=self.pg, async_op=True)
-        else:
-            self._works[b] = dist.all_reduce(view, op=op, group=self.pg, async_op=True)
+        self._works[b] = dist.all_reduce(view, op=op, group=self.pg, async_op=True)
 
     # -- step API ----------------------------------------------------------
     def start(self) -> None:

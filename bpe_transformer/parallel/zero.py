@@ -37,7 +37,6 @@ import torch
 import torch.distributed as dist
 from torch import Tensor, nn
 
-from ..ops import streams
 from ..ops.optim import grad_norm
 from ..optim.flat import ALIGN, FlatAdamW, FlatParameters
 
@@ -111,11 +110,7 @@ class ShardedDataParallel:
                                                   group=self.pg, async_op=True)
             return dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
-        if full.is_cuda and streams.enabled(full):
-            with streams.after_compute(full.device):  # ordered after side-stream weight-gradient writes
-                self._rs[b] = issue()
-        else:
-            self._rs[b] = issue()
+        self._rs[b] = issue()
 
     def start(self) -> None:
         """Call before each backward that should reduce."""

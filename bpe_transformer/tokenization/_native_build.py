@@ -3,8 +3,8 @@
 ``python -m bpe_transformer.tokenization._native_build`` compiles
 ``csrc/tokenizer/bpe_native.cpp`` with g++ (-O3, C++20, pthreads) into
 ``bpe_transformer/tokenization/_bpe_native<ext-suffix>``.  Incremental by CONTENT:
-the library carries a stamp (``<lib>.stamp``) with the sha256 of the compile
-command and every source / header; a mismatch (sources edited, whatever their
+the library carries a stamp (``<lib>.stamp``, untracked) with the sha256 of the compile
+command and every source / header, and of the library bytes themselves; a mismatch (sources edited, whatever their
 mtimes) rebuilds, and ``_native.py`` checks the stamp before importing.
 """
 
@@ -47,10 +47,17 @@ def digest() -> str:
     return h.hexdigest()
 
 
+def _lib_sha() -> str:
+    return hashlib.sha256(LIB.read_bytes()).hexdigest()
+
+
 def is_fresh() -> bool:
+    """The stamp (never committed: .gitignore) names both the source digest and the sha256 of the library bytes it
+    was written for, so a library and a stamp that did not come out of one build never pass together."""
     try:
-        return LIB.exists() and STAMP.read_text().strip() == digest()
-    except OSError:
+        src, lib = STAMP.read_text().split()
+        return LIB.exists() and src == digest() and lib == _lib_sha()
+    except (OSError, ValueError):
         return False
 
 
@@ -65,7 +72,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("building the native tokenizer failed")
-    STAMP.write_text(digest() + "\n")
+    STAMP.write_text(f"{digest()} {_lib_sha()}\n")
     return LIB
 
 

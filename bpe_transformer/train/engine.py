@@ -17,7 +17,6 @@ from contextlib import nullcontext
 import torch
 from torch import Tensor, nn
 
-from ..ops import streams
 from ..optim.flat import FlatAdamW, FlatParameters
 from ..optim.flat import ALIGN
 from ..parallel.ddp import BucketedAllReduce
@@ -128,8 +127,6 @@ class TrainEngine:
                     self._mark("fwd")
                 (loss / n if n > 1 else loss).backward()
             total = loss.detach() if total is None else total + loss.detach()
-        if self.flat.grad.is_cuda:
-            streams.join(self.flat.grad.device)  # side-stream weight gradients (ops/streams.py) are in
         self._mark("bwd")
         if self.ddp is not None:
             self.ddp.finish()

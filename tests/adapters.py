@@ -58,7 +58,7 @@ def run_swiglu(d_model: int, d_ff: int, w1_weight: Tensor, w2_weight: Tensor, w3
 
 
 def run_scaled_dot_product_attention(Q: Tensor, K: Tensor, V: Tensor, mask: Tensor | None = None) -> Tensor:
-    return ops.reference.scaled_dot_product_attention(Q, K, V, mask)
+    return ops.scaled_dot_product_attention(Q, K, V, mask)  # GPU tensors: csrc/masked_sdpa.hip
 
 
 def _mha(d_model, num_heads, q, k, v, o, max_seq_len=None, theta=None):

@@ -77,8 +77,16 @@ def test_stale_library_refuses_to_load(tmp_path, monkeypatch):
     B.stamp_path(lib).write_text(json.dumps({"digest": "0" * 64}))
     with pytest.raises(RuntimeError, match="stale"):
         _ext.check_fresh()
-    B.stamp_path(lib).write_text(json.dumps({"digest": B.source_digest()}))
+    B.stamp_path(lib).write_text(json.dumps({"digest": B.source_digest(), "lib_sha256": B.lib_sha(lib)}))
     _ext.check_fresh()  # matching stamp: accepted
+    # a current stamp next to OTHER library bytes (a library replaced after its build, e.g. a stale copy beside a
+    # stamp rewritten for a newer checkout): refused
+    lib.write_bytes(b"y")
+    with pytest.raises(RuntimeError, match="stale"):
+        _ext.check_fresh()
+    B.stamp_path(lib).write_text(json.dumps({"digest": B.source_digest()}))  # no library hash: refused
+    with pytest.raises(RuntimeError, match="stale"):
+        _ext.check_fresh()
     B.stamp_path(lib).unlink()
     with pytest.raises(RuntimeError, match="stale"):
         _ext.check_fresh()

@@ -71,6 +71,45 @@ def test_transformer_lm_snapshot(numpy_snapshot, ts_state_dict, in_indices, voca
     numpy_snapshot.assert_match(out6, atol=1e-4, rtol=1e-2, test_name="test_transformer_lm_truncated_input")
 
 
+def test_swiglu_snapshot(numpy_snapshot, ts_state_dict, in_embeddings, d_model, d_ff):
+    """``/root/reference/tests/test_model.py:43``."""
+    w1, w2, w3 = (ts_state_dict[0][f"layers.0.ffn.{k}.weight"] for k in ("w1", "w2", "w3"))
+    numpy_snapshot.assert_match(run_swiglu(d_model, d_ff, w1, w2, w3, in_embeddings), atol=1e-5,
+                                test_name="test_swiglu")
+
+
+def _attn_weights(sd):
+    return [sd[f"layers.0.attn.{k}_proj.weight"] for k in ("q", "k", "v", "output")]
+
+
+def test_multihead_self_attention_snapshot(numpy_snapshot, ts_state_dict, in_embeddings, d_model, n_heads):
+    """``/root/reference/tests/test_model.py:77``."""
+    out = run_multihead_self_attention(d_model, n_heads, *_attn_weights(ts_state_dict[0]), in_embeddings)
+    numpy_snapshot.assert_match(out, atol=1e-6, test_name="test_multihead_self_attention")
+
+
+def test_multihead_self_attention_with_rope_snapshot(numpy_snapshot, ts_state_dict, in_embeddings, d_model, n_heads,
+                                                     n_keys, theta, pos_ids):
+    """``/root/reference/tests/test_model.py:94`` (positions as a (1, seq) batch, as the reference passes them)."""
+    out = run_multihead_self_attention_with_rope(d_model, n_heads, n_keys, theta, *_attn_weights(ts_state_dict[0]),
+                                                 in_embeddings, pos_ids.reshape(1, -1))
+    numpy_snapshot.assert_match(out, atol=1e-6, test_name="test_multihead_self_attention_with_rope")
+
+
+def test_transformer_block_snapshot(numpy_snapshot, ts_state_dict, in_embeddings, d_model, n_heads, d_ff, n_keys,
+                                    theta):
+    """``/root/reference/tests/test_model.py:158``."""
+    weights = {k.replace("layers.0.", ""): v for k, v in ts_state_dict[0].items() if "layers.0." in k}
+    out = run_transformer_block(d_model, n_heads, d_ff, n_keys, theta, weights, in_embeddings)
+    numpy_snapshot.assert_match(out, atol=1e-6, test_name="test_transformer_block")
+
+
+def test_rmsnorm_snapshot(numpy_snapshot, ts_state_dict, in_embeddings):
+    """``/root/reference/tests/test_model.py:176``."""
+    w = ts_state_dict[0]["layers.1.ln1.weight"]
+    numpy_snapshot.assert_match(run_rmsnorm(w.shape[0], 1e-5, w, in_embeddings), atol=1e-6, test_name="test_rmsnorm")
+
+
 # ---------------------------------------------------------------- independent oracles
 def _w(*shape, seed=0):
     g = torch.Generator().manual_seed(seed)

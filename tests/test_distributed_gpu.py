@@ -1,10 +1,9 @@
 """Data parallelism through the GPU training path: 2 ranks on one MI355X (gloo backend).
 
-The node's 8-GPU RCCL run is the driver's; this exercises everything around the collective on real HIP
-streams: the fused blocks writing weight gradients on the compute stream or (side = "1") the side stream
-(ops/streams.py), gradient-ready
-notifications from both streams, bucketed all-reduces launched from the side stream, the engine's join
-before the optimizer.  Both ranks must end with identical gradients and weights, and the all-reduced
+The node's 8-GPU RCCL run is the driver's; this exercises everything around the collective on a real HIP
+stream: the fused blocks writing weight gradients into the flat buffer, gradient-ready notifications, bucketed
+all-reduces launched mid-backward (in the gradient dtype, or through an fp32 staging buffer: ``comm = "fp32"``),
+the wait before the optimizer.  Both ranks must end with identical gradients and weights, and the all-reduced
 gradient must match one process that trains on the concatenated batch (bf16 tolerance).
 """
 
@@ -41,15 +40,16 @@ def _batch(rank: int, dev):
     return x.to(dev), torch.roll(x, -1, 1).to(dev)
 
 
-def _worker(rank, world, port, bucket_mb, side, out_q):
+def _worker(rank, world, port, bucket_mb, comm, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0", BPE_DW_STREAM=side)  # both ranks share cuda:0
+                      LOCAL_RANK="0")  # both ranks share cuda:0
     from bpe_transformer.parallel import cleanup, init_distributed
     from bpe_transformer.train.engine import TrainEngine
 
     info = init_distributed("cuda", backend="gloo")
     eng = TrainEngine(_model(info.device), info, lr=1e-3, weight_decay=0.0, max_grad_norm=1.0, bucket_mb=bucket_mb,
-                      ddp_check_every=1)  # also asserts bit-identical grads / weights across the ranks
+                      ddp_check_every=1,  # also asserts bit-identical grads / weights across the ranks
+                      comm_dtype=torch.float32 if comm == "fp32" else None)
     eng.train_step([_batch(rank, info.device)])
     g1 = eng.flat.grad.float().cpu()
     eng.train_step([_batch(rank, info.device)])
@@ -59,13 +59,13 @@ def _worker(rank, world, port, bucket_mb, side, out_q):
     cleanup()
 
 
-@pytest.mark.parametrize("side", ["0", "1"])
+@pytest.mark.parametrize("comm", ["grad", "fp32"])
 @pytest.mark.parametrize("bucket_mb", [0.25, 64.0])
-def test_dp2_gpu(gpu_device, bucket_mb, side):
+def test_dp2_gpu(gpu_device, bucket_mb, comm):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, side, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, comm, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {r: (torch.from_numpy(g), torch.from_numpy(d), nb) for r, g, d, nb in (q.get(timeout=240) for _ in range(world))}
@@ -88,9 +88,9 @@ def test_dp2_gpu(gpu_device, bucket_mb, side):
     assert err < 2e-2, err
 
 
-def _zero_worker(rank, world, port, side, out_q):
+def _zero_worker(rank, world, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0", BPE_DW_STREAM=side)
+                      LOCAL_RANK="0")
     from bpe_transformer.parallel import cleanup, init_distributed
     from bpe_transformer.train.engine import TrainEngine
 
@@ -109,15 +109,14 @@ def _zero_worker(rank, world, port, side, out_q):
     cleanup()
 
 
-@pytest.mark.parametrize("side", ["0", "1"])
-def test_zero1_gpu(gpu_device, side):
+def test_zero1_gpu(gpu_device):
     """Sharded DP (parallel/zero.py) on the GPU path: fused blocks notify gradient readiness, buckets are
     reduced, AdamW runs on each rank's pieces only and the weight all-gathers are waited per module by the next
     forward; the ranks end identical and equal to the unsharded engine (bf16 tolerance)."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_zero_worker, args=(r, world, port, side, q)) for r in range(world)]
+    procs = [ctx.Process(target=_zero_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in range(world))

@@ -149,9 +149,13 @@ def test_fp8_engine_reduces_loss(gpu_device):
     assert model.fp8_state.pos == 31
 
 
-def test_forward_is_bitwise_deterministic(gpu_device):
-    """Every forward kernel (attention, norms, CE, GEMM routing) is run-to-run deterministic; only the attention
-    dQ accumulation (fp32 atomics) makes gradients non-bitwise-reproducible."""
+def test_forward_and_backward_are_bitwise_deterministic(gpu_device):
+    """Every kernel of the step is run-to-run deterministic at D = 64: the forward (attention, norms, CE, GEMM
+    routing) and -- since the split attention backward has no dQ atomics (csrc/flash_attn_bwd_split.hip) and the
+    split-K weight gradients reduce their fp32 slabs in a fixed order -- every gradient as well."""
+    import torch.ops
+
+    assert torch.ops.bpe_hip.fa_bwd_config(-1) == 0, "the default D = 64 backward is the split form"
     _, gpu = _pair(gpu_device)
     ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
     tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
@@ -159,6 +163,13 @@ def test_forward_is_bitwise_deterministic(gpu_device):
         a = gpu.loss(ids, tgt)
         b = gpu.loss(ids, tgt)
     assert torch.equal(a, b)
+    grads = []
+    for _ in range(2):
+        gpu.zero_grad(set_to_none=True)
+        gpu.loss(ids, tgt).backward()
+        grads.append([p.grad.clone() for p in gpu.parameters()])
+    for (n, _), g0, g1 in zip(gpu.named_parameters(), *grads):
+        assert torch.equal(g0, g1), n
 
 
 def test_engine_phase_timing(gpu_device):

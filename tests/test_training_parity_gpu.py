@@ -1,26 +1,37 @@
 """At-scale training parity: the fused HIP training engine against an independent eager PyTorch implementation.
 
 The reference implies one training step (``/root/reference/tests/test_optimizer.py:18-25``: forward, cross-entropy,
-backward, clip, AdamW with a cosine schedule).  Here both implementations train the same GPT-2-shaped model
-(d_model 768, 12 heads, SwiGLU d_ff 2048, RoPE, RMSNorm; 2 layers so the test stays short) from identical
+backward, clip, AdamW with a cosine schedule).  Here both implementations train the same model from identical
 weights on the same real-token batches for 150 steps:
 
 * ours: ``TrainEngine`` -- bf16 weights, fp32 master and moments in the flat AdamW kernel, fused blocks (split
   flash attention, SwiGLU GEMM epilogues, TN-layout input gradients), fused LM head + CE, device-side clip;
-* eager: a separate module tree written here with ``torch.nn.functional.scaled_dot_product_attention``, fp32
-  parameters under bf16 autocast, ``torch.optim.AdamW``, ``clip_grad_norm_`` and the same cosine schedule.
+* eager: a separate module tree written here with ``torch.nn.functional.scaled_dot_product_attention`` (KV heads
+  repeated for GQA), fp32 parameters under bf16 autocast, ``torch.optim.AdamW``, ``clip_grad_norm_`` and the same
+  cosine schedule.
+
+Shapes (2 layers each, so the tests stay short):
+
+* ``gpt2``: d_model 768, 12 heads, SwiGLU d_ff 2048, batch x seq = 4 x 1024 -- with one micro-batch per step and
+  with 4 accumulated micro-batches (fp32 gradient buffer);
+* ``llama``: d_model 2048, 32 query / 4 KV heads (GQA, the split backward's KV-head sweep), d_ff 5632 (the
+  unfused SwiGLU forward past d_model 1024), batch x seq = 2 x 2048;
+* ``llama`` fp8: our engine with fp8 projections (e4m3 forward, e5m2 x e4m3 input gradients) against our bf16
+  engine, once through the per-shape routes and once with every fp8 GEMM forced onto the hand-written
+  ``gemm_pp`` F8 kernel (``BPE_FP8_GEMM=hip``).
 
 Tokens: a 4 096-token BPE vocabulary trained here (``train_bpe``) on ``tinystories_sample.txt``, encoding
 ``corpus.en`` + ``tinystories_sample.txt`` (the reference's pickled sample tokenizer is not shipped to the GPU box).
-batch x seq = 4 x 1024 (a multiple of 256, so every fused path engages).  A second run accumulates 4 micro-batches
-of one sequence per step (fp32 gradient buffer).  Set ``BPE_PARITY_LOG=<dir>`` to write both loss curves.
+Set ``BPE_PARITY_LOG=<dir>`` to write the loss curves.
 """
 
 from __future__ import annotations
 
+import functools
 import json
 import math
 import os
+from dataclasses import dataclass
 
 import pytest
 import torch
@@ -31,15 +42,33 @@ from .conftest import FIXTURES
 
 pytestmark = pytest.mark.gpu
 
-STEPS, B, S = 150, 4, 1024
-D, L, H, FF, THETA = 768, 2, 12, 2048, 10000.0
-LR_MAX, LR_MIN, WARMUP = 1e-3, 1e-4, 10
+STEPS, L, THETA = 150, 2, 10000.0
+WARMUP = 10
 
 
-def _lr(it: int) -> float:
+@dataclass(frozen=True)
+class Shape:
+    name: str
+    B: int
+    S: int
+    D: int
+    H: int
+    Hkv: int
+    FF: int
+    lr: float  # peak learning rate (cosine to lr / 10)
+
+
+# Llama-shape peak LR 3e-4 (the usual for d_model 2048): at 1e-3 both implementations hit loss spikes from step ~25
+# on and their trajectories part chaotically (matching to 6e-4 relative before the first spike), which says nothing
+# about the arithmetic.
+SHAPES = {"gpt2": Shape("gpt2shape", 4, 1024, 768, 12, 12, 2048, 1e-3),
+          "llama": Shape("llamashape", 2, 2048, 2048, 32, 4, 5632, 3e-4)}
+
+
+def _lr(it: int, c) -> float:
     from bpe_transformer.optim.schedule import get_lr_cosine_schedule
 
-    return get_lr_cosine_schedule(it, LR_MAX, LR_MIN, WARMUP, STEPS)
+    return get_lr_cosine_schedule(it, c.lr, c.lr / 10, WARMUP, STEPS)
 
 
 class _RMS(nn.Module):
@@ -60,36 +89,42 @@ def _rope(x, cos, sin):  # x [B, H, S, Dh], interleaved pairs (2i, 2i+1)
 
 
 class _Attn(nn.Module):
-    def __init__(self):
+    def __init__(self, c: Shape):
         super().__init__()
-        self.q_proj = nn.Linear(D, D, bias=False)
-        self.k_proj = nn.Linear(D, D, bias=False)
-        self.v_proj = nn.Linear(D, D, bias=False)
-        self.output_proj = nn.Linear(D, D, bias=False)
+        self.c = c
+        dk = c.D // c.H
+        self.q_proj = nn.Linear(c.D, c.D, bias=False)
+        self.k_proj = nn.Linear(c.D, c.Hkv * dk, bias=False)
+        self.v_proj = nn.Linear(c.D, c.Hkv * dk, bias=False)
+        self.output_proj = nn.Linear(c.D, c.D, bias=False)
 
     def forward(self, x, cos, sin):
         b, s, _ = x.shape
-        q, k, v = (p(x).view(b, s, H, D // H).transpose(1, 2) for p in (self.q_proj, self.k_proj, self.v_proj))
+        c, dk = self.c, self.c.D // self.c.H
+        q = self.q_proj(x).view(b, s, c.H, dk).transpose(1, 2)
+        k, v = (p(x).view(b, s, c.Hkv, dk).transpose(1, 2) for p in (self.k_proj, self.v_proj))
         q, k = _rope(q, cos, sin), _rope(k, cos, sin)
+        if c.Hkv < c.H:  # GQA: query head h reads KV head h // (H / Hkv)
+            k, v = (t.repeat_interleave(c.H // c.Hkv, dim=1) for t in (k, v))
         o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        return self.output_proj(o.transpose(1, 2).reshape(b, s, D))
+        return self.output_proj(o.transpose(1, 2).reshape(b, s, c.D))
 
 
 class _FFN(nn.Module):
-    def __init__(self):
+    def __init__(self, c: Shape):
         super().__init__()
-        self.w1 = nn.Linear(D, FF, bias=False)
-        self.w2 = nn.Linear(FF, D, bias=False)
-        self.w3 = nn.Linear(D, FF, bias=False)
+        self.w1 = nn.Linear(c.D, c.FF, bias=False)
+        self.w2 = nn.Linear(c.FF, c.D, bias=False)
+        self.w3 = nn.Linear(c.D, c.FF, bias=False)
 
     def forward(self, x):
         return self.w2(F.silu(self.w1(x)) * self.w3(x))
 
 
 class _Block(nn.Module):
-    def __init__(self):
+    def __init__(self, c: Shape):
         super().__init__()
-        self.ln1, self.attn, self.ln2, self.ffn = _RMS(D), _Attn(), _RMS(D), _FFN()
+        self.ln1, self.attn, self.ln2, self.ffn = _RMS(c.D), _Attn(c), _RMS(c.D), _FFN(c)
 
     def forward(self, x, cos, sin):
         x = x + self.attn(self.ln1(x), cos, sin)
@@ -99,10 +134,11 @@ class _Block(nn.Module):
 class EagerLM(nn.Module):
     """Independent implementation with the reference's parameter names (``tests/adapters.py:311-353``)."""
 
-    def __init__(self, vocab):
+    def __init__(self, vocab, c: Shape):
         super().__init__()
+        D, H, S = c.D, c.H, c.S
         self.token_embeddings = nn.Embedding(vocab, D)
-        self.layers = nn.ModuleList(_Block() for _ in range(L))
+        self.layers = nn.ModuleList(_Block(c) for _ in range(L))
         self.ln_final = _RMS(D)
         self.lm_head = nn.Linear(D, vocab, bias=False)
         inv = THETA ** (-torch.arange(0, D // H, 2, dtype=torch.float64) / (D // H))
@@ -119,6 +155,7 @@ class EagerLM(nn.Module):
         return F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), y.reshape(-1))
 
 
+@functools.lru_cache(maxsize=1)
 def _tokens():
     from bpe_transformer import train_bpe
     from bpe_transformer.tokenization import BPETokenizer
@@ -130,7 +167,7 @@ def _tokens():
     return torch.tensor(tok.encode(text), dtype=torch.long), len(tok.vocab)
 
 
-def _batches(ids, n, micro, dev):
+def _batches(ids, n, micro, S, dev):
     g = torch.Generator().manual_seed(1234)
     out = []
     for _ in range(n):
@@ -140,29 +177,40 @@ def _batches(ids, n, micro, dev):
     return out
 
 
-def _run(accum: int, gpu_device):
+def _ours(vocab, c: Shape, dev):
     from bpe_transformer.models import TransformerLM
+
+    torch.manual_seed(0)
+    return TransformerLM(vocab, c.S, c.D, L, c.H, c.FF, THETA, num_kv_heads=c.Hkv, device=dev, dtype=torch.bfloat16)
+
+
+def _engine(model, accum, c):
     from bpe_transformer.train.engine import TrainEngine
 
+    return TrainEngine(model, lr=c.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0,
+                       grad_dtype=torch.float32 if accum > 1 else None)
+
+
+def _run(c: Shape, accum: int, gpu_device):
+    """Our engine vs the eager implementation: (our losses, eager losses)."""
+    assert torch.ops.bpe_hip.fa_bwd_config(-1) == 0, "the default D = 64 backward is the split form"
     ids, vocab = _tokens()
-    torch.manual_seed(0)
-    ours = TransformerLM(vocab, S, D, L, H, FF, THETA, device=gpu_device, dtype=torch.bfloat16)
-    eager = EagerLM(vocab).to(gpu_device)
+    ours = _ours(vocab, c, gpu_device)
+    eager = EagerLM(vocab, c).to(gpu_device)
     missing, unexpected = eager.load_state_dict({k: v.float() for k, v in ours.state_dict().items()}, strict=False)
     assert not missing and not [k for k in unexpected if "rope" not in k], (missing, unexpected)
-    eng = TrainEngine(ours, lr=LR_MAX, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0,
-                      grad_dtype=torch.float32 if accum > 1 else None)
+    eng = _engine(ours, accum, c)
     decay = [p for p in eager.parameters() if p.dim() >= 2]
     nodecay = [p for p in eager.parameters() if p.dim() < 2]
     opt = torch.optim.AdamW([{"params": decay, "weight_decay": 0.1}, {"params": nodecay, "weight_decay": 0.0}],
-                            lr=LR_MAX, betas=(0.9, 0.95), eps=1e-8)
-    micro = B // accum
-    data = _batches(ids, STEPS * accum, micro, gpu_device)
+                            lr=c.lr, betas=(0.9, 0.95), eps=1e-8)
+    micro = c.B // accum
+    data = _batches(ids, STEPS * accum, micro, c.S, gpu_device)
     lo, le = [], []
     for it in range(STEPS):
         mb = data[it * accum : (it + 1) * accum]
-        lo.append(eng.train_step(mb, lr=_lr(it)))
-        lr = _lr(it)
+        lo.append(eng.train_step(mb, lr=_lr(it, c)))
+        lr = _lr(it, c)
         for gr in opt.param_groups:
             gr["lr"] = lr
         opt.zero_grad(set_to_none=True)
@@ -179,17 +227,56 @@ def _run(accum: int, gpu_device):
     return lo, le
 
 
-@pytest.mark.parametrize("accum", [1, 4])
-def test_fused_engine_tracks_eager_pytorch(gpu_device, accum):
-    lo, le = _run(accum, gpu_device)
-    assert all(math.isfinite(v) for v in lo + le)
-    rel = [abs(a - b) / b for a, b in zip(lo, le)]
+def _run_ours(c: Shape, fp8: bool, gpu_device):
+    ids, vocab = _tokens()
+    model = _ours(vocab, c, gpu_device)
+    if fp8:
+        model.enable_fp8()
+    eng = _engine(model, 1, c)
+    data = _batches(ids, STEPS, c.B, c.S, gpu_device)
+    out = [eng.train_step([data[it]], lr=_lr(it, c)) for it in range(STEPS)]
+    return [float(v) for v in torch.stack(out).cpu()]
+
+
+def _log(name, payload):
     log = os.environ.get("BPE_PARITY_LOG")
     if log:
         os.makedirs(log, exist_ok=True)
-        with open(os.path.join(log, f"parity_gpt2shape_L{L}_accum{accum}.json"), "w") as f:
-            json.dump({"steps": STEPS, "batch": B, "seq": S, "accum": accum, "ours": lo, "eager": le,
-                       "max_rel": max(rel), "final_rel": rel[-1]}, f)
+        with open(os.path.join(log, name), "w") as f:
+            json.dump(payload, f)
+
+
+@pytest.mark.parametrize("shape,accum", [("gpt2", 1), ("gpt2", 4), ("llama", 1)])
+def test_fused_engine_tracks_eager_pytorch(gpu_device, shape, accum):
+    c = SHAPES[shape]
+    lo, le = _run(c, accum, gpu_device)
+    assert all(math.isfinite(v) for v in lo + le)
+    rel = [abs(a - b) / b for a, b in zip(lo, le)]
+    _log(f"parity_{c.name}_L{L}_accum{accum}.json",
+         {"steps": STEPS, "batch": c.B, "seq": c.S, "d_model": c.D, "heads": c.H, "kv_heads": c.Hkv, "d_ff": c.FF,
+          "accum": accum, "ours": lo, "eager": le, "max_rel": max(rel), "final_rel": rel[-1]})
     assert le[-1] < le[0] - 2.0, "the eager reference did not learn: the comparison would be vacuous"
+    assert lo[-1] < lo[0] - 2.0
     assert max(rel) < 0.02, (max(rel), rel.index(max(rel)))
     assert rel[-1] < 0.01, rel[-1]
+
+
+@pytest.mark.parametrize("route", ["routes", "hip"])
+def test_fp8_engine_tracks_bf16_engine(gpu_device, monkeypatch, route):
+    """fp8 projections (``model.enable_fp8()``: delayed-scaling e4m3 / e5m2, ops/fp8.py) against the bf16 engine on
+    the Llama shape: the final loss within 2 %, every step within 5 %.  ``route``: the per-shape route table, or
+    every fp8 GEMM on the hand-written gemm_pp F8 kernel."""
+    from bpe_transformer.ops import fp8
+
+    monkeypatch.setattr(fp8, "_MODE", route)
+    c = SHAPES["llama"]
+    lb = _run_ours(c, False, gpu_device)
+    l8 = _run_ours(c, True, gpu_device)
+    assert all(math.isfinite(v) for v in lb + l8)
+    rel = [abs(a - b) / b for a, b in zip(l8, lb)]
+    _log(f"parity_{c.name}_L{L}_fp8_{route}_vs_bf16.json",
+         {"steps": STEPS, "batch": c.B, "seq": c.S, "route": route, "fp8": l8, "bf16": lb, "max_rel": max(rel),
+          "final_rel": rel[-1]})
+    assert lb[-1] < lb[0] - 2.0
+    assert max(rel) < 0.05, (max(rel), rel.index(max(rel)))
+    assert rel[-1] < 0.02, rel[-1]
