@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-rope", action="store_true", help="plain attention (isolates the fused-RoPE cost)")
+    ap.add_argument("--no-causal", action="store_true", help="full (non-causal) attention")
     ap.add_argument("--bwd-ab", action="store_true",
                     help="interleaved same-process A/B of the backward forms (ops.fa_bwd_config): fused (atomics) "
                          "and split")
@@ -44,6 +45,7 @@ def main():
     hip = _ops()
     scale = 1.0 / D ** 0.5
     rope = cos is not None
+    causal = not a.no_causal
     pre = a.mode == "block" and rope
     x = qkv.detach().clone()
     q, k, v = x[:, : H * D], x[:, H * D : (H + Hkv) * D], x[:, (H + Hkv) * D :]
@@ -53,16 +55,16 @@ def main():
     def fwd():
         if pre:
             hip.rope_qk_(x, c, s_, B, S, H, Hkv, D)  # in place, as the fused block does (values drift: timing only)
-        return hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
+        return hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, causal, rope, scale, pre)
 
     def bwd(o, lse):
-        return hip.fa_bwd(do, q, k, v, o, lse, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
+        return hip.fa_bwd(do, q, k, v, o, lse, c, s_, B, S, H, Hkv, D, causal, rope, scale, pre)
 
     for _ in range(3):
         o, lse = fwd()
         bwd(o, lse)
     torch.cuda.synchronize()
-    fl = 4.0 * B * H * S * S * D / 2
+    fl = 4.0 * B * H * S * S * D / (1 if a.no_causal else 2)
     if a.fwd_ab:
         prev = hip.fa_fwd_config(0)
         times = {v: [] for v in a.fwd_versions}
@@ -70,10 +72,10 @@ def main():
         for _ in range(a.rounds):
             for ver in times:
                 hip.fa_fwd_config(ver)
-                hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
+                hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, causal, rope, scale, pre)
                 ev[0].record()
                 for _ in range(a.iters):
-                    hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
+                    hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, causal, rope, scale, pre)
                 ev[1].record()
                 torch.cuda.synchronize()
                 times[ver].append(ev[0].elapsed_time(ev[1]) / a.iters)
@@ -85,7 +87,8 @@ def main():
         if not a.bwd_ab:
             return
     if a.bwd_ab:
-        arms = {"fused": 1, "split": 0}
+        arms = {"fused": 1, "split": 0, "split_dq1wg": 2, "split_dkv1wg": 4, "split_both1wg": 6,
+                "dkv_nodma": 8, "dkv_noexp": 16, "dkv_nodvdk": 32, "dkv_nosdp": 64, "dkv_noexp_nodvdk": 48, "dkv_stagger": 128, "dkv_pipe": 256, "dkv_pipe_stagger": 384, "dkv_prefetch": 768, "dkv_prefetch_stagger": 896, "dkv_persist": 2048, "dq_persist": 4096, "both_persist": 6144}
         if a.bwd_arms:
             arms = {n: arms[n] for n in a.bwd_arms}
         prev = hip.fa_bwd_config(-1)
@@ -115,7 +118,7 @@ def main():
         if pre:
             hip.rope_qk_(x, c, s_, B, S, H, Hkv, D)
         e[3].record()
-        o, lse = hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, True, rope, scale, pre)
+        o, lse = hip.fa_fwd(q, k, v, c, s_, B, S, H, Hkv, D, causal, rope, scale, pre)
         e[1].record()
         bwd(o, lse)
         e[2].record()

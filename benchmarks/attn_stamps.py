@@ -1,0 +1,55 @@
+"""Per-workgroup phase times of the split attention backward from in-kernel s_memtime stamps.
+
+Needs the stamps variant build (``python -m bpe_transformer.ops.build --variant stamps -D BPE_FA_STAMPS``) and runs
+with ``BPE_HIP_VARIANT=stamps``.  For each kernel (dQ, dK/dV) and each tile count it prints the mean workgroup
+duration, its prologue (entry -> first barrier) and the per-tile loop time, in shader cycles.
+usage: BPE_HIP_VARIANT=stamps python benchmarks/attn_stamps.py [--batch B] [--seq S] [--heads H] [--kv-heads Hkv]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from bpe_transformer.ops import reference as R  # noqa: E402
+from bpe_transformer.ops._ext import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--heads", type=int, default=12)
+    ap.add_argument("--kv-heads", type=int, default=None)
+    a = ap.parse_args()
+    h = ops()
+    B, S, H, D = a.batch, a.seq, a.heads, 64
+    Hkv = a.kv_heads or H
+    torch.manual_seed(0)
+    qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    cos, sin = R.rope_tables(D, S, 10000.0, device="cuda")
+    h.rope_qk_(qkv, cos, sin, B, S, H, Hkv, D)
+    q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
+    o, lse = h.fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, True, D ** -0.5, True)
+    do = torch.randn_like(o)
+    for _ in range(3):
+        h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, True, D ** -0.5, True)
+    torch.cuda.synchronize()
+    st = h.fa_stamps(65536).double()
+    if st.numel() == 0:
+        sys.exit("not a BPE_FA_STAMPS build: set BPE_HIP_VARIANT=stamps (ops.build --variant stamps -D BPE_FA_STAMPS)")
+    nblk = (S + 127) // 128
+    for name, base, n in (("dQ", 0, nblk * B * H), ("dK/dV", 32768, nblk * B * Hkv)):
+        r = st[base : base + n]
+        dur, pro, loop, nt = r[:, 3] - r[:, 0], r[:, 1] - r[:, 0], r[:, 3] - r[:, 1], r[:, 5]
+        print(f"{name} B={B} S={S} H={H} Hkv={Hkv}: {n} workgroups, mean {dur.mean():.0f} cycles, prologue "
+              f"{pro.mean():.0f} ({pro.sum() / dur.sum() * 100:.1f} %)")
+        for t in sorted(set(nt.tolist())):
+            m = nt == t
+            print(f"  tiles {int(t):3d}: n {int(m.sum()):5d}  workgroup {dur[m].mean():8.0f}  prologue {pro[m].mean():6.0f}"
+                  f"  loop/tile {(loop[m] / t).mean():6.0f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -43,6 +43,20 @@ constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4;
 // 4 waves x 32 rows per workgroup, 2 workgroups per CU (2 waves per SIMD at <= 256 VGPRs)
 constexpr int NW = 4, CPT = 512 / (NW * 64);
 
+// Per-workgroup s_memtime stamps (a diagnostic variant build: ops.build --variant stamps -D BPE_FA_STAMPS): slot 0
+// entry, 1 after the prologue barrier, 3 after the tile loop, 5 the tile count; rows 0.. the dQ kernel's workgroups,
+// rows 32768.. the dK/dV kernel's; read with ops.fa_stamps().  The normal build compiles them out.
+#ifdef BPE_FA_STAMPS
+__device__ long long g_stamps[65536 * 8];
+#define FA_STAMP(base, i, v)                                                                         \
+    if (threadIdx.x == 0) {                                                                          \
+        g_stamps[((base) + (long)(blockIdx.x & 32767)) * 8 + (i)] = __builtin_amdgcn_s_memtime();   \
+        if ((i) == 3) g_stamps[((base) + (long)(blockIdx.x & 32767)) * 8 + 5] = (v);               \
+    }
+#else
+#define FA_STAMP(base, i, v)
+#endif
+
 template <bool CAUSAL, bool ROPE, bool ROPE_IN>
 __global__ void __launch_bounds__(NW * 64, 2)
 fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
@@ -60,6 +74,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     char* Vs = smem + 2 * BUF;  // [2][KT keys][128 B]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    FA_STAMP(0, 0, 0);
     const int nqb = (S + QB - 1) / QB;
     int rank, bh;
     grouped_order((int)blockIdx.x, nqb, B * H, group, rank, bh);
@@ -70,46 +85,18 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     const long qc = q_ok ? q : S - 1;
     const long qrow = (long)b * S + qc;
 
-    // ---- pinned B operands (query on the lane, d = 16 ks + 8 hh + j) and delta = rowsum(dO * O)
-    bf16x8 qf[KS], of[KS];
-    float dsum = 0.f;
+    // ---- prologue: every load issued before any of them is waited for -- the pinned Q / dO rows, the O rows of
+    // delta, the LSE and K / V tile 0 -- so the prologue costs one memory round trip, not three (per-workgroup
+    // s_memtime stamps at GPT-2 B 128: ~8k of a ~42k-cycle workgroup went to the serial form)
+    u16x8 tqr[KS], tgr[KS], tor[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
         const int d0 = 16 * ks + 8 * hh;
-        u16x8 tq = *reinterpret_cast<const u16x8*>(Q + qrow * ld_q + (long)h * D + d0);
-        // softmax scale * log2(e) folded into the pinned Q (as the forward does): S^T comes out in log2 units
-        if (ROPE_IN) {
-            tq = rope_u16x8(tq, cosT + qc * (D / 2) + d0 / 2, sinT + qc * (D / 2) + d0 / 2, scale_log2);
-        } else {
-            float x[8];
-            unpack8(tq, x);
-            tq = pack8(x, scale_log2);
-        }
-        qf[ks] = __builtin_bit_cast(bf16x8, tq);
-        const u16x8 tg = *reinterpret_cast<const u16x8*>(dO + qrow * ld_do + (long)h * D + d0);
-        const u16x8 to = *reinterpret_cast<const u16x8*>(O + qrow * ld_o + (long)h * D + d0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dsum += bf2f(tg[i]) * bf2f(to[i]);
-        of[ks] = __builtin_bit_cast(bf16x8, tg);
+        tqr[ks] = *reinterpret_cast<const u16x8*>(Q + qrow * ld_q + (long)h * D + d0);
+        tgr[ks] = *reinterpret_cast<const u16x8*>(dO + qrow * ld_do + (long)h * D + d0);
+        tor[ks] = *reinterpret_cast<const u16x8*>(O + qrow * ld_o + (long)h * D + d0);
     }
-    dsum += __shfl_xor(dsum, 32, 64);
-    if (q_ok && hh == 0) DELTA[((long)b * H + h) * S + q] = dsum;
     const float lse = LSE[((long)b * H + h) * S + qc];
-    // row constants as the initial accumulators (query = lane): S^T starts at -lse, so P = exp2(S^T) with no
-    // VALU before the exponential (-inf for empty / pad rows: P = 0); dP^T starts at -delta
-    const float nl = (q_ok && lse < INFINITY) ? -lse : -INFINITY;
-    f32x16 ns, nd;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        ns[r] = nl;
-        nd[r] = -dsum;
-    }
-
-    f32x16 acc[2];
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
 
     const int kend = CAUSAL ? min(S, q0 + QB) : S;
     const int nkt = (kend + KT - 1) / KT;
@@ -154,9 +141,50 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         }
     } else {
         load_tile(0);
-        write_tile(0, 0);
     }
+
+    // ---- pinned B operands (query on the lane, d = 16 ks + 8 hh + j) and delta = rowsum(dO * O)
+    bf16x8 qf[KS], of[KS];
+    float dsum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int d0 = 16 * ks + 8 * hh;
+        u16x8 tq = tqr[ks];
+        // softmax scale * log2(e) folded into the pinned Q (as the forward does): S^T comes out in log2 units
+        if (ROPE_IN) {
+            tq = rope_u16x8(tq, cosT + qc * (D / 2) + d0 / 2, sinT + qc * (D / 2) + d0 / 2, scale_log2);
+        } else {
+            float x[8];
+            unpack8(tq, x);
+            tq = pack8(x, scale_log2);
+        }
+        qf[ks] = __builtin_bit_cast(bf16x8, tq);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dsum += bf2f(tgr[ks][i]) * bf2f(tor[ks][i]);
+        of[ks] = __builtin_bit_cast(bf16x8, tgr[ks]);
+    }
+    dsum += __shfl_xor(dsum, 32, 64);
+    // (delta is stored for the dK/dV kernel in the epilogue, not here: a store before the prologue barrier, whose
+    // vmcnt(0) also waits for it, put its write-acknowledge latency into the prologue)
+    // row constants as the initial accumulators (query = lane): S^T starts at -lse, so P = exp2(S^T) with no
+    // VALU before the exponential (-inf for empty / pad rows: P = 0); dP^T starts at -delta
+    const float nl = (q_ok && lse < INFINITY) ? -lse : -INFINITY;
+    f32x16 ns, nd;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        ns[r] = nl;
+        nd[r] = -dsum;
+    }
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
+
+    if constexpr (!DM) write_tile(0, 0);
     __syncthreads();
+    FA_STAMP(0, 1, 0);
 
     const int trow = 4 * hh + ((l & 15) >> 2);          // tr-read row inside a 16-key step
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);  // tr-read column inside a 32-wide d tile
@@ -177,10 +205,12 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                 }
             }
             if (!CAUSAL || k0 <= qw + 31) {
-                const bool need_mask = (CAUSAL && k0 + KT - 1 > qw) || (k0 + KT > S);
 #pragma unroll
                 for (int kq = 0; kq < KT / 32; ++kq) {
                     if (CAUSAL && k0 + 32 * kq > qw + 31) break;  // this 32-key step is past every query of the wave
+                    // masked only where a key of the step can pass a query of the wave (the diagonal 32 x 32 step)
+                    // or the sequence end: the other steps of a diagonal tile take the unmasked path
+                    const bool need_mask = (CAUSAL && k0 + 32 * kq + 31 > qw) || (k0 + 32 * kq + 32 > S);
                     // step kq: image kq / 2 of the tile, its 32-key half kh
                     char* Kh = Kc + (kq >> 1) * TILE;
                     const char* Vh = Vc + (kq >> 1) * TILE;
@@ -242,11 +272,16 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
             }
         };
         body(Ks + cur * BUF, Vs + cur * BUF, Ks + (cur ^ 1) * BUF, Vs + (cur ^ 1) * BUF);
-        if (!DM && it + 1 < nkt) write_tile(it + 1, cur ^ 1);
-        __syncthreads();
+        if (it + 1 < nkt) {  // (no barrier after the last tile: a wave done with the diagonal leaves early)
+            if (!DM) write_tile(it + 1, cur ^ 1);
+            __syncthreads();
+        }
     }
 
-    // ---- epilogue: dQ = scale * R(-pos) dQ^T (query on the lane, 4 consecutive d per register group)
+    FA_STAMP(0, 3, nkt);
+    // ---- epilogue: delta for the dK/dV kernel; dQ = scale * R(-pos) dQ^T (query on the lane, 4 consecutive d per
+    // register group)
+    if (q_ok && hh == 0) DELTA[((long)b * H + h) * S + q] = dsum;
     if (q_ok) {
         __bf16* dqp = dQ + ((long)b * S + q) * ld_dq + (long)h * D;
 #pragma unroll
@@ -290,6 +325,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     float* dltS = lseS + 2 * QT;                                // [2][QT]  -delta
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    FA_STAMP(32768, 0, 0);
     const int nkb = (S + KB - 1) / KB;
     // One workgroup per (batch, KV head, key block) sweeps the G = H / Hkv query heads of its group one after the
     // other, summing their dK / dV in the accumulators: no fp32 partials, no reduce kernel (GQA).
@@ -303,48 +339,32 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     const bool key_ok = key < S;
     const long kpos = key_ok ? key : S - 1;
 
-    // ---- pinned B operands: K (roped) and V rows of the lane's key, d = 16 ks + 8 hh + j
-    bf16x8 kf[KS], vf[KS];
+    // ---- prologue: every load issued before any of them is waited for -- the pinned K / V rows, tile 0's row
+    // constants and its Q / dO (LDS-DMA) -- one memory round trip instead of three (per-workgroup s_memtime stamps
+    // at GPT-2 B 128: the serial form spent ~8k cycles of a ~42k-cycle workgroup here)
+    u16x8 tkr[KS], tvr[KS];
     {
         const __bf16* kp = K + ((long)b * S + kpos) * ld_kv + (long)hk * D;
         const __bf16* vp = Vv + ((long)b * S + kpos) * ld_kv + (long)hk * D;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-            const int d0 = 16 * ks + 8 * hh;
-            // unconditional loads (kpos is clamped) consumed by a VALU select here: the wait for them then sits in
-            // this prologue.  (As a branch around the loads, the wait-count pass placed a vmcnt(0) before the first
-            // use of V inside the tile loop -- draining the next tile's prefetch in every half-tile.)
-            u16x8 tk = *reinterpret_cast<const u16x8*>(kp + d0);
-            u16x8 tv = *reinterpret_cast<const u16x8*>(vp + d0);
-            const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-            tk = key_ok ? tk : z;
-            tv = key_ok ? tv : z;
-            // softmax scale * log2(e) folded into the pinned K: S comes out in log2 units
-            if (ROPE_IN) {
-                tk = rope_u16x8(tk, cosT + kpos * (D / 2) + d0 / 2, sinT + kpos * (D / 2) + d0 / 2, scale_log2);
-            } else {
-                float x[8];
-                unpack8(tk, x);
-                tk = pack8(x, scale_log2);
-            }
-            kf[ks] = __builtin_bit_cast(bf16x8, tk);
-            vf[ks] = __builtin_bit_cast(bf16x8, tv);
+            // unconditional loads (kpos is clamped), consumed by a VALU select below in this prologue.  (As a branch
+            // around the loads, the wait-count pass placed a vmcnt(0) before the first use of V inside the tile loop
+            // -- draining the next tile's prefetch in every half-tile.)
+            tkr[ks] = *reinterpret_cast<const u16x8*>(kp + 16 * ks + 8 * hh);
+            tvr[ks] = *reinterpret_cast<const u16x8*>(vp + 16 * ks + 8 * hh);
         }
     }
-
-    f32x16 dk[2], dv[2];
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
-
     const int m_start = CAUSAL ? kb0 : 0;  // kb0 is a multiple of 64
     const int nqt = m_start < S ? (S - m_start + QT - 1) / QT : 0;
     const int nsteps = GL * nqt;  // (query head, query tile) steps, head-major
     // step j: query head h + j / nqt, query tile j % nqt
     auto q_of = [&](int j) { return Q + (long)b * S * ld_q + (long)(h + j / nqt) * D; };
     auto o_of = [&](int j) { return dO + (long)b * S * ld_do + (long)(h + j / nqt) * D; };
-    auto m0_of = [&](int j) { return m_start + (j % nqt) * QT; };
+    // query tiles last to first: the diagonal tile (whose waves have 4, 3, 2, 1 half-steps) comes last, with no
+    // barrier after it, so a wave done with it leaves its SIMD to the co-resident workgroup instead of waiting; and
+    // the key blocks of one (batch, head) pair, launched together, start on the same Q / dO tile (L2 reuse)
+    auto m0_of = [&](int j) { return m_start + (nqt - 1 - j % nqt) * QT; };
     u16x8 qreg[CPT], oreg[CPT];
     float lreg = 0.f, dreg = 0.f;
     // DM: Q / dO tiles by LDS-DMA through per-head buffer resources (no staging registers, no per-tile address
@@ -392,19 +412,47 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
         }
     };
 
+
     if (nqt > 0) {
         load_tile(0);
         if constexpr (DM) {
 #pragma unroll
             for (int sb = 0; sb < NSUB; ++sb) {
-                dma_tile64_buf(q_of(0), head_bytes(ld_q, S, D), qvo, m_start + 64 * sb, ld_q, Qs + sb * TILE, wu);
-                dma_tile64_buf(o_of(0), head_bytes(ld_do, S, D), ovo, m_start + 64 * sb, ld_do, dOs + sb * TILE, wu);
+                dma_tile64_buf(q_of(0), head_bytes(ld_q, S, D), qvo, m0_of(0) + 64 * sb, ld_q, Qs + sb * TILE, wu);
+                dma_tile64_buf(o_of(0), head_bytes(ld_do, S, D), ovo, m0_of(0) + 64 * sb, ld_do, dOs + sb * TILE, wu);
             }
         }
-        write_tile(0, 0);
     }
-    __syncthreads();
 
+    // ---- pinned B operands: K (roped) and V rows of the lane's key, d = 16 ks + 8 hh + j
+    bf16x8 kf[KS], vf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int d0 = 16 * ks + 8 * hh;
+        const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        u16x8 tk = key_ok ? tkr[ks] : z;
+        const u16x8 tv = key_ok ? tvr[ks] : z;
+        // softmax scale * log2(e) folded into the pinned K: S comes out in log2 units
+        if (ROPE_IN) {
+            tk = rope_u16x8(tk, cosT + kpos * (D / 2) + d0 / 2, sinT + kpos * (D / 2) + d0 / 2, scale_log2);
+        } else {
+            float x[8];
+            unpack8(tk, x);
+            tk = pack8(x, scale_log2);
+        }
+        kf[ks] = __builtin_bit_cast(bf16x8, tk);
+        vf[ks] = __builtin_bit_cast(bf16x8, tv);
+    }
+
+    f32x16 dk[2], dv[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+
+    if (nqt > 0) write_tile(0, 0);
+    __syncthreads();
+    FA_STAMP(32768, 1, 0);
     const int trow = 4 * hh + ((l & 15) >> 2);
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
     const int klim = CAUSAL ? (key_ok ? key : S) : (key_ok ? 0 : S);
@@ -430,10 +478,13 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
             const float* lc = lseS + cur * QT;
             const float* dc = dltS + cur * QT;
             if (!CAUSAL || m0 + QT - 1 >= kw0) {
-                const bool need_mask = (CAUSAL && m0 < kw0 + 31) || (m0 + QT > S) || (kw0 + 32 > S);
 #pragma unroll
                 for (int qq = 0; qq < QT / 32; ++qq) {
                     if (CAUSAL && m0 + 32 * qq + 31 < kw0) continue;  // every query of this step precedes every key
+                    // masked only where a query of the step can precede a key of the wave (the diagonal 32 x 32
+                    // step) or at the sequence end: the other steps of a diagonal tile take the unmasked path
+                    const bool need_mask =
+                        (CAUSAL && m0 + 32 * qq < kw0 + 31) || (m0 + 32 * qq + 32 > S) || (kw0 + 32 > S);
                     // step qq: image qq / 2 of the tile, its 32-query half qt
                     char* Qh = Qc + (qq >> 1) * TILE;
                     char* Oh = Oc + (qq >> 1) * TILE;
@@ -493,10 +544,13 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
             }
         };
         body(Qs + cur * BUF, dOs + cur * BUF, Qs + (cur ^ 1) * BUF, dOs + (cur ^ 1) * BUF);
-        if (it + 1 < nsteps) write_tile(it + 1, cur ^ 1);
-        __syncthreads();
+        if (it + 1 < nsteps) {  // (no barrier after the last tile: see m0_of)
+            write_tile(it + 1, cur ^ 1);
+            __syncthreads();
+        }
     }
 
+    FA_STAMP(32768, 3, nsteps);
     if (!key_ok) return;
     // ---- dK = scale * R(-pos) dK^T, dV = dV^T (key on the lane, d in registers)
     __bf16* dkp = dK + ((long)b * S + key) * ld_dkv + (long)hk * D;
@@ -566,6 +620,19 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
 // whether a GQA backward of head size D needs the fp32 dK / dV partials buffer (FaArgs::dkv_part): only the fused
 // backward does (the split dK/dV kernel sweeps the query heads of its KV head)
 bool fa_dkv_partials_needed(int D) { return !fa_bwd_split_active(D); }
+
+// copy the last launch's stamps out (BPE_FA_STAMPS builds; false otherwise)
+bool fa_read_stamps(long long* host, int n) {
+#ifdef BPE_FA_STAMPS
+    (void)hipDeviceSynchronize();
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(split::g_stamps), (size_t)n * 8 * sizeof(long long), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess;
+#else
+    (void)host;
+    (void)n;
+    return false;
+#endif
+}
 
 bool launch_fa_bwd_split(const FaArgs& a, hipStream_t s) {
     if (!fa_bwd_split_active(a.D)) return false;

@@ -45,17 +45,13 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
     const int q0 = qb * 128, qw0 = q0 + 32 * w, qrow = qw0 + l31;
 
-    // Q fragments (B operand of S^T = K.Q^T), softmax scale * log2(e) folded in; rows past the end clamped
-    bf16x8 qf[KS];
+    // prologue: the Q rows and K / V tile 0 are all requested before any is waited for (one memory round trip)
+    u16x8 qr[KS];
     {
-        const long qpos = min(qrow, S - 1);
+        const long qpos = min(qrow, S - 1);  // rows past the end clamped
         const __bf16* qp = Q + ((long)b * S + qpos) * ld_q + (long)h * D;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            float x[8];
-            unpack8(*reinterpret_cast<const u16x8*>(qp + 16 * ks + 8 * hh), x);
-            qf[ks] = __builtin_bit_cast(bf16x8, pack8(x, scale_log2));
-        }
+        for (int ks = 0; ks < KS; ++ks) qr[ks] = *reinterpret_cast<const u16x8*>(qp + 16 * ks + 8 * hh);
     }
     const int n_end = CAUSAL ? min(S, q0 + 128) : S;
     const int ntiles = (n_end + 63) / 64;
@@ -85,6 +81,14 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     const DmaVoff<4> vo = dma_voff<4>(ld_kv, wu, l);
     dma_tile64_buf(kbase, hbytes, vo, 0, ld_kv, Ks, wu);
     dma_tile64_buf(vbase, hbytes, vo, 0, ld_kv, Vs, wu);
+    // Q fragments (B operand of S^T = K.Q^T), softmax scale * log2(e) folded in
+    bf16x8 qf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        float x[8];
+        unpack8(qr[ks], x);
+        qf[ks] = __builtin_bit_cast(bf16x8, pack8(x, scale_log2));
+    }
     __syncthreads();
     for (int t = 0; t < ntiles; ++t) {
         const int cur = t & 1, n0 = t * 64;
@@ -173,8 +177,8 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                                  pf[kk], o[dt]);
             }
         }
-
-        __syncthreads();
+        // no barrier after the last (diagonal) tile: a wave done with it does not wait for the others
+        if (t + 1 < ntiles) __syncthreads();
     }
 
     // ---- epilogue: O = O^T / l (query on the lane, 4 consecutive d per register group), LSE = m + log2 l

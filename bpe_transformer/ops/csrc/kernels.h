@@ -166,5 +166,7 @@ void launch_fa_bwd(const FaArgs& a, hipStream_t s);
 bool fa_bwd_split_active(int D);
 // D = 64 backward form 0 split / 1 fused; negative = unchanged; returns the form in force before the call
 int fa_bwd_config(int mode);
+// per-workgroup s_memtime stamps of the last split-backward launch (BPE_FA_STAMPS builds only; false otherwise)
+bool fa_read_stamps(long long* host, int n);
 // whether FaArgs::dkv_part (GQA fp32 dK / dV partials of the fused backward) must be set
 bool fa_dkv_partials_needed(int D);

@@ -97,3 +97,16 @@ def test_shipped_library_matches_tree():
     if not B.LIB.exists():
         pytest.skip("library not built")
     assert B.read_stamp(B.LIB) == B.source_digest()
+
+
+def test_shipped_library_loads_on_cpu():
+    """The library resolves every symbol (dlopen, no GPU needed): an undefined symbol -- e.g. a declaration that
+    landed in an anonymous namespace -- would otherwise only show up on the GPU box."""
+    import subprocess
+    import sys
+
+    if not B.LIB.exists():
+        pytest.skip("library not built")
+    code = f"import torch; torch.ops.load_library({str(B.LIB)!r}); print(hasattr(torch.ops.bpe_hip, 'fa_fwd'))"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("True"), r.stderr[-2000:]
