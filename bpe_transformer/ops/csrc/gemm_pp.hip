@@ -340,10 +340,14 @@ __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2
 // SPLIT (spread mode 2, the weight-gradient layout): the second piece of each
 // pair is issued by the same wave in its MFMA section,
 // between the two halves of the quadrant, so a load section carries one piece; the waits become vmcnt(3).
+// FIRST: K-tile 0 of a tile, whose image was retired (vmcnt(0)) before the loop.  Its phases 0-1 would only retire
+// pieces of that image, so they wait for LDS only; phases 2-3 retire the first pieces of K-tile 1 (read before any
+// wait of K-tile 1) as always.  In the persistent kernel this lets the previous tile's epilogue stores, which
+// share the vmcnt counter with the DMA, drain during the first two phases instead of before them.
 template <bool AK, bool BKM, int DIAG, bool SPLIT = false, int F8 = 0>
 __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
                                              const __bf16* an, const __bf16* bn, const SpreadOff& so, int g, int wl,
-                                             int l, f32x4 (&acc)[8][4]) {
+                                             int l, f32x4 (&acc)[8][4], bool first = false) {
     Frags f;
     char* Ac = cur;
     char* Bc = cur + OPB;
@@ -351,13 +355,14 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     // one phase: fragment reads (done by the caller), pieces of (tile, off, img, lbase), wait, barrier, MFMAs
     auto phase = [&](const __bf16* t0, const int (&off)[2], char* img, int lb, int m, int n, bool last_nodma_wait2) {
         if (dma) {
-            if constexpr (SPLIT) {
-                dma_one(t0, off[0], img, lb);
-                asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
-            } else {
-                dma_pair(t0, off, img, lb);
-                asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-            }
+            if constexpr (SPLIT) dma_one(t0, off[0], img, lb);
+            else dma_pair(t0, off, img, lb);
+        }
+        if (first && m == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else if (dma) {
+            if constexpr (SPLIT) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
         } else if (last_nodma_wait2) {
             asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
         } else {
@@ -400,6 +405,29 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
 // columns are 128 columns of g and the SAME 128 columns of u (B rows [128 t, +128) and [F + 128 t, +128) of
 // [W1; W3]), so the epilogue writes both halves of gu and the gate a from one tile -- the separate swiglu_fwd
 // pass over gu (read 2F, write F per token) disappears.  Same rounding as swiglu_fwd_kernel (a from bf16 g, u).
+// Per-workgroup s_memtime stamps (a diagnostic variant build: ops.build --variant stamps -D BPE_GPP_STAMPS; read
+// by benchmarks/gemm_stamps.py): slot 0 entry, 1 prologue retired, 2 main loop done, 3 epilogue staged, 4 stores
+// issued, 6 work id, 7 hardware XCC id.  Thread 0 writes them (wave 0's view of the workgroup).
+#ifdef BPE_GPP_STAMPS
+__device__ long long g_gpp_stamps[65536 * 8];
+#define GPP_STAMP(i)                                                                                       \
+    do {                                                                                                   \
+        if (threadIdx.x == 0) g_gpp_stamps[(long)(blockIdx.x & 65535) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define GPP_STAMP_VAL(i, v)                                                                                \
+    do {                                                                                                   \
+        if (threadIdx.x == 0) g_gpp_stamps[(long)(blockIdx.x & 65535) * 8 + (i)] = (v);                      \
+    } while (0)
+#define GPP_STAMP_T(t, i)                                                                                  \
+    do {                                                                                                   \
+        if (threadIdx.x == 0) g_gpp_stamps[(long)((t) & 65535) * 8 + (i)] = __builtin_amdgcn_s_memtime();    \
+    } while (0)
+#else
+#define GPP_STAMP(i)
+#define GPP_STAMP_VAL(i, v)
+#define GPP_STAMP_T(t, i)
+#endif
+
 enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2 };
 struct Epi {
     const __bf16* gu;
@@ -412,6 +440,119 @@ struct Epi {
     const float* sa = nullptr;  // F8: device-resident per-tensor inverse scales of A and B (output x sa x sb)
     const float* sb = nullptr;
 };
+
+// bf16 epilogue: the tile is staged through LDS at stg as [256 / NPASS][512 B] images (16-byte chunk c of row i at
+// c ^ (i & 15)) and written back as whole rows.  NPASS 1: the whole tile at once (128 KiB, the one-tile kernel);
+// NPASS 2: group h's rows [128 h, +128) in pass h through one 64 KiB image (the persistent kernel, whose other
+// stage already holds the next tile's K-tile 0).  Raw barriers with LDS-only waits: the stores of a pass stay in
+// flight.  TAIL: a barrier after the last pass too (the image is the next tile's DMA target).
+template <int EPI, int F8, int NPASS>
+__device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* stg, int g, int wl, int l, int tid,
+                                              int i0, int j0, int jb, __bf16* C, long ldc, float beta, const Epi& ep,
+                                              bool st_on, bool tail, int sid) {
+    constexpr int RP = BT / NPASS;  // tile rows per pass
+    float osc = 1.f;  // F8: the product of the operands' inverse scales (device-resident, one load)
+    if constexpr (F8 != 0) osc = ep.sa[0] * ep.sb[0];
+#pragma unroll
+    for (int h = 0; h < NPASS; ++h) {
+        const int r0 = h * RP;  // first tile row of this pass
+        if (NPASS == 1 || g == h) {
+#pragma unroll
+            for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+                for (int jq = 0; jq < 4; ++jq) {
+                    const int i = 128 * g + 16 * ib + (l & 15) - r0;
+                    const int j = 64 * wl + 16 * jq + 4 * (l >> 4);
+                    const f32x4 v = F8 != 0 ? acc[ib][jq] * osc : acc[ib][jq];
+                    const u16x4 p = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+                    *reinterpret_cast<u16x4*>(stg + i * 512 + ((((j >> 3) ^ (i & 15))) << 4) + ((j & 7) << 1)) = p;
+                }
+        }
+        if constexpr (EPI == EPI_SWIGLU_BWD) {
+            // every g / u load of this thread's row segments is issued before the barrier (the accumulators are in
+            // LDS now, their registers free): one memory round trip per pass instead of one per unrolled group of
+            // rows, overlapped with the other waves' staging writes
+            constexpr int NQ = 16 / NPASS;
+            const int c = tid & 31;
+            u16x8 gv[NQ], uv[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const long ro = (long)(i0 + r0 + q * 16 + (tid >> 5)) * ep.ld + j0 + c * 8;
+                gv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro));  // read once
+                uv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F));
+            }
+            // raw barrier after the staging writes only: __syncthreads() would also wait for the loads (vmcnt(0))
+            // before the first row's math; this way row q waits for its own pair (in-order vmcnt) and its math and
+            // stores overlap the later rows' loads
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
+            bar();
+            if (h == 0) GPP_STAMP_T(sid, 3);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int i = q * 16 + (tid >> 5);
+                const u16x8 v = *reinterpret_cast<const u16x8*>(stg + i * 512 + ((c ^ (i & 15)) << 4));
+                const long ro = (long)(i0 + r0 + i) * ep.ld + j0 + c * 8;
+                u16x8 dg, du;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float gg = bf2f(gv[q][e]), uu = bf2f(uv[q][e]), d = bf2f(v[e]);
+                    const float sg = fast_sigmoid(gg);
+                    du[e] = f2bf(d * (gg * sg));
+                    dg[e] = f2bf(d * uu * sg * (1.f + gg * (1.f - sg)));
+                }
+                if (st_on) {
+                    *reinterpret_cast<u16x8*>(ep.dgu + ro) = dg;
+                    *reinterpret_cast<u16x8*>(ep.dgu + ro + ep.F) = du;
+                }
+            }
+        } else if constexpr (EPI == EPI_SWIGLU_FWD) {
+            // row i: g = staged columns [0, 128), u = [128, 256); 16 threads x 16 bytes per 256-byte segment
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            bar();
+            if (h == 0) GPP_STAMP_T(sid, 3);
+            const int c = tid & 15;
+#pragma unroll 4
+            for (int q = 0; q < 8 / NPASS; ++q) {
+                const int i = q * 32 + (tid >> 4);
+                const u16x8 gv = *reinterpret_cast<const u16x8*>(stg + i * 512 + ((c ^ (i & 15)) << 4));
+                const u16x8 uv = *reinterpret_cast<const u16x8*>(stg + i * 512 + (((16 + c) ^ (i & 15)) << 4));
+                u16x8 av;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float gg = bf2f(gv[e]);
+                    av[e] = f2bf(gg * fast_sigmoid(gg) * bf2f(uv[e]));
+                }
+                const long r = i0 + r0 + i;
+                // gu is next read by the backward, long after this step's forward: streaming stores
+                if (st_on) {
+                    st_stream(reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + jb + c * 8), gv);
+                    st_stream(reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + ep.F + jb + c * 8), uv);
+                    *reinterpret_cast<u16x8*>(ep.act + r * ep.ld_act + jb + c * 8) = av;
+                }
+            }
+        } else {
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            bar();
+            if (h == 0) GPP_STAMP_T(sid, 3);
+#pragma unroll 4
+            for (int q = 0; q < 16 / NPASS; ++q) {
+                const int i = q * 16 + (tid >> 5), c = tid & 31;
+                u16x8 v = *reinterpret_cast<const u16x8*>(stg + i * 512 + ((c ^ (i & 15)) << 4));
+                __bf16* cp = C + (long)(i0 + r0 + i) * ldc + j0 + c * 8;
+                if (beta != 0.f) {
+                    const u16x8 o = *reinterpret_cast<const u16x8*>(cp);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + beta * bf2f(o[e]));
+                }
+                if (st_on) *reinterpret_cast<u16x8*>(cp) = v;
+            }
+        }
+        if (h + 1 < NPASS || tail) {  // every read of the image retired before it is rewritten
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            bar();
+        }
+    }
+}
 
 template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, int SPREAD = 0, int F8 = 0>
 __global__ void __launch_bounds__(NT, 1)
@@ -435,6 +576,17 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     const int nkt = R / BK;
     const int kb = (int)((long)split * nkt / splits);
     const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
+    GPP_STAMP(0);
+    GPP_STAMP_VAL(6, wid);
+#ifdef BPE_GPP_STAMPS
+    {
+        unsigned xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        GPP_STAMP_VAL(7, (long long)(xcc & 15));
+        GPP_STAMP_VAL(5, (long long)hw);
+    }
+#endif
 
     constexpr bool SPR = SPREAD != 0;
     if (ep.prio && g == 1) __builtin_amdgcn_s_setprio(1);  // g is wave-uniform (readfirstlane): a scalar branch
@@ -469,6 +621,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bar();
         }
+        GPP_STAMP(1);
         if (g == 1) bar();  // the stagger
         for (int kt = 0; kt < nk; ++kt) {
             char* cur = smem + (kt & 1) * STAGE;
@@ -503,6 +656,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
                                  wl, l, acc);
         }
     }
+    GPP_STAMP(2);
     if (g == 0 && DIAG != 4) bar();
     // every fragment read and LDS-DMA done: the LDS is free for the epilogue.  The builtin (not inline asm)
     // tells the compiler's wait-count model that the DMA has retired; after an asm wait it still counts the
@@ -512,6 +666,8 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     __builtin_amdgcn_s_waitcnt(0x70);  // vmcnt(0) expcnt(7) lgkmcnt(0)
     bar();
 
+    // DIAG 6 (timing only): the epilogue's global stores are skipped (kept in the code behind a runtime test
+    // that is never true, so the MFMAs and the LDS staging stay): prices the store burst at the end of each tile
     // DIAG 6 (timing only): the epilogue's global stores are skipped (kept in the code behind a runtime test
     // that is never true, so the MFMAs and the LDS staging stay): prices the store burst at the end of each tile
     const bool st_on = DIAG != 6 || ep.prio == 77;
@@ -527,98 +683,120 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
                 if (st_on) *reinterpret_cast<f32x4*>(sp + i * N + j) = acc[ib][jb];
             }
     } else {
-        float osc = 1.f;  // F8: the product of the operands' inverse scales (device-resident, one load)
-        if constexpr (F8 != 0) osc = ep.sa[0] * ep.sb[0];
-        // stage bf16 tile as [256][512 B], 16-byte chunk c of row i at c ^ (i & 15)
-#pragma unroll
-        for (int ib = 0; ib < 8; ++ib)
-#pragma unroll
-            for (int jb = 0; jb < 4; ++jb) {
-                const int i = 128 * g + 16 * ib + (l & 15);
-                const int j = 64 * wl + 16 * jb + 4 * (l >> 4);
-                const f32x4 v = F8 != 0 ? acc[ib][jb] * osc : acc[ib][jb];
-                const u16x4 p = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-                *reinterpret_cast<u16x4*>(smem + i * 512 + ((((j >> 3) ^ (i & 15))) << 4) + ((j & 7) << 1)) = p;
-            }
-        if constexpr (EPI == EPI_SWIGLU_BWD) {
-            // every g / u load of this thread's 16 row segments is issued before the barrier (the accumulators
-            // are in LDS now, their registers free): one memory round trip for the tile instead of one per
-            // unrolled group of rows, overlapped with the other waves' staging writes
-            const int c = tid & 31;
-            u16x8 gv[16], uv[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const long ro = (long)(i0 + q * 16 + (tid >> 5)) * ep.ld + j0 + c * 8;
-                gv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro));  // read once
-                uv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F));
-            }
-            // raw barrier after the staging writes only: __syncthreads() would also wait for all 32 loads
-            // (vmcnt(0)) before the first row's math; this way row q waits for its own pair (in-order vmcnt)
-            // and its math and stores overlap the later rows' loads
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
-            bar();
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int i = q * 16 + (tid >> 5);
-                const u16x8 v = *reinterpret_cast<const u16x8*>(smem + i * 512 + ((c ^ (i & 15)) << 4));
-                const long ro = (long)(i0 + i) * ep.ld + j0 + c * 8;
-                u16x8 dg, du;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float gg = bf2f(gv[q][e]), uu = bf2f(uv[q][e]), d = bf2f(v[e]);
-                    const float sg = fast_sigmoid(gg);
-                    du[e] = f2bf(d * (gg * sg));
-                    dg[e] = f2bf(d * uu * sg * (1.f + gg * (1.f - sg)));
-                }
-                *reinterpret_cast<u16x8*>(ep.dgu + ro) = dg;
-                *reinterpret_cast<u16x8*>(ep.dgu + ro + ep.F) = du;
-            }
-            return;
-        }
-        if constexpr (EPI == EPI_SWIGLU_FWD) {
-            // row i: g = staged columns [0, 128), u = [128, 256); 16 threads x 16 bytes per 256-byte segment
-            __syncthreads();
-            const int c = tid & 15;
-#pragma unroll 4
-            for (int q = 0; q < 8; ++q) {
-                const int i = q * 32 + (tid >> 4);
-                const u16x8 gv = *reinterpret_cast<const u16x8*>(smem + i * 512 + ((c ^ (i & 15)) << 4));
-                const u16x8 uv = *reinterpret_cast<const u16x8*>(smem + i * 512 + (((16 + c) ^ (i & 15)) << 4));
-                u16x8 av;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float gg = bf2f(gv[e]);
-                    av[e] = f2bf(gg * fast_sigmoid(gg) * bf2f(uv[e]));
-                }
-                const long r = i0 + i;
-                // gu is next read by the backward, long after this step's forward: streaming stores
-                st_stream(reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + jb + c * 8), gv);
-                st_stream(reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + ep.F + jb + c * 8), uv);
-                *reinterpret_cast<u16x8*>(ep.act + r * ep.ld_act + jb + c * 8) = av;
-            }
-            return;
-        }
-        __syncthreads();
-#pragma unroll 4
-        for (int q = 0; q < 16; ++q) {
-            const int i = q * 16 + (tid >> 5), c = tid & 31;
-            u16x8 v = *reinterpret_cast<const u16x8*>(smem + i * 512 + ((c ^ (i & 15)) << 4));
-            __bf16* cp = C + (long)(i0 + i) * ldc + j0 + c * 8;
-            if (beta != 0.f) {
-                const u16x8 o = *reinterpret_cast<const u16x8*>(cp);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + beta * bf2f(o[e]));
-            }
-            if (st_on) *reinterpret_cast<u16x8*>(cp) = v;
-        }
+        epilogue_bf16<EPI, F8, 1>(acc, smem, g, wl, l, tid, i0, j0, jb, C, ldc, beta, ep, st_on, false, blockIdx.x);
+        GPP_STAMP(4);
     }
 }
 
 
-// (A persistent form -- one workgroup per CU walking its tiles with the K-tile prefetch running across tile seams
-// and the previous tile's accumulators stored from registers during the next tile -- ran the K = 768 forward GEMMs
-// at 1.19-1.37 PF/s without its output stores but 0.74-0.89 with them: the 8-byte stores of 32 accumulators per lane
-// cost more than the overlap gained.  It was removed; docs/performance.md, ping-pong GEMM.)
+// Persistent form of the bf16 (or fp8) one-pass GEMM: one workgroup per CU walks tiles wid, wid + grid, ... (the
+// same tile order as the one-tile kernel's XCD-aware grid).  What it removes, measured with the stamps build at
+// GPT-2 B 128 (benchmarks/gemm_stamps.py): a one-tile workgroup spends ~10-12 % of its time in the prologue (K-tile
+// 0's round trip) and then ~2-3k cycles pass before the CU's next workgroup runs.  Here the next tile's K-tile 0
+// is DMA'd during the last K-tile of the current one (the in-loop prefetch simply continues across the seam), so
+// its image is resident before the epilogue; the epilogue stages through the other 64 KiB stage in two passes
+// (NPASS 2), and its stores stay in flight into the first two phases of the next tile's K-tile 0 (which wait for
+// LDS only); phase 2's vmcnt wait retires them.
+// (An earlier persistent form stored the accumulators from registers as 8-byte row pieces during the next tile's
+// first load section and lost to the one-tile kernel: 0.74-0.89 vs 1.0 PF/s on the K = 768 forward GEMMs.)
+template <bool AK, bool BKM, int EPI, int SPREAD, int F8 = 0>
+__global__ void __launch_bounds__(NT, 1)
+gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
+                       __bf16* __restrict__ C, long ldc, float beta, int M, int N, int R, Epi ep = Epi{}) {
+    static_assert(SPREAD != 0, "the persistent kernel runs the spread DMA schedule");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = w >> 2, wl = w & 3;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    const int tiles_n = N / BT;
+    const int ntiles = (M / BT) * tiles_n;
+    const int nk = R / BK;
+    if (ep.prio && g == 1) __builtin_amdgcn_s_setprio(1);
+    SpreadOff so = spread_offsets<AK, BKM>(g, wl, l, (int)lda, (int)ldb);
+    if constexpr (EPI == EPI_SWIGLU_FWD) {
+        static_assert(BKM, "SwiGLU forward: B = [W1; W3] is K-major");
+        if (g == 1) {
+            const int du = (ep.F - BT / 2) * (int)ldb;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                so.b0[j] += du;
+                so.b1[j] += du;
+            }
+        }
+    }
+    // tile t: output origin (i0, j0) and B origin jb (EPI_SWIGLU_FWD: 128 g columns + the matching u columns)
+    auto origin = [&](int t, int& i0, int& j0, int& jb) {
+        i0 = (t / tiles_n) * BT;
+        j0 = (t % tiles_n) * BT;
+        jb = EPI == EPI_SWIGLU_FWD ? (t % tiles_n) * (BT / 2) : j0;
+    };
+    int t = wid, i0, j0, jb;
+    origin(t, i0, j0, jb);
+    {  // prologue of the first tile: all of its K-tile 0, retired before the first read
+        const __bf16* a0 = tile_ptr<AK>(A, lda, i0, 0);
+        const __bf16* b0 = tile_ptr<BKM>(B, ldb, jb, 0);
+        dma_pair(a0, so.a0, smem, so.la0);
+        dma_pair(b0, so.b0, smem + OPB, so.lb0);
+        dma_pair(b0, so.b1, smem + OPB, so.lb1);
+        dma_pair(a0, so.a1, smem, so.la1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+    }
+    int st = 0;  // the stage holding the current K-tile
+    f32x4 acc[8][4];
+#ifdef BPE_GPP_STAMPS
+    unsigned xcc_id, hw_id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+#endif
+    for (;;) {
+        GPP_STAMP_T(t, 0);
+#ifdef BPE_GPP_STAMPS
+        if (threadIdx.x == 0) {
+            g_gpp_stamps[(long)(t & 65535) * 8 + 5] = hw_id;
+            g_gpp_stamps[(long)(t & 65535) * 8 + 6] = wid;
+            g_gpp_stamps[(long)(t & 65535) * 8 + 7] = xcc_id & 15;
+        }
+#endif
+        const int tn = t + nwg;
+        const bool more = tn < ntiles;
+        int i0n = i0, j0n = j0, jbn = jb;
+        if (more) origin(tn, i0n, j0n, jbn);
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (g == 1) bar();  // the stagger
+        GPP_STAMP_T(t, 1);
+        for (int kt = 0; kt < nk; ++kt) {
+            char* cur = smem + st * STAGE;
+            char* nxt = smem + (st ^ 1) * STAGE;
+            const bool last = kt + 1 == nk;
+            // the next K-tile of this tile, or K-tile 0 of the next tile
+            const __bf16* an = last ? tile_ptr<AK>(A, lda, i0n, 0) : tile_ptr<AK>(A, lda, i0, (long)(kt + 1) * BK);
+            const __bf16* bn = last ? tile_ptr<BKM>(B, ldb, jbn, 0) : tile_ptr<BKM>(B, ldb, jb, (long)(kt + 1) * BK);
+            ktile_spread<AK, BKM, 0, SPREAD == 2, F8>(cur, nxt, !last || more, an, bn, so, g, wl, l, acc, kt == 0);
+            st ^= 1;
+        }
+        GPP_STAMP_T(t, 2);
+        if (g == 0) bar();
+        // the next tile's K-tile 0 (stage st) retired; the stage just read (st ^ 1) is free for the staging
+        __builtin_amdgcn_s_waitcnt(0x70);
+        bar();
+        epilogue_bf16<EPI, F8, 2>(acc, smem + (st ^ 1) * STAGE, g, wl, l, tid, i0, j0, jb, C, ldc, beta, ep, true,
+                                  more, t);
+        GPP_STAMP_T(t, 4);
+        if (!more) break;
+        t = tn;
+        i0 = i0n;
+        j0 = j0n;
+        jb = jbn;
+    }
+}
+
 }  // namespace gpp
 }  // namespace bpe
 
@@ -632,6 +810,41 @@ static int prio_mode() { return 1; }
 // profiles/bench/ab_gpp_dma_split.log).  0, the burst schedule of ktile, serves the DIAG 5 build only.
 static int spread_mode(bool weight_grad = false) { return weight_grad ? 2 : 1; }
 
+// Persistent kernel (gemm_pp_persist_kernel) for the one-pass bf16 / fp8 GEMMs: 1 = on (one workgroup per CU),
+// 0 = the one-tile kernel, n >= 2 = on with at most n workgroups (tests: many tiles per workgroup on small shapes).
+#ifndef BPE_GPP_PERSIST  // build define: the default form (variant builds A/B the one-tile kernel with 0)
+#define BPE_GPP_PERSIST 1
+#endif
+static int g_persist = BPE_GPP_PERSIST;
+int gpp_persist_config(int mode) {
+    const int prev = g_persist;
+    if (mode >= 0) g_persist = mode;
+    return prev;
+}
+
+static int num_cus() {
+    static int n[16] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int& c = n[dev & 15];
+    if (c == 0 && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) c = 256;
+    return c;
+}
+
+// launch the persistent kernel k over ntiles tiles: one workgroup per CU
+template <typename K, typename... Args>
+static void launch_persist(K* k, int ntiles, hipStream_t s, Args... args) {
+    static_assert(sizeof...(Args) > 0, "");
+    const int cap = g_persist >= 2 ? g_persist : num_cus();  // mode >= 2: a test hook, at most `mode` workgroups
+    const int grid = ntiles < cap ? ntiles : cap;
+    k<<<grid, NT, LDS_BYTES, s>>>(args...);
+}
+
+template <typename K>
+static void lds_attr(K* k) {  // > 64 KiB dynamic LDS must be opted into once per instantiation
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+}
+
 // dgu = swiglu_bwd(dY . W2, gu): A = dY [M][R] (K-major), B = W2 [R][F] (MN-major)
 void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ldw, const void* gu, void* dgu,
                                long ldg, int M, int F, int R, hipStream_t s) {
@@ -644,6 +857,13 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
     const int grid = (M / BT) * (F / BT);
     Epi ep{(const __bf16*)gu, (__bf16*)dgu, ldg, F};
     ep.prio = prio_mode();
+    if (g_persist) {
+        static bool pattr = false;
+        auto* kp = &gemm_pp_persist_kernel<true, false, EPI_SWIGLU_BWD, 1>;
+        if (!pattr) lds_attr(kp), pattr = true;
+        return launch_persist(kp, grid, s, (const __bf16*)dY, ldy, (const __bf16*)W2, ldw, (__bf16*)nullptr, 0L, 0.f,
+                              M, F, R, ep);
+    }
     k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)dY, ldy, (const __bf16*)W2, ldw, nullptr, nullptr, 0, 0.f, M, F, R,
                                   1, ep);
 }
@@ -660,6 +880,13 @@ void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ld
     const int grid = (M / BT) * (F / (BT / 2));
     Epi ep{nullptr, (__bf16*)gu, ldg, F, (__bf16*)act, lda_};
     ep.prio = prio_mode();
+    if (g_persist) {
+        static bool pattr = false;
+        auto* kp = &gemm_pp_persist_kernel<true, true, EPI_SWIGLU_FWD, 1>;
+        if (!pattr) lds_attr(kp), pattr = true;
+        return launch_persist(kp, grid, s, (const __bf16*)X, ldx, (const __bf16*)W13, ldw, (__bf16*)nullptr, 0L, 0.f,
+                              M, 2 * F, R, ep);
+    }
     k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)X, ldx, (const __bf16*)W13, ldw, nullptr, nullptr, 0, 0.f, M, 2 * F,
                                   R, 1, ep);
 }
@@ -682,6 +909,15 @@ void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, 
     ep.sa = sa;
     ep.sb = sb;
     // the fp8 rows as bf16 rows of half the length: R = K / 2 "bf16" elements = K / 128 K-tiles of 128 fp8
+    if (g_persist) {
+        static bool pattr1 = false, pattr2 = false;
+        auto* kp = fmt_a == 1 ? &gemm_pp_persist_kernel<true, true, EPI_NONE, 1, 2>
+                              : &gemm_pp_persist_kernel<true, true, EPI_NONE, 1, 1>;
+        bool& pa = fmt_a == 1 ? pattr2 : pattr1;
+        if (!pa) lds_attr(kp), pa = true;
+        return launch_persist(kp, (M / BT) * (N / BT), s, (const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2,
+                              (__bf16*)C, ldc, 0.f, M, N, K / 2, ep);
+    }
     k<<<(M / BT) * (N / BT), NT, LDS_BYTES, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, nullptr,
                                                   (__bf16*)C, ldc, 0.f, M, N, K / 2, 1, ep);
 }
@@ -703,6 +939,14 @@ static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, fl
     const int grid = (M / BT) * (N / BT) * splits;
     Epi ep{};
     ep.prio = prio_mode();
+    if constexpr (!SLAB && DIAG == 0 && SPREAD != 0) {
+        if (g_persist) {
+            static bool pattr = false;
+            auto* kp = &gemm_pp_persist_kernel<AK, BKM, EPI_NONE, SPREAD>;
+            if (!pattr) lds_attr(kp), pattr = true;
+            return launch_persist(kp, grid, s, a, lda, b, ldb, c, ldc, beta, M, N, R, ep);
+        }
+    }
     k<<<grid, NT, LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, ep);
 }
 
@@ -741,4 +985,17 @@ void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const v
         else { if (b_kmajor) L(false, true, false); else L(false, false, false); }
     }
 #undef L
+}
+
+// copy the last gemm_pp launch's stamps out (BPE_GPP_STAMPS builds; false otherwise)
+bool gpp_read_stamps(long long* host, int n) {
+#ifdef BPE_GPP_STAMPS
+    (void)hipDeviceSynchronize();
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(bpe::gpp::g_gpp_stamps), (size_t)n * 8 * sizeof(long long), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess;
+#else
+    (void)host;
+    (void)n;
+    return false;
+#endif
 }

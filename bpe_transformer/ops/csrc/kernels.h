@@ -168,5 +168,10 @@ bool fa_bwd_split_active(int D);
 int fa_bwd_config(int mode);
 // per-workgroup s_memtime stamps of the last split-backward launch (BPE_FA_STAMPS builds only; false otherwise)
 bool fa_read_stamps(long long* host, int n);
+// per-workgroup s_memtime stamps of the last gemm_pp launch (BPE_GPP_STAMPS builds only; false otherwise)
+bool gpp_read_stamps(long long* host, int n);
+// gemm_pp: 1 = persistent kernel for the one-pass bf16 / fp8 GEMMs, 0 = one tile per workgroup; -1 queries.
+// Returns the previous mode.
+int gpp_persist_config(int mode);
 // whether FaArgs::dkv_part (GQA fp32 dK / dV partials of the fused backward) must be set
 bool fa_dkv_partials_needed(int D);

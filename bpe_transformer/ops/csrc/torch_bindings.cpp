@@ -600,10 +600,17 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
 bool fa_bwd_needs_dq_acc(int64_t D) { return !fa_bwd_split_active((int)D); }
 int64_t fa_fwd_config_op(int64_t ver) { return fa_fwd_config((int)ver); }
 int64_t fa_bwd_config_op(int64_t mode) { return fa_bwd_config((int)mode); }
+int64_t gpp_persist_config_op(int64_t mode) { return gpp_persist_config((int)mode); }
 // [n, 8] int64 stamps of the last split-backward kernel (a BPE_FA_STAMPS variant build), or an empty tensor
 at::Tensor fa_stamps_op(int64_t n) {
     auto t = at::empty({n, 8}, at::TensorOptions().dtype(at::kLong));
     if (!fa_read_stamps(reinterpret_cast<long long*>(t.data_ptr<int64_t>()), (int)n)) return at::empty({0, 8}, t.options());
+    return t;
+}
+// the same for the last gemm_pp kernel (a BPE_GPP_STAMPS variant build)
+at::Tensor gpp_stamps_op(int64_t n) {
+    auto t = at::empty({n, 8}, at::TensorOptions().dtype(at::kLong));
+    if (!gpp_read_stamps(reinterpret_cast<long long*>(t.data_ptr<int64_t>()), (int)n)) return at::empty({0, 8}, t.options());
     return t;
 }
 
@@ -884,6 +891,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("fa_bwd_needs_dq_acc(int D) -> bool", &fa_bwd_needs_dq_acc);  // no tensors: a catch-all kernel
     m.def("fa_bwd_config(int mode=-1) -> int", &fa_bwd_config_op);
     m.def("fa_stamps(int n) -> Tensor", &fa_stamps_op);
+    m.def("gpp_stamps(int n) -> Tensor", &gpp_stamps_op);
+    m.def("gpp_persist_config(int mode=-1) -> int", &gpp_persist_config_op);
     m.def("fa_fwd_config(int ver=0) -> int", &fa_fwd_config_op);
 }
 

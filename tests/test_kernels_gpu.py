@@ -390,7 +390,17 @@ def test_transpose_bf16(gpu_device, shape):
         assert torch.equal(t.cpu(), w.t().cpu())
 
 
-def test_gemm_swiglu_bwd(gpu_device):
+@pytest.fixture(params=[0, 1, 3], ids=["tile", "persist", "persist3"])
+def gpp_mode(request, gpu_device):
+    """gemm_pp kernel form: one tile per workgroup, persistent (one workgroup per CU), persistent with 3
+    workgroups (several tiles each, unevenly split, even on small shapes)."""
+    h = torch.ops.bpe_hip
+    prev = h.gpp_persist_config(request.param)
+    yield request.param
+    h.gpp_persist_config(prev)
+
+
+def test_gemm_swiglu_bwd(gpu_device, gpp_mode):
     """dY @ W2 with the SwiGLU backward in the epilogue vs the fp32 oracle of the same two steps."""
     torch.manual_seed(2)
     M, d, F = 512, 192, 768
@@ -408,7 +418,7 @@ def test_gemm_swiglu_bwd(gpu_device):
 
 
 @pytest.mark.parametrize("M,d,F", [(512, 192, 768), (256, 64, 128)])
-def test_gemm_swiglu_fwd(gpu_device, M, d, F):
+def test_gemm_swiglu_fwd(gpu_device, gpp_mode, M, d, F):
     """x @ [W1; W3]^T with a = silu(g) * u in the epilogue.  Small-integer operands make gu exact, so gu must
     equal the plain product bitwise and a must equal the unfused swiglu_fwd of it; random operands are
     compared with the fp32 oracle of the same two steps."""
@@ -428,9 +438,38 @@ def test_gemm_swiglu_fwd(gpu_device, M, d, F):
     assert rel(a.cpu(), (g * torch.sigmoid(g) * u).cpu()) < 2e-2
 
 
+def test_gemm_pp_persistent_bitwise_many_tiles(gpu_device):
+    """More tiles than CUs (every workgroup walks several, the last round partial): the persistent kernel runs the
+    same per-tile MFMA sequence as the one-tile kernel, so plain, SwiGLU-forward and SwiGLU-backward outputs must
+    match it bitwise."""
+    h = torch.ops.bpe_hip
+    torch.manual_seed(5)
+    M, d, F = 8448, 768, 1024  # 33 x 9 = 297 plain tiles, 33 x 8 = 264 SwiGLU-forward, 33 x 4 = 132 backward
+    x = torch.randn(M, d, device=gpu_device, dtype=torch.bfloat16)
+    w = (0.05 * torch.randn(2304, d, device=gpu_device)).to(torch.bfloat16)
+    w13 = (0.05 * torch.randn(2 * F, d, device=gpu_device)).to(torch.bfloat16)
+    w2 = (0.05 * torch.randn(d, F, device=gpu_device)).to(torch.bfloat16)
+    dy = torch.randn(M, d, device=gpu_device, dtype=torch.bfloat16)
+    outs = {}
+    prev = h.gpp_persist_config(0)
+    try:
+        for mode in (0, 1):
+            h.gpp_persist_config(mode)
+            c = torch.empty(M, 2304, device=gpu_device, dtype=torch.bfloat16)
+            h.gemm_pp(x, True, w, True, c, 0.0, 1)
+            gu, a = h.gemm_swiglu_fwd(x, w13)
+            dgu = h.gemm_swiglu_bwd(dy, w2, gu)
+            outs[mode] = (c, gu, a, dgu)
+    finally:
+        h.gpp_persist_config(prev)
+    for t0, t1 in zip(outs[0], outs[1]):
+        assert torch.equal(t0, t1)
+    assert rel(outs[1][0].cpu(), (x.float() @ w.float().t()).cpu()) < 1e-2
+
+
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("splits", [1, 3])
-def test_gemm_pp_exact(gpu_device, a_k, b_k, splits):
+def test_gemm_pp_exact(gpu_device, gpp_mode, a_k, b_k, splits):
     """Ping-pong GEMM on small-integer operands: every output is exact, so any layout/index slip shows."""
     torch.manual_seed(1)
     M, N, R = 512, 768, 448
@@ -445,7 +484,7 @@ def test_gemm_pp_exact(gpu_device, a_k, b_k, splits):
 
 
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
-def test_gemm_pp_random(gpu_device, a_k, b_k):
+def test_gemm_pp_random(gpu_device, gpp_mode, a_k, b_k):
     torch.manual_seed(0)
     M, N, R = 1024, 512, 1536
     A = torch.randn(M, R, device=gpu_device, dtype=torch.bfloat16)
@@ -781,7 +820,7 @@ def test_update_scales(gpu_device):
 # ---------------------------------------------------------------- hand-written fp8 GEMM (gemm_pp.hip, F8)
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 256, 384), (256, 768, 1024)])
 @pytest.mark.parametrize("fmt_a", ["e4m3", "e5m2"])
-def test_gemm_fp8_exact(gpu_device, M, N, K, fmt_a):
+def test_gemm_fp8_exact(gpu_device, gpp_mode, M, N, K, fmt_a):
     """y = (a8 @ b8^T) * sa * sb on the fp8 MFMA ping-pong kernel, exact on small-integer operands (fp32 sums of
     integers are exact; the bf16 output is the round-to-nearest of the exact value) with power-of-two scales:
     checks the fragment / k mapping of v_mfma_scale_f32_16x16x128_f8f6f4 for both operand formats."""
@@ -801,7 +840,7 @@ def test_gemm_fp8_exact(gpu_device, M, N, K, fmt_a):
     assert torch.equal(y.cpu(), ref)
 
 
-def test_gemm_fp8_random_vs_dequantised(gpu_device):
+def test_gemm_fp8_random_vs_dequantised(gpu_device, gpp_mode):
     """Random e4m3 operands at a Llama projection shape against the fp32 product of the dequantised operands."""
     torch.manual_seed(7)
     M, N, K = 1024, 2560, 2048
