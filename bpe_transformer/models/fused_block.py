@@ -5,8 +5,8 @@ One ``autograd.Function`` per transformer block instead of ~10 autograd nodes:
 forward (x = xr + xd: the previous block's residual and its not-yet-added FFN output)::
 
     x, h1 = add_rmsnorm(xr, xd; ln1)  HIP (the residual add fused into the norm)
-    qkv = h1 @ [Wq;Wk;Wv]^T           hipBLASLt (one GEMM; fp8: ops/fp8.py)
-    rope_qk_(qkv)                     HIP, in place on Q / K (D = 64; D = 128 rotates inside attention)
+    qkv = h1 @ [Wq;Wk;Wv]^T, RoPE     our persistent ping-pong GEMM with RoPE on Q / K in its epilogue (D = 64;
+                                      D = 128 rotates inside attention; fp8: ops/fp8.py + the in-place rope_qk_)
     o = flash_attn(qkv)               HIP (csrc/flash_attn_fwd_v4.hip)
     g1 = o @ Wo^T                     hipBLASLt
     xm, h2 = add_rmsnorm(x, g1; ln2)  HIP
@@ -18,8 +18,8 @@ backward: the mirror image, with
   * the SwiGLU backward fused into the epilogue of the dY @ W2 GEMM (our
     ping-pong MFMA kernel): the gate gradient da never goes to HBM;
   * weight gradients ACCUMULATED IN PLACE into the flat gradient buffer
-    (``param.main_grad``, set by the training engine) by ``addmm_`` with
-    beta = 1 -- no temporary dW, no AccumulateGrad add kernels;
+    (``param.main_grad``, set by the training engine) by the per-shape dW
+    route of ops/gemm.py -- no temporary dW, no AccumulateGrad add kernels;
   * the fused [Wq;Wk;Wv] and [W1;W3] weights and their gradients as zero-copy
     views of the flat buffers when the parameters are adjacent there (no
     torch.cat / split);
@@ -89,6 +89,17 @@ def _fuse_swiglu_fwd(x: Tensor, w13: Tensor) -> bool:
             and w13.stride(1) == 1)
 
 
+_FUSE_QKV_ROPE = True  # module flag (tests and A/B runs compare the unfused path)
+
+
+def _fuse_qkv_rope(x: Tensor, w: Tensor, S: int) -> bool:
+    """The QKV projection with RoPE in its epilogue (csrc/gemm_pp.hip EPI_ROPE) instead of hipBLASLt plus the
+    in-place ``rope_qk_`` pass: tokens and the QKV width in multiples of 256, d_model of 64."""
+    return (_FUSE_QKV_ROPE and x.dtype == torch.bfloat16 and x.shape[0] % 256 == 0 and x.shape[0] % S == 0
+            and x.shape[1] % 64 == 0 and w.shape[0] % 256 == 0 and x.stride(1) == 1 and w.stride(1) == 1
+            and x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0)
+
+
 def _dx_tn(w: Tensor) -> bool:
     """Run dX = dY . W as dY . (W^T)^T with W^T materialised (``ops.transpose_bf16``): hipBLASLt's TN layout
     (both operands contiguous along the reduction) beats the NN layout of the stored weight by 10-20 % at the
@@ -136,11 +147,15 @@ class FusedBlockFn(torch.autograd.Function):
                 return r
 
             qkv = mm(h1, w_qkv, 0)
-        else:
-            qkv = torch.matmul(h1, w_qkv.t())
         pre = use_rope and prerotate_default(D)
-        if pre:  # RoPE once, in place on Q / K of the QKV activation (saved rotated for the backward)
-            hip().rope_qk_(qkv, cos, sin, B, S, H, Hkv, D)
+        if fp8 is None and pre and _fuse_qkv_rope(h1, w_qkv, S):
+            # RoPE on Q / K in the projection's epilogue (saved rotated for the backward)
+            qkv = hip().gemm_qkv_rope(h1, w_qkv, cos, sin, S, D, (H + Hkv) * D)
+        else:
+            if fp8 is None:
+                qkv = torch.matmul(h1, w_qkv.t())
+            if pre:  # RoPE once, in place on Q / K of the QKV activation (saved rotated for the backward)
+                hip().rope_qk_(qkv, cos, sin, B, S, H, Hkv, D)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         # training: the forward kernel zeroes the backward's fp32 dQ accumulator in its epilogue (hidden under
         # its compute; the backward pre-pass then only reads O / dO).  Only the fused atomics backward has that

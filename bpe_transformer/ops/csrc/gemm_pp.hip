@@ -428,7 +428,10 @@ __device__ long long g_gpp_stamps[65536 * 8];
 #define GPP_STAMP_T(t, i)
 #endif
 
-enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2 };
+// EPI_ROPE: the QKV projection with RoPE on its Q / K columns (output columns [0, rot_cols)), applied to the
+// bf16-rounded products exactly as rope_qk_kernel (rope.hip) applies it to the stored activation: interleaved
+// pairs, position = row % S, fp32 cos / sin tables [S][D / 2].  Saves the separate in-place pass over Q / K.
+enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2, EPI_ROPE = 3 };
 struct Epi {
     const __bf16* gu;
     __bf16* dgu;  // EPI_SWIGLU_BWD: dgu out; EPI_SWIGLU_FWD: gu out
@@ -439,6 +442,9 @@ struct Epi {
     int prio = 0;  // 1: group 1 (the younger waves 4-7) runs at s_setprio 1 (guide T5, static form)
     const float* sa = nullptr;  // F8: device-resident per-tensor inverse scales of A and B (output x sa x sb)
     const float* sb = nullptr;
+    const float* cosT = nullptr;  // EPI_ROPE: [S][D / 2] tables, S, head dim, rotated column count
+    const float* sinT = nullptr;
+    int S = 0, D = 0, rot_cols = 0;
 };
 
 // bf16 epilogue: the tile is staged through LDS at stg as [256 / NPASS][512 B] images (16-byte chunk c of row i at
@@ -529,6 +535,40 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
                     st_stream(reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + ep.F + jb + c * 8), uv);
                     *reinterpret_cast<u16x8*>(ep.act + r * ep.ld_act + jb + c * 8) = av;
                 }
+            }
+        } else if constexpr (EPI == EPI_ROPE) {
+            // this thread's 8 columns are one quarter of a pair block of one head: the cos / sin loads of its rows
+            // (positions) are issued before the barrier, like the SwiGLU-backward operands
+            constexpr int NQ = 16 / NPASS;
+            const int c = tid & 31;
+            const int col = j0 + c * 8;
+            const bool rot = col < ep.rot_cols;
+            const int pb = (col % ep.D) >> 1;  // first pair of the 8 columns
+            f32x4 cs[NQ], sn[NQ];
+            if (rot) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const long pos = (long)((i0 + r0 + q * 16 + (tid >> 5)) % ep.S) * (ep.D >> 1) + pb;
+                    cs[q] = *reinterpret_cast<const f32x4*>(ep.cosT + pos);
+                    sn[q] = *reinterpret_cast<const f32x4*>(ep.sinT + pos);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            bar();
+            if (h == 0) GPP_STAMP_T(sid, 3);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int i = q * 16 + (tid >> 5);
+                u16x8 v = *reinterpret_cast<const u16x8*>(stg + i * 512 + ((c ^ (i & 15)) << 4));
+                if (rot) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float a = bf2f(v[2 * j]), b = bf2f(v[2 * j + 1]);
+                        v[2 * j] = f2bf(a * cs[q][j] - b * sn[q][j]);
+                        v[2 * j + 1] = f2bf(a * sn[q][j] + b * cs[q][j]);
+                    }
+                }
+                if (st_on) *reinterpret_cast<u16x8*>(C + (long)(i0 + r0 + i) * ldc + col) = v;
             }
         } else {
             __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -889,6 +929,31 @@ void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ld
     }
     k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)X, ldx, (const __bf16*)W13, ldw, nullptr, nullptr, 0, 0.f, M, 2 * F,
                                   R, 1, ep);
+}
+
+// qkv = X . Wqkv^T with RoPE on columns [0, rot_cols) (EPI_ROPE): X [M][R], Wqkv [N][R] (both K-major)
+void launch_gemm_pp_rope(const void* X, long ldx, const void* W, long ldw, void* C, long ldc, int M, int N, int R,
+                         const float* cosT, const float* sinT, int S, int D, int rot_cols, hipStream_t s) {
+    Epi ep{};
+    ep.prio = prio_mode();
+    ep.cosT = cosT;
+    ep.sinT = sinT;
+    ep.S = S;
+    ep.D = D;
+    ep.rot_cols = rot_cols;
+    const int ntiles = (M / BT) * (N / BT);
+    if (g_persist) {
+        static bool pattr = false;
+        auto* kp = &gemm_pp_persist_kernel<true, true, EPI_ROPE, 1>;
+        if (!pattr) lds_attr(kp), pattr = true;
+        return launch_persist(kp, ntiles, s, (const __bf16*)X, ldx, (const __bf16*)W, ldw, (__bf16*)C, ldc, 0.f, M,
+                              N, R, ep);
+    }
+    static bool attr = false;
+    auto* k = &gemm_pp_kernel<true, true, false, 0, EPI_ROPE, 1>;
+    if (!attr) lds_attr(k), attr = true;
+    k<<<ntiles, NT, LDS_BYTES, s>>>((const __bf16*)X, ldx, (const __bf16*)W, ldw, nullptr, (__bf16*)C, ldc, 0.f, M,
+                                    N, R, 1, ep);
 }
 
 // C[M][N] (bf16) = (A8 . B8^T) * sa * sb with A8 [M][K], B8 [N][K] fp8 row-major (K-major), row strides in

@@ -173,5 +173,8 @@ bool gpp_read_stamps(long long* host, int n);
 // gemm_pp: 1 = persistent kernel for the one-pass bf16 / fp8 GEMMs, 0 = one tile per workgroup; -1 queries.
 // Returns the previous mode.
 int gpp_persist_config(int mode);
+// qkv = X . Wqkv^T (bf16, both K-major) with RoPE applied to output columns [0, rot_cols) in the epilogue
+void launch_gemm_pp_rope(const void* X, long ldx, const void* W, long ldw, void* C, long ldc, int M, int N, int R,
+                         const float* cosT, const float* sinT, int S, int D, int rot_cols, hipStream_t s);
 // whether FaArgs::dkv_part (GQA fp32 dK / dV partials of the fused backward) must be set
 bool fa_dkv_partials_needed(int D);

@@ -455,6 +455,34 @@ std::tuple<at::Tensor, at::Tensor> gemm_swiglu_fwd(const at::Tensor& x, const at
     return {gu, a};
 }
 
+// qkv = x @ w^T with RoPE on its first rot_cols columns (Q and K heads, interleaved pairs, position = row % S)
+// applied in the GEMM epilogue: the fused form of matmul + rope_qk_ (no second pass over Q / K)
+at::Tensor gemm_qkv_rope(const at::Tensor& x, const at::Tensor& w, const at::Tensor& cos, const at::Tensor& sin,
+                         int64_t S, int64_t D, int64_t rot_cols) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+                "gemm_qkv_rope: bf16 operands required");
+    TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1,
+                "gemm_qkv_rope: row-major 2-D operands required");
+    const int M = (int)x.size(0), R = (int)x.size(1), N = (int)w.size(0);
+    TORCH_CHECK(w.size(1) == R, "gemm_qkv_rope: shape mismatch");
+    TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && R % 64 == 0, "gemm_qkv_rope: M, N multiples of 256, K of 64");
+    TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm_qkv_rope: 16-byte row alignment");
+    TORCH_CHECK((long)N * w.stride(0) < (1L << 31) && 256L * x.stride(0) < (1L << 31),
+                "gemm_qkv_rope: operand offsets exceed 32 bits");
+    TORCH_CHECK(D % 8 == 0 && rot_cols % D == 0 && rot_cols <= N && S > 0 && M % S == 0,
+                "gemm_qkv_rope: D multiple of 8, rot_cols of D, rows a multiple of S");
+    TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+                    sin.is_contiguous() && cos.is_cuda() && sin.is_cuda(),
+                "gemm_qkv_rope: contiguous fp32 cos / sin tables on the GPU required");
+    TORCH_CHECK(cos.numel() >= S * (D / 2) && sin.numel() >= S * (D / 2), "gemm_qkv_rope: cos / sin shorter than S");
+    DevGuard g(x.device());
+    auto out = at::empty({M, N}, x.options());
+    launch_gemm_pp_rope(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), N, M, N, R,
+                        cos.data_ptr<float>(), sin.data_ptr<float>(), (int)S, (int)D, (int)rot_cols, cur_stream());
+    return out;
+}
+
 // ---------------------------------------------------------------- FP8 quantisation (delayed scaling)
 void cast_fp8(const at::Tensor& x, const at::Tensor& scale, at::Tensor out, at::Tensor amax_bits) {
     check_cuda(x, "x");
@@ -870,6 +898,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");
     m.def("gemm_swiglu_bwd(Tensor dy, Tensor w2, Tensor gu) -> Tensor");
     m.def("gemm_swiglu_fwd(Tensor x, Tensor w13) -> (Tensor, Tensor)");
+    m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int S, int D, int rot_cols) -> Tensor");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb) -> Tensor");
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
@@ -915,6 +944,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("gemm_pp", &gemm_pp);
     m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
     m.impl("gemm_swiglu_fwd", &gemm_swiglu_fwd);
+    m.impl("gemm_qkv_rope", &gemm_qkv_rope);
     m.impl("gemm_fp8", &gemm_fp8);
     m.impl("cast_fp8", &cast_fp8);
     m.impl("transpose_bf16", &transpose_bf16);

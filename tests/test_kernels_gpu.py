@@ -438,6 +438,33 @@ def test_gemm_swiglu_fwd(gpu_device, gpp_mode, M, d, F):
     assert rel(a.cpu(), (g * torch.sigmoid(g) * u).cpu()) < 2e-2
 
 
+@pytest.mark.parametrize("H,Hkv", [(8, 2), (4, 4)])
+def test_gemm_qkv_rope(gpu_device, gpp_mode, H, Hkv):
+    """QKV projection with RoPE in the GEMM epilogue vs the unfused pair (matmul, then rope_qk_ in place).  Small
+    integer operands make every product exact, so the two must agree bitwise (the RoPE arithmetic is the same
+    fp32 formula on the same bf16 values); the partly rotated tile (Q / K end inside a 256-column tile) and the
+    untouched V columns are both covered."""
+    from bpe_transformer.ops import reference as R
+    h = torch.ops.bpe_hip
+    B, S, D, d = 2, 256, 64, 256
+    N = (H + 2 * Hkv) * D
+    g = torch.Generator(device="cpu").manual_seed(H * 10 + Hkv)
+    x = torch.randint(-2, 3, (B * S, d), generator=g).to(torch.bfloat16).to(gpu_device)
+    w = torch.randint(-1, 2, (N, d), generator=g).to(torch.bfloat16).to(gpu_device)
+    cos, sin = R.rope_tables(D, 1024, 10000.0, device=gpu_device)
+    ref = torch.matmul(x, w.t())
+    h.rope_qk_(ref, cos, sin, B, S, H, Hkv, D)
+    out = h.gemm_qkv_rope(x, w, cos, sin, S, D, (H + Hkv) * D)
+    assert torch.equal(out, ref)
+    # random operands against the fp32 oracle (rotation of the bf16-rounded product)
+    x = torch.randn(B * S, d, device=gpu_device, dtype=torch.bfloat16)
+    w = (0.1 * torch.randn(N, d, device=gpu_device)).to(torch.bfloat16)
+    out = h.gemm_qkv_rope(x, w, cos, sin, S, D, (H + Hkv) * D)
+    y = (x.float() @ w.float().t()).to(torch.bfloat16)
+    h.rope_qk_(y, cos, sin, B, S, H, Hkv, D)
+    assert rel(out.float().cpu(), y.float().cpu()) < 1e-2
+
+
 def test_gemm_pp_persistent_bitwise_many_tiles(gpu_device):
     """More tiles than CUs (every workgroup walks several, the last round partial): the persistent kernel runs the
     same per-tile MFMA sequence as the one-tile kernel, so plain, SwiGLU-forward and SwiGLU-backward outputs must
