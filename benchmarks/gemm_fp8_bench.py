@@ -61,5 +61,51 @@ def main():
         print(json.dumps(row), flush=True)
 
 
+def wgrad(a) -> None:
+    """Weight-gradient GEMMs dW = dY^T X of the Llama projections: fp8 (e5m2 dY^T x e4m3 X^T, both [., tokens],
+    hipBLASLt) against the bf16 route the model takes (ops.gemm.accumulate_weight_grad)."""
+    from bpe_transformer.ops.gemm import accumulate_weight_grad
+
+    for name, (n, k) in {"qkv_dw": (2560, 2048), "o_dw": (2048, 2048), "w13_dw": (11264, 2048),
+                         "w2_dw": (2048, 5632)}.items():
+        T = a.tokens
+        g = torch.randn(T, n, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(T, k, device="cuda", dtype=torch.bfloat16)
+        gt8 = g.t().contiguous().to(torch.float8_e5m2)
+        xt8 = x.t().contiguous().to(torch.float8_e4m3fn)
+        one = torch.ones(1, device="cuda")
+        acc = torch.zeros(n, k, device="cuda", dtype=torch.bfloat16)
+        arms = {
+            "lib_fp8": lambda: torch._scaled_mm(gt8, xt8.t(), scale_a=one[0], scale_b=one[0],
+                                                out_dtype=torch.bfloat16),
+            "bf16_route": lambda: accumulate_weight_grad(acc, g, x),
+        }
+        times = {kk: [] for kk in arms}
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for _ in range(a.rounds):
+            for kk, f in arms.items():
+                f()
+                ev[0].record()
+                for _ in range(a.iters):
+                    f()
+                ev[1].record()
+                torch.cuda.synchronize()
+                times[kk].append(ev[0].elapsed_time(ev[1]) / a.iters)
+        row = {"shape": name, "NKT": [n, k, T]}
+        for kk, t in times.items():
+            med = sorted(t)[len(t) // 2]
+            row[f"{kk}_ms"] = round(med, 4)
+            row[f"{kk}_tflops"] = round(2 * n * k * T / med / 1e9, 1)
+        print(json.dumps(row), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if "--wgrad" in sys.argv:
+        sys.argv.remove("--wgrad")
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--iters", type=int, default=10)
+        ap.add_argument("--rounds", type=int, default=3)
+        ap.add_argument("--tokens", type=int, default=65536)
+        wgrad(ap.parse_args())
+    else:
+        main()

@@ -120,7 +120,8 @@ class FusedBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xr, xd, ln1, wq, wk, wv, wo, ln2, w1, w3, w2, cos, sin, meta):
         B, S, H, Hkv, D, eps, use_rope = meta[:7]
-        # fp8: (e4m3 Fp8State, first slot, e5m2 gradient Fp8State or None, first gradient slot) or None
+        # fp8: (e4m3 Fp8State, first slot, e5m2 gradient Fp8State or None, first gradient slot, fp8 weight
+        # gradients) or None
         fp8 = meta[7]
         train = meta[8]  # a backward will run (decided by the caller: grad mode is off inside forward)
         scale = 1.0 / math.sqrt(D)
@@ -134,17 +135,23 @@ class FusedBlockFn(torch.autograd.Function):
         else:
             x2, h1, r1 = hip().add_rmsnorm_fwd(xr, xd, ln1, eps)
         w8s = None
+        xt8s = None
         if fp8 is not None:
             st, s0 = fp8[0], fp8[1]  # slots s0..s0+3: activations, s0+4..s0+7: weights
             keep = fp8[2] is not None  # fp8 input-gradient GEMMs reuse the quantised weights
+            # fp8 weight gradients: the activation cast also writes X^T (e4m3) for dW = dY^T X
+            wg = keep and train and len(fp8) > 4 and bool(fp8[4])
             w8s = []
+            xt8s = [] if wg else None
 
             def mm(x, w, i):
-                r = st.matmul(x, w, s0 + i, s0 + 4 + i, keep_w8=keep)
-                if keep:
-                    w8s.append(r[1])
-                    return r[0]
-                return r
+                if not keep:
+                    return st.matmul(x, w, s0 + i, s0 + 4 + i)
+                y, w8t, xt8 = st.matmul(x, w, s0 + i, s0 + 4 + i, keep_w8=True, keep_xt=wg)
+                w8s.append(w8t)
+                if wg:
+                    xt8s.append(xt8)
+                return y
 
             qkv = mm(h1, w_qkv, 0)
         pre = use_rope and prerotate_default(D)
@@ -173,7 +180,10 @@ class FusedBlockFn(torch.autograd.Function):
             a = hip().swiglu_fwd(gu)
         g2 = mm(a, w2.detach(), 3) if fp8 is not None else torch.matmul(a, w2.t())
         ctx.w8s = w8s if w8s else None
+        ctx.xt8s = xt8s
         ctx.has_xd = xd is not None
+        if xt8s is not None:  # h1, h2, a only fed the bf16 weight gradients: not kept
+            h1 = h2 = a = None
         ctx.save_for_backward(x2, r1, h1, qkv, o, lse, xm, r2, h2, gu, a, cos, sin)
         ctx.params = (ln1, wq, wk, wv, wo, ln2, w1, w3, w2)
         ctx.meta = meta
@@ -216,6 +226,29 @@ class FusedBlockFn(torch.autograd.Function):
 
         fp8 = ctx.meta[7]
         w8s = getattr(ctx, "w8s", None)
+        xt8s = getattr(ctx, "xt8s", None)
+        ctx.xt8s = None
+
+        def acc_dw(ps: list[Tensor], dw: Tensor) -> None:
+            """Add a formed weight gradient (the fp8 weight-gradient GEMM's bf16 output) for the row-stacked ``ps``."""
+            if main:
+                view = _adjacent_view([p.main_grad for p in ps])
+                if view is not None:
+                    view.add_(dw)
+                else:
+                    off = 0
+                    for p in ps:
+                        n = p.shape[0]
+                        p.main_grad.add_(dw[off : off + n])
+                        off += n
+                for p in ps:
+                    _notify(p)
+            else:
+                off = 0
+                for p in ps:
+                    n = p.shape[0]
+                    grads[id(p)] = dw[off : off + n]
+                    off += n
 
         def dx(g_out: Tensor, ws: list[Tensor], i: int) -> Tensor:
             """Input gradient g_out @ W of projection i (0 qkv, 1 o, 2 w13, 3 w2): fp8 e5m2 x e4m3 when enabled;
@@ -229,26 +262,36 @@ class FusedBlockFn(torch.autograd.Function):
                 return torch.matmul(g_out, hip().transpose_bf16(w).t())
             return torch.matmul(g_out, w)
 
+        def proj(g_out: Tensor, ws: list[Tensor], i: int, x_in: Tensor | None) -> Tensor:
+            """Both gradients of projection i: returns dX = g_out @ W, accumulates dW = g_out^T x_in.  With fp8
+            weight gradients both come from one e5m2 cast of g_out (ops/fp8.py ``grads``)."""
+            if xt8s is not None:
+                from ..ops.fp8 import grads as fp8_grads
+
+                dxv, dw = fp8_grads(fp8[2], g_out, fp8[3] + i, w8s[i], fp8[0], fp8[1] + 4 + i, xt8s[i], fp8[0],
+                                    fp8[1] + i)
+                acc_dw(ws, dw)
+                return dxv
+            acc_weight(ws, g_out, x_in)
+            return dx(g_out, ws, i)
+
         # ---- FFN
-        acc_weight([w2], dy, a)
         if w8s is None and _fuse_swiglu_bwd(dy, w2, gu):
+            acc_weight([w2], dy, a)
             # da = dy @ W2 with the SwiGLU backward in the GEMM epilogue (csrc/gemm_pp.hip): da never reaches HBM
             dgu = hip().gemm_swiglu_bwd(dy, w2.detach(), gu)
         else:
-            da = dx(dy, [w2], 3)
+            da = proj(dy, [w2], 3, a)
             dgu = hip().swiglu_bwd(da, gu)
-        acc_weight([w1, w3], dgu, h2)
-        dh2 = dx(dgu, [w1, w3], 2)
+        dh2 = proj(dgu, [w1, w3], 2, h2)
         dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dxm_out)
         # ---- attention
-        acc_weight([wo], dxm, o)
-        do = dx(dxm, [wo], 1)
+        do = proj(dxm, [wo], 1, o)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         dqkv = hip().fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, ctx.prerotated,
                             ctx.dq_acc)
         ctx.dq_acc = None
-        acc_weight([wq, wk, wv], dqkv, h1)
-        dh1 = dx(dqkv, [wq, wk, wv], 0)
+        dh1 = proj(dqkv, [wq, wk, wv], 0, h1)
         dx2, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm)
         dxd = dx2 if ctx.has_xd else None
         if main:

@@ -22,6 +22,8 @@ from .layers import Embedding, Linear, RMSNorm, TransformerBlock
 # dimension of the head GEMMs and the logits row stride are aligned (profiles/bench/lm_head_vocab_pad.log)
 _VOCAB_PAD = 256
 
+FP8_WGRAD = True  # enable_fp8's default for fp8 weight gradients (module flag: A/B runs set it)
+
 
 class TransformerLM(nn.Module):
     # sharded data parallelism (parallel/zero.py) sets this to a callable(module) that waits for the in-flight
@@ -84,9 +86,11 @@ class TransformerLM(nn.Module):
     fp8_state = None
     fp8_grad_state = None
 
-    def enable_fp8(self, history: int = 16, margin: float = 1.0, dgrad: bool = True):
-        """Run the block projections in fp8 with delayed scaling: forward GEMMs e4m3 x e4m3, and with ``dgrad``
-        the input-gradient GEMMs e5m2 (gradient) x e4m3 (weight) as well; weight gradients stay bf16.
+    def enable_fp8(self, history: int = 16, margin: float = 1.0, dgrad: bool = True, wgrad: bool | None = None):
+        """Run the block projections in fp8 with delayed scaling: forward GEMMs e4m3 x e4m3; with ``dgrad`` the
+        input-gradient GEMMs e5m2 (gradient) x e4m3 (weight) as well, and with ``wgrad`` (needs ``dgrad``) the
+        weight-gradient GEMMs e5m2 (gradient^T) x e4m3 (activation^T) from the same gradient cast (None: the
+        module default ``FP8_WGRAD``).
 
         Only the fused GPU block path quantises (``models/fused_block.py``); every block owns 8 e4m3 scale
         slots (4 activations + 4 weights) and 4 e5m2 slots (output gradients).  The training engine calls
@@ -99,7 +103,8 @@ class TransformerLM(nn.Module):
         self.fp8_state = Fp8State(8 * L, dev, history=history, margin=margin)
         self.fp8_grad_state = Fp8State(4 * L, dev, history=history, margin=margin, fmt="e5m2") if dgrad else None
         for i, layer in enumerate(self.layers):
-            layer.fp8 = (self.fp8_state, 8 * i, self.fp8_grad_state, 4 * i)
+            layer.fp8 = (self.fp8_state, 8 * i, self.fp8_grad_state, 4 * i,
+                         bool(dgrad and (FP8_WGRAD if wgrad is None else wgrad)))
         return self.fp8_state
 
     def fp8_states(self) -> list:

@@ -77,49 +77,56 @@ __global__ void __launch_bounds__(256) cast_fp8_kernel(const T* __restrict__ x, 
     if (threadIdx.x == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
 
-// Weight cast for the fp8 path: W [N][K] bf16 -> w8 [N][K] AND w8t [K][N] (e4m3), one pass, amax folded in.
-// The input-gradient GEMM dX = dY . W needs W with the reduction index (N) contiguous; writing that copy here
-// replaces a strided PyTorch transpose of the fp8 weight per GEMM (~0.3 TB/s).  64 x 64 tiles through LDS
-// (row stride 68 B: the transposed byte reads of one wave spread over the banks).
+// Two-layout cast: W [N][K] bf16 -> w8 [N][K] AND w8t [K][N] (FMT 0 e4m3 / 1 e5m2), one pass, amax folded in.
+// Weights: the input-gradient GEMM dX = dY . W needs W with the reduction index (N) contiguous; writing that
+// copy here replaces a strided PyTorch transpose of the fp8 weight per GEMM (~0.3 TB/s).  Activations and output
+// gradients: the fp8 weight-gradient GEMM dW = dY^T . X reduces over tokens, so both operands are wanted with the
+// token index contiguous ([N][T], [K][T]) -- the layout of the fp8 kernel and of the library.  64 x 64 tiles
+// through LDS (row stride 68 B: the transposed byte reads of one wave spread over the banks); a grid-stride loop
+// over the tiles, so one amax atomic per workgroup stays a few thousand at most.
+template <int FMT>
 __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const __bf16* __restrict__ w, int N, int K,
                                                          const float* __restrict__ scale, uint8_t* __restrict__ w8,
                                                          uint8_t* __restrict__ w8t, unsigned* __restrict__ amax_bits) {
     __shared__ uint8_t tile[64][68];
     __shared__ float red[4];
     const int tid = threadIdx.x;
-    const int tiles_k = K / 64;
-    const int n0 = (blockIdx.x / tiles_k) * 64, k0 = (blockIdx.x % tiles_k) * 64;
+    const int tiles_k = K / 64, ntiles = (N / 64) * tiles_k;
     const float sc = *scale;
     const int r = tid >> 2, c = (tid & 3) * 16;
-    const __bf16* src = w + (long)(n0 + r) * K + k0 + c;
-    const u16x8 a = *reinterpret_cast<const u16x8*>(src);
-    const u16x8 b = *reinterpret_cast<const u16x8*>(src + 8);
-    float v[16];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { v[j] = bf2f(a[j]); v[8 + j] = bf2f(b[j]); }
     float am = 0.f;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int n0 = (t / tiles_k) * 64, k0 = (t % tiles_k) * 64;
+        const __bf16* src = w + (long)(n0 + r) * K + k0 + c;
+        const u16x8 a = *reinterpret_cast<const u16x8*>(src);
+        const u16x8 b = *reinterpret_cast<const u16x8*>(src + 8);
+        float v[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
-    uint4 q;
-    q.x = pack4_fp8<0>(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc);
-    q.y = pack4_fp8<0>(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc);
-    q.z = pack4_fp8<0>(v[8] * sc, v[9] * sc, v[10] * sc, v[11] * sc);
-    q.w = pack4_fp8<0>(v[12] * sc, v[13] * sc, v[14] * sc, v[15] * sc);
-    *reinterpret_cast<uint4*>(w8 + (long)(n0 + r) * K + k0 + c) = q;
-    const unsigned qq[4] = {q.x, q.y, q.z, q.w};
+        for (int j = 0; j < 8; ++j) { v[j] = bf2f(a[j]); v[8 + j] = bf2f(b[j]); }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *reinterpret_cast<unsigned*>(&tile[r][c + 4 * j]) = qq[j];
-    __syncthreads();
-    // transposed: thread -> output row k0 + r (a column of the tile), 16 consecutive n
-    unsigned o[4];
+        for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
+        uint4 q;
+        q.x = pack4_fp8<FMT>(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc);
+        q.y = pack4_fp8<FMT>(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc);
+        q.z = pack4_fp8<FMT>(v[8] * sc, v[9] * sc, v[10] * sc, v[11] * sc);
+        q.w = pack4_fp8<FMT>(v[12] * sc, v[13] * sc, v[14] * sc, v[15] * sc);
+        *reinterpret_cast<uint4*>(w8 + (long)(n0 + r) * K + k0 + c) = q;
+        const unsigned qq[4] = {q.x, q.y, q.z, q.w};
+        __syncthreads();  // the previous tile's transposed reads are done
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        unsigned x = 0;
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<unsigned*>(&tile[r][c + 4 * j]) = qq[j];
+        __syncthreads();
+        // transposed: thread -> output row k0 + r (a column of the tile), 16 consecutive n
+        unsigned o[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x |= (unsigned)tile[c + 4 * j + e][r] << (8 * e);
-        o[j] = x;
+        for (int j = 0; j < 4; ++j) {
+            unsigned x = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x |= (unsigned)tile[c + 4 * j + e][r] << (8 * e);
+            o[j] = x;
+        }
+        *reinterpret_cast<uint4*>(w8t + (long)(k0 + r) * N + n0 + c) = uint4{o[0], o[1], o[2], o[3]};
     }
-    *reinterpret_cast<uint4*>(w8t + (long)(k0 + r) * N + n0 + c) = uint4{o[0], o[1], o[2], o[3]};
     am = block_max(am, red);
     if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
@@ -158,9 +165,15 @@ void launch_cast_fp8(int dtype, int fmt, const void* x, size_t n, const float* s
 }
 
 void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8, void* w8t, unsigned* amax_bits,
-                       hipStream_t s) {
-    cast_fp8_t_kernel<<<(N / 64) * (K / 64), 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8,
-                                                         (uint8_t*)w8t, amax_bits);
+                       int fmt, hipStream_t s) {
+    const int ntiles = (N / 64) * (K / 64);
+    const int grid = ntiles < 2048 ? ntiles : 2048;
+    if (fmt == 0)
+        cast_fp8_t_kernel<0><<<grid, 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8, (uint8_t*)w8t,
+                                                  amax_bits);
+    else
+        cast_fp8_t_kernel<1><<<grid, 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8, (uint8_t*)w8t,
+                                                  amax_bits);
 }
 
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,

@@ -58,7 +58,7 @@ void launch_cast_fp8(int dtype, int fmt, const void* x, size_t n, const float* s
 // dst[C, R] = src[R, C]^T, bf16, R and C multiples of 64 (16-byte aligned rows)
 void launch_transpose_bf16(const void* src, long ld_src, void* dst, long ld_dst, int R, int C, hipStream_t s);
 void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8, void* w8t, unsigned* amax_bits,
-                       hipStream_t s);  // bf16 W [N][K] -> e4m3 w8 [N][K] and w8t [K][N]
+                       int fmt, hipStream_t s);  // bf16 W [N][K] -> e4m3 w8 [N][K] and w8t [K][N]
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,
                           float margin, int fmt, hipStream_t s);
 

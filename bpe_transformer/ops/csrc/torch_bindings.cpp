@@ -512,20 +512,22 @@ at::Tensor transpose_bf16(const at::Tensor& w) {
     return out;
 }
 
-// W [N][K] bf16 -> e4m3 copies w8 [N][K] and w8t [K][N] in one pass (amax folded into amax_bits)
+// W [N][K] bf16 -> fp8 copies w8 [N][K] and w8t [K][N] in one pass (e4m3 or e5m2, both outputs the same format;
+// amax folded into amax_bits)
 void cast_fp8_t(const at::Tensor& w, const at::Tensor& scale, at::Tensor w8, at::Tensor w8t, at::Tensor amax_bits) {
     check_cuda(w, "w");
     TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.scalar_type() == at::kBFloat16, "cast_fp8_t: bf16 [N, K]");
     const int N = (int)w.size(0), K = (int)w.size(1);
     TORCH_CHECK(N % 64 == 0 && K % 64 == 0, "cast_fp8_t: N and K must be multiples of 64");
+    const bool e4 = w8.scalar_type() == at::kFloat8_e4m3fn, e5 = w8.scalar_type() == at::kFloat8_e5m2;
     TORCH_CHECK(w8.is_contiguous() && w8t.is_contiguous() && w8.numel() == w.numel() && w8t.numel() == w.numel() &&
-                    w8.scalar_type() == at::kFloat8_e4m3fn && w8t.scalar_type() == at::kFloat8_e4m3fn &&
-                    w8t.size(0) == K, "cast_fp8_t: e4m3 outputs [N, K] and [K, N] required");
+                    (e4 || e5) && w8t.scalar_type() == w8.scalar_type() && w8t.size(0) == K,
+                "cast_fp8_t: e4m3 or e5m2 outputs [N, K] and [K, N] of one format required");
     TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1 && amax_bits.scalar_type() == at::kInt &&
                     amax_bits.numel() == 1, "cast_fp8_t: one fp32 scale and one int32 amax slot");
     DevGuard g(w.device());
     launch_cast_fp8_t(w.data_ptr(), N, K, scale.data_ptr<float>(), w8.data_ptr(), w8t.data_ptr(),
-                      reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
+                      reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), e5 ? 1 : 0, cur_stream());
 }
 
 void update_scales(at::Tensor amax_bits, at::Tensor hist, at::Tensor scale, at::Tensor inv_scale, int64_t pos,

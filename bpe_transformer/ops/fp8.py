@@ -17,8 +17,12 @@ Recipe (BASELINE.json "Llama-style 1.1B fp8 MFMA path"):
   * input-gradient GEMMs (dX = dY . W) optionally run in fp8 too: dY is
     quantised to e5m2 (wider range, the usual gradient format) with its own
     delayed scales, W reuses the forward's e4m3 copy (transposed once);
-    weight-gradient GEMMs stay bf16 on the saved bf16 activations; master
-    weights and optimizer state stay fp32.
+  * weight-gradient GEMMs (dW = dY^T . X) optionally as well (``wgrad``):
+    they reduce over tokens, so the forward's activation cast also writes
+    X^T (e4m3, [K, tokens], saved for the backward instead of nothing extra
+    on the bf16 side) and the backward's one gradient cast writes dY and dY^T
+    (e5m2) together (``cast_t``: both layouts in one pass, csrc/fp8.hip);
+    master weights and optimizer state stay fp32.
 """
 
 from __future__ import annotations
@@ -75,7 +79,11 @@ def mm_fp8(a8: Tensor, b8: Tensor, sa: Tensor, sb: Tensor) -> Tensor:
     256 x 256 x 128-aligned, else hipBLASLt."""
     M, K = a8.shape
     N = b8.shape[0]
-    if (_use_hip(M, N, K, a8.dtype) and M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and a8.stride(1) == 1
+    # the hand kernel has no split-K: a weight-gradient shape (few output tiles, K = all tokens) would leave most
+    # CUs idle, so those go to the library even when BPE_FP8_GEMM=hip
+    few_tiles = (M // 256) * (N // 256) < 128 and K > 4 * max(M, N)
+    if (not few_tiles and M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and _use_hip(M, N, K, a8.dtype)
+            and a8.stride(1) == 1
             and b8.stride(1) == 1 and a8.stride(0) % 16 == 0 and b8.stride(0) % 16 == 0 and b8.dtype == FP8):
         return ops().gemm_fp8(a8, b8, sa.reshape(1), sb.reshape(1))
     return torch._scaled_mm(a8, b8.t(), scale_a=sa, scale_b=sb, out_dtype=torch.bfloat16)
@@ -121,27 +129,43 @@ class Fp8State:
         self.margin = float(sd["margin"])
 
     def cast_t(self, w: Tensor, slot: int) -> tuple[Tensor, Tensor]:
-        """Weight cast: (w8 [N, K], w8t [K, N]) in one pass (csrc/fp8.hip cast_fp8_t)."""
+        """Two-layout cast of a bf16 [N, K] matrix (N, K multiples of 64): (w8 [N, K], w8t [K, N]) in this state's
+        format, one pass (csrc/fp8.hip cast_fp8_t)."""
         w = w.contiguous()
         w8 = torch.empty(w.shape, dtype=self.dtype, device=w.device)
         w8t = torch.empty(w.shape[1], w.shape[0], dtype=self.dtype, device=w.device)
         ops().cast_fp8_t(w, self.scale[slot : slot + 1], w8, w8t, self.amax[slot : slot + 1])
         return w8, w8t
 
-    def matmul(self, x: Tensor, w: Tensor, x_slot: int, w_slot: int, keep_w8: bool = False):
-        """``x @ w.T`` in fp8 with bf16 output; x: [M, K] bf16, w: [N, K] bf16.  ``keep_w8`` also returns the
-        quantised weight in the [K, N] layout the input-gradient GEMM needs (written by the same cast pass)."""
-        x8 = self.cast(x, x_slot)
-        t_ok = keep_w8 and self.fmt == "e4m3" and w.dtype == torch.bfloat16 and w.shape[0] % 64 == 0 \
-            and w.shape[1] % 64 == 0
-        if t_ok:
+    def matmul(self, x: Tensor, w: Tensor, x_slot: int, w_slot: int, keep_w8: bool = False,
+               keep_xt: bool = False):
+        """``x @ w.T`` in fp8 with bf16 output; x: [M, K] bf16, w: [N, K] bf16.  Without flags returns y.  With
+        ``keep_w8`` / ``keep_xt`` returns ``(y, w8t, xt8)``: the quantised weight in the [K, N] layout the
+        input-gradient GEMM needs and the quantised activation in the [K, M] layout of the weight-gradient GEMM
+        (each written by the same cast pass as the forward operand; None when not asked for)."""
+        xt8 = None
+        if keep_xt:
+            x8, xt8 = self.cast_t(x, x_slot) if _t_ok(x) else (self.cast(x, x_slot), None)
+            if xt8 is None:
+                xt8 = x8.t().contiguous()
+        else:
+            x8 = self.cast(x, x_slot)
+        w8t = None
+        if keep_w8 and _t_ok(w):
             w8, w8t = self.cast_t(w, w_slot)
         else:
-            w8, w8t = self.cast(w, w_slot), None
+            w8 = self.cast(w, w_slot)
+            if keep_w8:
+                w8t = w8.t().contiguous()
         y = mm_fp8(x8, w8, self.inv_scale[x_slot], self.inv_scale[w_slot])
-        if not keep_w8:
+        if not keep_w8 and not keep_xt:
             return y
-        return y, (w8t if w8t is not None else w8.t().contiguous())
+        return y, w8t, xt8
+
+
+def _t_ok(t: Tensor) -> bool:
+    """A bf16 matrix the two-layout cast takes (contiguous rows and columns in multiples of 64)."""
+    return t.dtype == torch.bfloat16 and t.dim() == 2 and t.shape[0] % 64 == 0 and t.shape[1] % 64 == 0
 
 
 def dgrad(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8State, w_slot: int) -> Tensor:
@@ -150,6 +174,25 @@ def dgrad(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8St
     along the reduction (N), the layout of the fp8 kernel and of the library."""
     g8 = g_state.cast(g.contiguous(), g_slot)
     return mm_fp8(g8, w8t, g_state.inv_scale[g_slot], w_state.inv_scale[w_slot])
+
+
+def grads(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8State, w_slot: int,
+          xt8: Tensor | None = None, x_state: Fp8State | None = None, x_slot: int = 0):
+    """Input gradient ``g @ W`` and, with ``xt8``, weight gradient ``g^T @ X`` of one projection from ONE e5m2 cast
+    of g: (dX, dW or None).  dW = g8t [N, tokens] x xt8 [K, tokens] -> [N, K] bf16, both operands contiguous along
+    the token reduction; its scale is g's inverse scale times X's (slot ``x_slot`` of ``x_state``)."""
+    if xt8 is None:
+        return dgrad(g_state, g, g_slot, w8t, w_state, w_slot), None
+    g = g.contiguous()
+    if _t_ok(g):
+        g8, g8t = g_state.cast_t(g, g_slot)
+    else:
+        g8 = g_state.cast(g, g_slot)
+        g8t = g8.t().contiguous()
+    gi = g_state.inv_scale[g_slot]
+    dx = mm_fp8(g8, w8t, gi, w_state.inv_scale[w_slot])
+    dw = mm_fp8(g8t, xt8, gi, x_state.inv_scale[x_slot])
+    return dx, dw
 
 
 def quantize_reference(x: Tensor, scale: float, fmt: str = "e4m3") -> Tensor:

@@ -808,15 +808,17 @@ def test_cast_fp8_and_amax(gpu_device, dtype, n, fmt):
     assert amax.view(torch.float32).item() == x.float().abs().max().item()
 
 
-def test_cast_fp8_transposed(gpu_device):
-    """Weight cast: both e4m3 layouts from one pass, identical bytes to the plain cast, amax folded in."""
+@pytest.mark.parametrize("N,K", [(192, 320), (4096, 1024)])  # the second: more tiles than the grid (stride loop)
+@pytest.mark.parametrize("fmt", [torch.float8_e4m3fn, torch.float8_e5m2])
+def test_cast_fp8_transposed(gpu_device, N, K, fmt):
+    """Two-layout cast (weights; activations and gradients of the fp8 weight-gradient GEMM): both layouts from one
+    pass, identical bytes to the plain cast of the same format, amax folded in."""
     torch.manual_seed(3)
-    N, K = 192, 320
     w = torch.randn(N, K, device=gpu_device, dtype=torch.bfloat16) * 3
     scale = torch.tensor([4.0], device=gpu_device)
     amax = torch.zeros(1, dtype=torch.int32, device=gpu_device)
-    w8 = torch.empty(N, K, dtype=torch.float8_e4m3fn, device=gpu_device)
-    w8t = torch.empty(K, N, dtype=torch.float8_e4m3fn, device=gpu_device)
+    w8 = torch.empty(N, K, dtype=fmt, device=gpu_device)
+    w8t = torch.empty(K, N, dtype=fmt, device=gpu_device)
     torch.ops.bpe_hip.cast_fp8_t(w, scale, w8, w8t, amax)
     ref = torch.empty_like(w8)
     torch.ops.bpe_hip.cast_fp8(w, scale, ref, torch.zeros(1, dtype=torch.int32, device=gpu_device))
@@ -824,6 +826,33 @@ def test_cast_fp8_transposed(gpu_device):
     assert torch.equal(w8t.view(torch.uint8), ref.view(torch.uint8).t().contiguous())
     am = amax.view(torch.float32).item()
     assert am == float(w.float().abs().max())
+
+
+def test_fp8_grads_weight_gradient(gpu_device):
+    """ops.fp8.grads: one e5m2 cast of the output gradient serves dX = g W and dW = g^T X; both against the fp32
+    products of the dequantised operands (the weight-gradient GEMM reduces over all tokens: M = N_out, K = T)."""
+    from bpe_transformer.ops.fp8 import Fp8State, grads
+    torch.manual_seed(11)
+    T, N, K = 8192, 512, 256
+    xs = Fp8State(2, gpu_device)
+    gs = Fp8State(1, gpu_device, fmt="e5m2")
+    x = torch.randn(T, K, device=gpu_device, dtype=torch.bfloat16)
+    w = (0.1 * torch.randn(N, K, device=gpu_device)).to(torch.bfloat16)
+    g = (1e-3 * torch.randn(T, N, device=gpu_device)).to(torch.bfloat16)
+    for _ in range(2):  # calibrate the delayed scales on the same tensors
+        y, w8t, xt8 = xs.matmul(x, w, 0, 1, keep_w8=True, keep_xt=True)
+        dx, dw = grads(gs, g, 0, w8t, xs, 1, xt8, xs, 0)
+        xs.update()
+        gs.update()
+    y, w8t, xt8 = xs.matmul(x, w, 0, 1, keep_w8=True, keep_xt=True)
+    dx, dw = grads(gs, g, 0, w8t, xs, 1, xt8, xs, 0)
+    assert dx.shape == (T, K) and dw.shape == (N, K) and xt8.shape == (K, T)
+    xq = xt8.float().t() * xs.inv_scale[0]
+    g8 = gs.cast(g, 0).float() * gs.inv_scale[0]
+    wq = w8t.float().t() * xs.inv_scale[1]
+    assert rel(dw.float(), g8.t() @ xq) < 1e-2
+    assert rel(dx.float(), g8 @ wq) < 1e-2
+    assert rel(dw.float(), g.float().t() @ x.float()) < 0.1  # fp8 rounding of both operands
 
 
 def test_update_scales(gpu_device):

@@ -107,13 +107,14 @@ def test_generate(gpu_device):
     assert out.shape == (11,)
 
 
-@pytest.mark.parametrize("dgrad", [False, True])
-def test_fp8_close_to_bf16(gpu_device, dgrad):
-    """fp8 projections (e4m3 forward; with dgrad also e5m2 x e4m3 input gradients), delayed scaling: loss and
-    grads stay close to the bf16 path after one calibration step."""
+@pytest.mark.parametrize("dgrad,wgrad", [(False, False), (True, False), (True, True)])
+def test_fp8_close_to_bf16(gpu_device, dgrad, wgrad):
+    """fp8 projections (e4m3 forward; with dgrad also e5m2 x e4m3 input gradients; with wgrad also e5m2 x e4m3
+    weight gradients from the same gradient cast), delayed scaling: loss and grads stay close to the bf16 path
+    after one calibration step."""
     _, a = _pair(gpu_device)
     b = copy.deepcopy(a)
-    st = b.enable_fp8(dgrad=dgrad)
+    st = b.enable_fp8(dgrad=dgrad, wgrad=wgrad)
     ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
     tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
     b.loss(ids, tgt).backward()  # calibration step: record activation / weight / gradient amaxes

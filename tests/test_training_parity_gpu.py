@@ -227,11 +227,11 @@ def _run(c: Shape, accum: int, gpu_device):
     return lo, le
 
 
-def _run_ours(c: Shape, fp8: bool, gpu_device):
+def _run_ours(c: Shape, fp8: bool, gpu_device, wgrad: bool = True):
     ids, vocab = _tokens()
     model = _ours(vocab, c, gpu_device)
     if fp8:
-        model.enable_fp8()
+        model.enable_fp8(wgrad=wgrad)
     eng = _engine(model, 1, c)
     data = _batches(ids, STEPS, c.B, c.S, gpu_device)
     out = [eng.train_step([data[it]], lr=_lr(it, c)) for it in range(STEPS)]
@@ -261,13 +261,15 @@ def test_fused_engine_tracks_eager_pytorch(gpu_device, shape, accum):
     assert rel[-1] < 0.01, rel[-1]
 
 
-@pytest.mark.parametrize("route", ["routes", "hip"])
-def test_fp8_engine_tracks_bf16_engine(gpu_device, monkeypatch, route):
+@pytest.mark.parametrize("route,wgrad", [("routes", True), ("hip", True), ("routes", False)])
+def test_fp8_engine_tracks_bf16_engine(gpu_device, monkeypatch, route, wgrad):
     """fp8 projections (``model.enable_fp8()``: delayed-scaling e4m3 / e5m2, ops/fp8.py) against the bf16 engine on
-    the Llama shape: the final loss within 2 %, the 10-step running mean within 3 % throughout (single steps of the
-    early transient differ by more: the two precisions take different paths through the same loss landscape).
+    the Llama shape: the final loss within 2 %, the 10-step running mean within 3 % throughout with bf16 weight
+    gradients and within 4 % with fp8 ones (single steps of the early transient differ by more: the two precisions
+    take different paths through the same loss landscape; the e5m2 rounding of the gradient in dW widens the
+    transient -- measured 1.4 % vs 3.1 % at its peak, step 24 -- while the final loss stays within 0.6 %).
     ``route``: the per-shape route table, or every fp8 GEMM on the hand-written gemm_pp F8 kernel (asserted: the
-    hand kernel served every fp8 GEMM of the run)."""
+    hand kernel served every fp8 GEMM of the run -- forward, input and weight gradients at this 4096-token shape)."""
     from bpe_transformer.ops import fp8
 
     monkeypatch.setattr(fp8, "_MODE", route)
@@ -282,16 +284,16 @@ def test_fp8_engine_tracks_bf16_engine(gpu_device, monkeypatch, route):
     monkeypatch.setattr(fp8, "_use_hip", counted)
     c = SHAPES["llama"]
     lb = _run_ours(c, False, gpu_device)
-    l8 = _run_ours(c, True, gpu_device)
+    l8 = _run_ours(c, True, gpu_device, wgrad)
     if route == "hip":
         assert taken[True] > 0 and taken[False] == 0, taken
     assert all(math.isfinite(v) for v in lb + l8)
     rel = [abs(a - b) / b for a, b in zip(l8, lb)]
     run = lambda x: [sum(x[max(0, i - 9) : i + 1]) / len(x[max(0, i - 9) : i + 1]) for i in range(len(x))]  # noqa: E731
     rel_mean = [abs(a - b) / b for a, b in zip(run(l8), run(lb))]
-    _log(f"parity_{c.name}_L{L}_fp8_{route}_vs_bf16.json",
-         {"steps": STEPS, "batch": c.B, "seq": c.S, "route": route, "fp8": l8, "bf16": lb, "max_rel": max(rel),
-          "max_rel_mean10": max(rel_mean), "final_rel": rel[-1], "gemm_fp8_calls": taken})
+    _log(f"parity_{c.name}_L{L}_fp8_{route}{'' if wgrad else '_bf16wgrad'}_vs_bf16.json",
+         {"steps": STEPS, "batch": c.B, "seq": c.S, "route": route, "fp8_wgrad": wgrad, "fp8": l8, "bf16": lb,
+          "max_rel": max(rel), "max_rel_mean10": max(rel_mean), "final_rel": rel[-1], "gemm_fp8_calls": taken})
     assert lb[-1] < lb[0] - 2.0
-    assert max(rel_mean) < 0.03, (max(rel_mean), rel_mean.index(max(rel_mean)))
+    assert max(rel_mean) < (0.04 if wgrad else 0.03), (max(rel_mean), rel_mean.index(max(rel_mean)))
     assert rel[-1] < 0.02, rel[-1]
