@@ -75,11 +75,21 @@ def wgrad(a) -> None:
         xt8 = x.t().contiguous().to(torch.float8_e4m3fn)
         one = torch.ones(1, device="cuda")
         acc = torch.zeros(n, k, device="cuda", dtype=torch.bfloat16)
+        from bpe_transformer.ops.gemm import choose_splits_pp
+
+        sp = choose_splits_pp(n, k, T // 2)
         arms = {
             "lib_fp8": lambda: torch._scaled_mm(gt8, xt8.t(), scale_a=one[0], scale_b=one[0],
                                                 out_dtype=torch.bfloat16),
+            "lib_fp8_acc": lambda: acc.add_(torch._scaled_mm(gt8, xt8.t(), scale_a=one[0], scale_b=one[0],
+                                                             out_dtype=torch.bfloat16)),
+            "hip_fp8_splitk_acc": lambda: ops().gemm_fp8_acc(gt8, xt8, one, one, acc, 1.0, sp),
             "bf16_route": lambda: accumulate_weight_grad(acc, g, x),
         }
+        ref = gt8.float() @ xt8.float().t()
+        acc.zero_()
+        ops().gemm_fp8_acc(gt8, xt8, one, one, acc, 1.0, sp)
+        err = float(((acc.float() - ref).norm() / ref.norm()).item())
         times = {kk: [] for kk in arms}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for _ in range(a.rounds):
@@ -91,7 +101,7 @@ def wgrad(a) -> None:
                 ev[1].record()
                 torch.cuda.synchronize()
                 times[kk].append(ev[0].elapsed_time(ev[1]) / a.iters)
-        row = {"shape": name, "NKT": [n, k, T]}
+        row = {"shape": name, "NKT": [n, k, T], "splits": sp, "hip_rel_err": round(err, 5)}
         for kk, t in times.items():
             med = sorted(t)[len(t) // 2]
             row[f"{kk}_ms"] = round(med, 4)

@@ -268,9 +268,15 @@ class FusedBlockFn(torch.autograd.Function):
             if xt8s is not None:
                 from ..ops.fp8 import grads as fp8_grads
 
+                # accumulated straight into the flat gradient buffer when the stacked weights are adjacent there
+                view = _adjacent_view([p.main_grad for p in ws]) if main else None
                 dxv, dw = fp8_grads(fp8[2], g_out, fp8[3] + i, w8s[i], fp8[0], fp8[1] + 4 + i, xt8s[i], fp8[0],
-                                    fp8[1] + i)
-                acc_dw(ws, dw)
+                                    fp8[1] + i, dw_out=view)
+                if view is None:
+                    acc_dw(ws, dw)
+                else:
+                    for p in ws:
+                        _notify(p)
                 return dxv
             acc_weight(ws, g_out, x_in)
             return dx(g_out, ws, i)

@@ -714,13 +714,15 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     // accumulator (ib, jb) register r of lane l: row i = 128 g + 16 ib + (l & 15), col j = 64 wl + 16 jb + 4 (l >> 4) + r
     if constexpr (SLAB) {
         float* sp = slab + (long)split * M * N;
+        float osc = 1.f;  // F8: the operands' inverse scales, applied to each partial (the reduce only sums)
+        if constexpr (F8 != 0) osc = ep.sa[0] * ep.sb[0];
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib)
 #pragma unroll
             for (int jb = 0; jb < 4; ++jb) {
                 const long i = i0 + 128 * g + 16 * ib + (l & 15);
                 const long j = j0 + 64 * wl + 16 * jb + 4 * (l >> 4);
-                if (st_on) *reinterpret_cast<f32x4*>(sp + i * N + j) = acc[ib][jb];
+                if (st_on) *reinterpret_cast<f32x4*>(sp + i * N + j) = F8 != 0 ? acc[ib][jb] * osc : acc[ib][jb];
             }
     } else {
         epilogue_bf16<EPI, F8, 1>(acc, smem, g, wl, l, tid, i0, j0, jb, C, ldc, beta, ep, st_on, false, blockIdx.x);
@@ -985,6 +987,26 @@ void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, 
     }
     k<<<(M / BT) * (N / BT), NT, LDS_BYTES, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, nullptr,
                                                   (__bf16*)C, ldc, 0.f, M, N, K / 2, 1, ep);
+}
+
+// C = beta * C + (A8 . B8^T) * sa * sb, split over K into `splits` fp32 partials (slab [splits][M][N]) summed in a
+// fixed order by splitk_reduce: the fp8 weight-gradient GEMM (few output tiles, K = all tokens).  C bf16 or fp32.
+void launch_gemm_fp8_splitk(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                            int fmt_a, const float* sa, const float* sb, float beta, int splits, float* slab,
+                            int c_f32, hipStream_t s) {
+    static bool attr1 = false, attr2 = false;
+    auto* k1 = &gemm_pp_kernel<true, true, true, 0, EPI_NONE, 1, 1>;
+    auto* k2 = &gemm_pp_kernel<true, true, true, 0, EPI_NONE, 1, 2>;
+    auto* k = fmt_a == 1 ? k2 : k1;
+    bool& attr = fmt_a == 1 ? attr2 : attr1;
+    if (!attr) lds_attr(k), attr = true;
+    Epi ep{};
+    ep.prio = prio_mode();
+    ep.sa = sa;
+    ep.sb = sb;
+    k<<<(M / BT) * (N / BT) * splits, NT, LDS_BYTES, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, slab,
+                                                           nullptr, 0, 0.f, M, N, K / 2, splits, ep);
+    splitk_reduce(slab, C, ldc, beta, M, N, splits, c_f32, s);
 }
 
 bool gemm_pp_shape_ok(int M, int N, int R, int splits) {

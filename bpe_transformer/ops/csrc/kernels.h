@@ -173,6 +173,10 @@ bool gpp_read_stamps(long long* host, int n);
 // gemm_pp: 1 = persistent kernel for the one-pass bf16 / fp8 GEMMs, 0 = one tile per workgroup; -1 queries.
 // Returns the previous mode.
 int gpp_persist_config(int mode);
+// C = beta * C + (A8 . B8^T) * sa * sb over `splits` fp32 partials (slab [splits][M][N]); C bf16 or fp32 (c_f32)
+void launch_gemm_fp8_splitk(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                            int fmt_a, const float* sa, const float* sb, float beta, int splits, float* slab,
+                            int c_f32, hipStream_t s);
 // qkv = X . Wqkv^T (bf16, both K-major) with RoPE applied to output columns [0, rot_cols) in the epilogue
 void launch_gemm_pp_rope(const void* X, long ldx, const void* W, long ldw, void* C, long ldc, int M, int N, int R,
                          const float* cosT, const float* sinT, int S, int D, int rot_cols, hipStream_t s);

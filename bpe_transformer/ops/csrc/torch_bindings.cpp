@@ -416,6 +416,35 @@ at::Tensor gemm_fp8(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor
     return y;
 }
 
+// c = beta * c + (a8 @ b8^T) * sa * sb, split-K (`splits` fp32 partials, ordered reduce): the fp8 weight-gradient
+// GEMM, accumulating straight into the (bf16 or fp32) gradient buffer view c
+void gemm_fp8_acc(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor& sa, const at::Tensor& sb, at::Tensor c,
+                  double beta, int64_t splits) {
+    check_cuda(a8, "a8");
+    check_cuda(c, "c");
+    const bool a_e5 = a8.scalar_type() == at::kFloat8_e5m2;
+    TORCH_CHECK((a8.scalar_type() == at::kFloat8_e4m3fn || a_e5) && b8.scalar_type() == at::kFloat8_e4m3fn,
+                "gemm_fp8_acc: a8 must be float8_e4m3fn or float8_e5m2, b8 float8_e4m3fn");
+    TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.stride(1) == 1 && b8.stride(1) == 1 && a8.size(1) == b8.size(1),
+                "gemm_fp8_acc: a8 [M, K] and b8 [N, K] row-major with a common K");
+    const int64_t M = a8.size(0), N = b8.size(0), K = a8.size(1);
+    TORCH_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1 &&
+                    (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
+                "gemm_fp8_acc: c [M, N] bf16 / fp32 with unit column stride");
+    TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && splits >= 1 && K / 128 >= splits,
+                "gemm_fp8_acc: M, N multiples of 256, K of 128 (>= 128 x splits)");
+    TORCH_CHECK(a8.stride(0) % 16 == 0 && b8.stride(0) % 16 == 0 && (a8.stride(0) * 256) < (1L << 32) &&
+                    (b8.stride(0) * 256) < (1L << 32), "gemm_fp8_acc: 16-byte aligned rows, 32-bit tile offsets");
+    TORCH_CHECK(sa.scalar_type() == at::kFloat && sb.scalar_type() == at::kFloat && sa.numel() >= 1 &&
+                    sb.numel() >= 1 && sa.is_cuda() && sb.is_cuda(), "gemm_fp8_acc: sa / sb must be fp32 device scalars");
+    DevGuard g(a8.device());
+    auto slab = at::empty({splits, M, N}, c.options().dtype(at::kFloat));
+    launch_gemm_fp8_splitk(a8.data_ptr(), a8.stride(0), b8.data_ptr(), b8.stride(0), c.data_ptr(), c.stride(0),
+                           (int)M, (int)N, (int)K, a_e5 ? 1 : 0, sa.data_ptr<float>(), sb.data_ptr<float>(),
+                           (float)beta, (int)splits, slab.data_ptr<float>(), c.scalar_type() == at::kFloat ? 1 : 0,
+                           cur_stream());
+}
+
 // dgu = swiglu_bwd(dy @ w2, gu) with the SwiGLU backward in the GEMM epilogue (da never reaches HBM)
 at::Tensor gemm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& w2, const at::Tensor& gu) {
     check_cuda(gu, "gu");
@@ -901,6 +930,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gemm_swiglu_bwd(Tensor dy, Tensor w2, Tensor gu) -> Tensor");
     m.def("gemm_swiglu_fwd(Tensor x, Tensor w13) -> (Tensor, Tensor)");
     m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int S, int D, int rot_cols) -> Tensor");
+    m.def("gemm_fp8_acc(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor(a!) c, float beta, int splits) -> ()");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb) -> Tensor");
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
@@ -947,6 +977,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
     m.impl("gemm_swiglu_fwd", &gemm_swiglu_fwd);
     m.impl("gemm_qkv_rope", &gemm_qkv_rope);
+    m.impl("gemm_fp8_acc", &gemm_fp8_acc);
     m.impl("gemm_fp8", &gemm_fp8);
     m.impl("cast_fp8", &cast_fp8);
     m.impl("transpose_bf16", &transpose_bf16);

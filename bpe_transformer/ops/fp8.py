@@ -176,11 +176,31 @@ def dgrad(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8St
     return mm_fp8(g8, w8t, g_state.inv_scale[g_slot], w_state.inv_scale[w_slot])
 
 
+_WGRAD_HIP = True  # fp8 weight gradients on the hand kernel's split-K form (True) or hipBLASLt (module flag)
+
+
+def wgrad_acc(g8t: Tensor, xt8: Tensor, sg: Tensor, sx: Tensor, out: Tensor) -> None:
+    """``out += (g8t @ xt8.T) * sg * sx``: the fp8 weight gradient (g8t [N, tokens] e5m2, xt8 [K, tokens] e4m3)
+    accumulated into a bf16 / fp32 gradient view [N, K].  The hand kernel's split-K form (fp32 partials and an
+    ordered reduce with beta = 1 straight into ``out``) when ``_WGRAD_HIP`` and the shape is tile-aligned, else
+    hipBLASLt's ``_scaled_mm`` and an add."""
+    N, T = g8t.shape
+    K = xt8.shape[0]
+    if (_WGRAD_HIP and N % 256 == 0 and K % 256 == 0 and T % 128 == 0 and out.stride(1) == 1
+            and g8t.stride(0) % 16 == 0 and xt8.stride(0) % 16 == 0):
+        from .gemm import choose_splits_pp
+
+        ops().gemm_fp8_acc(g8t, xt8, sg.reshape(1), sx.reshape(1), out, 1.0, choose_splits_pp(N, K, T // 2))
+        return
+    out.add_(torch._scaled_mm(g8t, xt8.t(), scale_a=sg, scale_b=sx, out_dtype=torch.bfloat16))
+
+
 def grads(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8State, w_slot: int,
-          xt8: Tensor | None = None, x_state: Fp8State | None = None, x_slot: int = 0):
+          xt8: Tensor | None = None, x_state: Fp8State | None = None, x_slot: int = 0, dw_out: Tensor | None = None):
     """Input gradient ``g @ W`` and, with ``xt8``, weight gradient ``g^T @ X`` of one projection from ONE e5m2 cast
-    of g: (dX, dW or None).  dW = g8t [N, tokens] x xt8 [K, tokens] -> [N, K] bf16, both operands contiguous along
-    the token reduction; its scale is g's inverse scale times X's (slot ``x_slot`` of ``x_state``)."""
+    of g: (dX, dW or None).  dW = g8t [N, tokens] x xt8 [K, tokens] -> [N, K], both operands contiguous along the
+    token reduction; its scale is g's inverse scale times X's (slot ``x_slot`` of ``x_state``).  With ``dw_out``
+    the weight gradient is accumulated into it (:func:`wgrad_acc`) and None is returned in its place."""
     if xt8 is None:
         return dgrad(g_state, g, g_slot, w8t, w_state, w_slot), None
     g = g.contiguous()
@@ -191,6 +211,9 @@ def grads(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8St
         g8t = g8.t().contiguous()
     gi = g_state.inv_scale[g_slot]
     dx = mm_fp8(g8, w8t, gi, w_state.inv_scale[w_slot])
+    if dw_out is not None:
+        wgrad_acc(g8t, xt8, gi, x_state.inv_scale[x_slot], dw_out)
+        return dx, None
     dw = mm_fp8(g8t, xt8, gi, x_state.inv_scale[x_slot])
     return dx, dw
 

@@ -855,6 +855,26 @@ def test_fp8_grads_weight_gradient(gpu_device):
     assert rel(dw.float(), g.float().t() @ x.float()) < 0.1  # fp8 rounding of both operands
 
 
+@pytest.mark.parametrize("c_dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_fp8_acc_splitk(gpu_device, c_dtype, splits):
+    """Split-K fp8 GEMM accumulating into C (the fp8 weight-gradient form): exact on small-integer operands with
+    power-of-two scales, e5m2 x e4m3, beta = 1 onto an existing C."""
+    g = torch.Generator(device="cpu").manual_seed(splits)
+    M, N, K = 512, 256, 1536
+    a = torch.randint(-4, 5, (M, K), generator=g).float()
+    b = torch.randint(-4, 5, (N, K), generator=g).float()
+    c0 = torch.randint(-8, 9, (M, N), generator=g).float()
+    a8 = a.to(torch.float8_e5m2).to(gpu_device)
+    b8 = b.to(torch.float8_e4m3fn).to(gpu_device)
+    c = c0.to(c_dtype).to(gpu_device)
+    sa = torch.tensor([0.5], device=gpu_device)
+    sb = torch.tensor([0.25], device=gpu_device)
+    torch.ops.bpe_hip.gemm_fp8_acc(a8, b8, sa, sb, c, 1.0, splits)
+    ref = (c0 + (a @ b.t()) * 0.125).to(c_dtype)
+    assert torch.equal(c.cpu(), ref)
+
+
 def test_update_scales(gpu_device):
     n, H = 3, 4
     amax = torch.tensor([2.0, 0.0, 1000.0], device=gpu_device).view(torch.int32).clone()

@@ -155,6 +155,17 @@ class EagerLM(nn.Module):
         return F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), y.reshape(-1))
 
 
+@pytest.fixture(autouse=True)
+def _fixed_dw_routes(monkeypatch):
+    """The dW route of a shape missing from ops/tuning/dw_routes.json is otherwise timed on first use (ops/gemm.py),
+    so two runs could take different kernels -- different bf16 roundings that a 150-step trajectory amplifies.
+    Here every off-table shape takes its first candidate, from a fresh route cache."""
+    from bpe_transformer.ops import gemm
+
+    monkeypatch.setattr(gemm, "_AUTOTUNE", False)
+    monkeypatch.setattr(gemm, "_route", {})
+
+
 @functools.lru_cache(maxsize=1)
 def _tokens():
     from bpe_transformer import train_bpe
