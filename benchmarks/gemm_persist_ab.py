@@ -36,7 +36,10 @@ def main():
     ap.add_argument("--tokens", type=int, default=131072)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--head", action="store_true", help="the LM-head GEMMs (vocab 50432 padded) instead")
     a = ap.parse_args()
+    if a.head:
+        return head(a)
     h = ops()
     T = a.tokens
     d, F, Nq = DIMS[a.model]
@@ -103,6 +106,37 @@ def main():
             print(json.dumps(row), flush=True)
     finally:
         h.gpp_persist_config(prev)
+
+
+def head(a):
+    """LM head at GPT-2 width: logits = h . Wp^T (K = 768, 13.2 GB written) and dh = dlogits . Wp (K = 50432) on
+    the persistent ping-pong kernel vs hipBLASLt (TN for dh, as ops/loss.py runs it)."""
+    h_ = ops()
+    T, d, V = a.tokens, 768, 50432
+    bf = dict(device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(T, d, **bf)
+    w = (0.05 * torch.randn(V, d, device="cuda")).to(torch.bfloat16)
+    wt = w.t().contiguous()
+    logits = torch.empty(T, V, **bf)
+    dh = torch.empty(T, d, **bf)
+    f = 2.0 * T * d * V
+    arms = {
+        "fwd pp": lambda: h_.gemm_pp(x, True, w, True, logits, 0.0, 1),
+        "fwd hipBLASLt": lambda: torch.matmul(x, w.t(), out=logits),
+        "dX pp (B K-major)": lambda: h_.gemm_pp(logits, True, wt, True, dh, 0.0, 1),
+        "dX hipBLASLt TN": lambda: torch.matmul(logits, wt.t(), out=dh),
+    }
+    for fn in arms.values():
+        fn()
+    torch.cuda.synchronize()
+    t = {k: [] for k in arms}
+    for _ in range(a.rounds):
+        for k, fn in arms.items():
+            t[k].append(timeit(fn, 3))
+    for k, v in t.items():
+        m = statistics.median(v)
+        print(json.dumps({"op": "lm head " + k, "tokens": T, "ms": round(m, 3), "tflops": round(f / m / 1e9, 1)}),
+              flush=True)
 
 
 if __name__ == "__main__":
