@@ -87,8 +87,7 @@ def main():
         if not a.bwd_ab:
             return
     if a.bwd_ab:
-        arms = {"fused": 1, "split": 0, "split_dq1wg": 2, "split_dkv1wg": 4, "split_both1wg": 6,
-                "dkv_nodma": 8, "dkv_noexp": 16, "dkv_nodvdk": 32, "dkv_nosdp": 64, "dkv_noexp_nodvdk": 48, "dkv_stagger": 128, "dkv_pipe": 256, "dkv_pipe_stagger": 384, "dkv_prefetch": 768, "dkv_prefetch_stagger": 896, "dkv_persist": 2048, "dq_persist": 4096, "both_persist": 6144}
+        arms = {"fused": 1, "split": 0}
         if a.bwd_arms:
             arms = {n: arms[n] for n in a.bwd_arms}
         prev = hip.fa_bwd_config(-1)
