@@ -40,14 +40,17 @@ def _batch(rank: int, dev):
     return x.to(dev), torch.roll(x, -1, 1).to(dev)
 
 
-def _worker(rank, world, port, bucket_mb, comm, out_q):
+def _worker(rank, world, port, bucket_mb, comm, out_q, fp8=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")  # both ranks share cuda:0
     from bpe_transformer.parallel import cleanup, init_distributed
     from bpe_transformer.train.engine import TrainEngine
 
     info = init_distributed("cuda", backend="gloo")
-    eng = TrainEngine(_model(info.device), info, lr=1e-3, weight_decay=0.0, max_grad_norm=1.0, bucket_mb=bucket_mb,
+    model = _model(info.device)
+    if fp8:  # fp8 projections incl. the fp8 weight gradients accumulated into the flat buffer's bucket views
+        model.enable_fp8()
+    eng = TrainEngine(model, info, lr=1e-3, weight_decay=0.0, max_grad_norm=1.0, bucket_mb=bucket_mb,
                       ddp_check_every=1,  # also asserts bit-identical grads / weights across the ranks
                       comm_dtype=torch.float32 if comm == "fp32" else None)
     eng.train_step([_batch(rank, info.device)])
@@ -57,6 +60,26 @@ def _worker(rank, world, port, bucket_mb, comm, out_q):
     # numpy copies travel by value; torch tensors go through fd sharing whose listener dies with this process
     out_q.put((rank, g1.numpy().copy(), eng.flat.data.float().cpu().numpy().copy(), len(eng.ddp.buckets)))
     cleanup()
+
+
+def test_dp2_gpu_fp8(gpu_device):
+    """Two ranks with fp8 projections (e4m3 forward, e5m2 input and weight gradients, the latter accumulated by the
+    split-K fp8 kernel straight into the flat buffer's views): several buckets, gradients and weights identical on
+    both ranks after two steps, all finite."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 0.25, "grad", q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (torch.from_numpy(g), torch.from_numpy(d), nb) for r, g, d, nb in (q.get(timeout=240) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][2] > 1
+    assert torch.equal(res[0][0], res[1][0]), "all-reduced gradients differ between ranks"
+    assert torch.equal(res[0][1], res[1][1]), "ranks diverged"
+    assert bool(torch.isfinite(res[0][0]).all()) and float(res[0][0].norm()) > 0
 
 
 @pytest.mark.parametrize("comm", ["grad", "fp32"])
