@@ -295,6 +295,10 @@ __device__ __forceinline__ void ktile(char* __restrict__ cur, char* __restrict__
 // after group 0, never before the issuing wave's wait).  WAR: a region of the other buffer is refilled at
 // least one barrier after its last read of K-tile kt-1 (A rows: phases 0 / 2, B halves: phases 3 / 1).
 // Last K-tile (no issue): vmcnt(2) in phase 0 (B rows [32, 64) of this tile), vmcnt(0) afterwards.
+#ifndef BPE_GPP_RELAX  // build define: phase 2 of the spread schedule waits vmcnt(6) (1) or vmcnt(4) (0)
+#define BPE_GPP_RELAX 1
+#endif
+
 struct SpreadOff {
     int a0[2], a1[2], b0[2], b1[2];  // source offsets (elements from the K-tile origin) of this thread's pieces
     int la0, la1, lb0, lb1;          // wave-uniform LDS chunk index of each piece pair (piece j at + 64 j)
@@ -353,7 +357,11 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     char* Bc = cur + OPB;
     if (DIAG == 1) dma = false;
     // one phase: fragment reads (done by the caller), pieces of (tile, off, img, lbase), wait, barrier, MFMAs
-    auto phase = [&](const __bf16* t0, const int (&off)[2], char* img, int lb, int m, int n, bool last_nodma_wait2) {
+    // RELAX: phase 2 (m1, n1) retires nothing that a read before phase 3's barrier needs (its own A rows of K-tile
+    // kt + 1 are first read in phase 0 of kt + 1; the group's B halves it issued are retired in phase 3 / phase 0),
+    // so it waits vmcnt(6) and leaves the piece pair issued two load sections ago in flight one section longer
+    auto phase = [&](const __bf16* t0, const int (&off)[2], char* img, int lb, int m, int n, bool last_nodma_wait2,
+                     bool relax = false) {
         if (dma) {
             if constexpr (SPLIT) dma_one(t0, off[0], img, lb);
             else dma_pair(t0, off, img, lb);
@@ -362,6 +370,7 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         } else if (dma) {
             if constexpr (SPLIT) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+            else if (BPE_GPP_RELAX && relax) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
         } else if (last_nodma_wait2) {
             asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
@@ -391,7 +400,7 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     phase(bn, so.b0, nxt + OPB, so.lb0, 0, 1, false);
     // phase 2: (m1, n1)
     load_a<AK, BKM, true>(f, Ac, g, 1, l);
-    phase(bn, so.b1, nxt + OPB, so.lb1, 1, 1, false);
+    phase(bn, so.b1, nxt + OPB, so.lb1, 1, 1, false, true);
     // phase 3: (m1, n0)
     load_b<AK, BKM, true>(f, Bc, wl, 0, l);
     phase(an, so.a1, nxt, so.la1, 1, 0, false);

@@ -36,7 +36,7 @@ void launch_embed_bwd(int dtype, const void* dout, const int64_t* sorted_ids, co
 // optim.hip
 void launch_adamw(int gdtype, float* p, float* m, float* v, const void* g, void* pout_bf16, size_t n, float lr,
                   double b1, double b2, float eps, float wd, float bc1, float bc2_sqrt, const float* gscale,
-                  const int* nstep, hipStream_t s);
+                  const int* nstep, const uint8_t* wd_mask, hipStream_t s);
 void launch_adam_count(int* nstep, const float* gscale, hipStream_t s);
 void launch_sumsq_partial(int dtype, const void* x, size_t n, float* partial, int nblocks, hipStream_t s);
 void launch_norm_finalize(const float* partial, int np, float max_norm, float* out_norm, float* out_coef,

@@ -54,19 +54,21 @@ __global__ void adam_count_kernel(int* __restrict__ nstep, const float* __restri
     }
 }
 
-__device__ __forceinline__ void adam_one(float& p, float& m, float& v, float g, const AdamArgs& a) {
-    p = p * (1.f - a.lr * a.wd);
+__device__ __forceinline__ void adam_one(float& p, float& m, float& v, float g, const AdamArgs& a, float wd) {
+    p = p * (1.f - a.lr * wd);
     m = a.b1 * m + (1.f - a.b1) * g;
     v = a.b2 * v + (1.f - a.b2) * g * g;
     const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
     p = p - (a.lr / a.bc1) * (m / denom);
 }
 
+// wdm (optional): one byte per 64 elements, nonzero where weight decay applies -- the whole flat buffer's
+// decay / no-decay segments (64-aligned) in ONE launch instead of one launch per segment
 template <typename GT>
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                                     const GT* __restrict__ g, __bf16* __restrict__ pout, size_t n,
                                                     AdamArgs a, const float* __restrict__ gscale,
-                                                    const int* __restrict__ nstep) {
+                                                    const int* __restrict__ nstep, const uint8_t* __restrict__ wdm) {
     const float sc = gscale ? *gscale : 1.f;
     if (!(sc >= 0.f)) return;  // non-finite gradient norm: the step is skipped on the device (no host sync)
     if (nstep) adam_bias_from_count(a, nstep);
@@ -80,10 +82,11 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float
         f32x4 vv = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(v + 4 * i));
         float gv[4];
         G4<GT>::load(g + 4 * i, gv);
+        const float wd = wdm == nullptr || wdm[i >> 4] ? a.wd : 0.f;  // 16 four-element vectors per 64 elements
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             float pj = pv[j], mj = mv[j], vj = vv[j];
-            adam_one(pj, mj, vj, gv[j] * sc, a);
+            adam_one(pj, mj, vj, gv[j] * sc, a, wd);
             pv[j] = pj; mv[j] = mj; vv[j] = vj;
         }
         __builtin_nontemporal_store(pv, reinterpret_cast<f32x4*>(p + 4 * i));
@@ -98,7 +101,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float
     const size_t t = n4 * 4 + blockIdx.x * (size_t)256 + threadIdx.x;
     if (blockIdx.x == 0 && t < n) {
         float pj = p[t], mj = m[t], vj = v[t];
-        adam_one(pj, mj, vj, ld1<GT>(g + t) * sc, a);
+        adam_one(pj, mj, vj, ld1<GT>(g + t) * sc, a, wdm == nullptr || wdm[t >> 6] ? a.wd : 0.f);
         p[t] = pj; m[t] = mj; v[t] = vj;
         if (pout) st1<__bf16>(pout + t, pj);
     }
@@ -179,14 +182,16 @@ using namespace bpe;
 
 void launch_adamw(int gdtype, float* p, float* m, float* v, const void* g, void* pout_bf16, size_t n, float lr,
                   double b1, double b2, float eps, float wd, float bc1, float bc2_sqrt, const float* gscale,
-                  const int* nstep, hipStream_t s) {
+                  const int* nstep, const uint8_t* wdm, hipStream_t s) {
     if (n == 0) return;
     AdamArgs a{lr, (float)b1, (float)b2, eps, wd, bc1, bc2_sqrt, b1, b2};
     const int grid = stream_grid(n / 4 + 1, 256, 2048);
     if (gdtype == DT_BF16)
-        adamw_kernel<__bf16><<<grid, 256, 0, s>>>(p, m, v, (const __bf16*)g, (__bf16*)pout_bf16, n, a, gscale, nstep);
+        adamw_kernel<__bf16><<<grid, 256, 0, s>>>(p, m, v, (const __bf16*)g, (__bf16*)pout_bf16, n, a, gscale, nstep,
+                                                  wdm);
     else
-        adamw_kernel<float><<<grid, 256, 0, s>>>(p, m, v, (const float*)g, (__bf16*)pout_bf16, n, a, gscale, nstep);
+        adamw_kernel<float><<<grid, 256, 0, s>>>(p, m, v, (const float*)g, (__bf16*)pout_bf16, n, a, gscale, nstep,
+                                                 wdm);
 }
 
 void launch_adam_count(int* nstep, const float* gscale, hipStream_t s) {

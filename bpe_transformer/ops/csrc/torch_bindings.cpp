@@ -212,7 +212,8 @@ at::Tensor embed_bwd(const at::Tensor& dout, const at::Tensor& ids, int64_t voca
 // ---------------------------------------------------------------- optimizer
 void adamw_step(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& grad, const c10::optional<at::Tensor>& pout,
                 double lr, double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt,
-                const c10::optional<at::Tensor>& gscale, const c10::optional<at::Tensor>& nstep) {
+                const c10::optional<at::Tensor>& gscale, const c10::optional<at::Tensor>& nstep,
+                const c10::optional<at::Tensor>& wd_mask) {
     check_cuda(p, "param");
     TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
                 "adamw: master param / moments must be fp32");
@@ -233,9 +234,16 @@ void adamw_step(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& grad
                     "adamw: nstep must be a one-element int32 tensor on the parameters' device");
         ns = nstep->data_ptr<int>();
     }
+    const uint8_t* wm = nullptr;  // one byte per 64 elements: weight decay applies where nonzero
+    if (wd_mask.has_value() && wd_mask->defined()) {
+        TORCH_CHECK(wd_mask->scalar_type() == at::kByte && wd_mask->is_contiguous() &&
+                        wd_mask->device() == p.device() && wd_mask->numel() >= (p.numel() + 63) / 64,
+                    "adamw: wd_mask must be a contiguous uint8 tensor of one byte per 64 elements");
+        wm = wd_mask->data_ptr<uint8_t>();
+    }
     DevGuard g(p.device());
     launch_adamw(dt_code(grad), p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(), po,
-                 p.numel(), (float)lr, b1, b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, gs, ns,
+                 p.numel(), (float)lr, b1, b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, gs, ns, wm,
                  cur_stream());
 }
 
@@ -923,7 +931,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("embed_fwd(Tensor weight, Tensor ids) -> Tensor");
     m.def("embed_bwd(Tensor dout, Tensor ids, int vocab) -> Tensor");
     m.def("adamw_step(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor grad, Tensor(d!)? pout, float lr, float b1, "
-          "float b2, float eps, float wd, float bc1, float bc2_sqrt, Tensor? gscale, Tensor? nstep=None) -> ()");
+          "float b2, float eps, float wd, float bc1, float bc2_sqrt, Tensor? gscale, Tensor? nstep=None, "
+          "Tensor? wd_mask=None) -> ()");
     m.def("adam_count_step(Tensor(a!) nstep, Tensor? gscale) -> ()");
     m.def("grad_norm(Tensor[] tensors, float max_norm) -> (Tensor, Tensor)");
     m.def("scale_(Tensor(a!) x, Tensor coef) -> ()");

@@ -69,6 +69,7 @@ def fused_adamw_step(
     step: int,
     grad_scale: Tensor | None = None,
     nstep: Tensor | None = None,
+    wd_mask: Tensor | None = None,
 ) -> None:
     """One AdamW step over flat fp32 buffers (one kernel launch on the GPU).
 
@@ -78,7 +79,10 @@ def fused_adamw_step(
     ``nstep`` (optional one-element int32 tensor, see :func:`count_adam_step`)
     is the number of updates applied so far INCLUDING this one; when given,
     the bias correction is computed from it (on the device) and ``step`` is
-    ignored, so skipped non-finite steps do not shift bc1/bc2.
+    ignored, so skipped non-finite steps do not shift bc1/bc2.  ``wd_mask``
+    (optional uint8, one byte per 64 elements) applies ``weight_decay`` only
+    where it is nonzero: a flat buffer's decay and no-decay segments in one
+    launch.
     """
     if nstep is not None and not param_fp32.is_cuda:
         step = int(nstep.item())
@@ -86,14 +90,21 @@ def fused_adamw_step(
     bc2_sqrt = (1.0 - beta2**step) ** 0.5
     if param_fp32.is_cuda:
         ops().adamw_step(param_fp32, exp_avg, exp_avg_sq, grad, param_bf16_out, lr, beta1, beta2, eps, weight_decay,
-                         bc1, bc2_sqrt, grad_scale, nstep)
+                         bc1, bc2_sqrt, grad_scale, nstep, wd_mask)
         return
+    if wd_mask is not None:  # per-64-element decay on the CPU path: expand the mask
+        wdv = torch.repeat_interleave(wd_mask.to(torch.float32), 64)[: param_fp32.numel()] * weight_decay
+    else:
+        wdv = None
     g = grad.float()
     if grad_scale is not None:
         if not bool(grad_scale >= 0):  # non-finite grad norm: skip (same rule as the kernel)
             return
         g = g * grad_scale
-    param_fp32.mul_(1.0 - lr * weight_decay)
+    if wdv is not None:
+        param_fp32.mul_(1.0 - lr * wdv)
+    else:
+        param_fp32.mul_(1.0 - lr * weight_decay)
     exp_avg.mul_(beta1).add_(g, alpha=1.0 - beta1)
     exp_avg_sq.mul_(beta2).addcmul_(g, g, value=1.0 - beta2)
     denom = (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)

@@ -297,6 +297,29 @@ def test_fused_adamw_kernel_vs_cpu(gpu_device, n, gdtype):
     assert torch.equal(out.cpu(), gp.cpu().to(torch.bfloat16))
 
 
+def test_flat_adamw_one_launch_matches_segments(gpu_device):
+    """The masked single-launch AdamW (one byte per 64 elements selects weight decay) equals the per-segment
+    launches bitwise over a model with decayed matrices and undecayed norm gains, three steps."""
+    from bpe_transformer.models import TransformerLM
+    from bpe_transformer.optim import FlatAdamW, FlatParameters
+
+    res = []
+    for masked in (True, False):
+        torch.manual_seed(0)
+        m = TransformerLM(300, 64, 64, 2, 4, 128, device=gpu_device, dtype=torch.bfloat16)
+        flat = FlatParameters.from_module(m)
+        opt = FlatAdamW(flat, lr=1e-2, weight_decay=0.1)
+        assert opt.wd_mask is not None and len(opt.segments) > 2
+        if not masked:
+            opt.wd_mask = None
+        g = torch.Generator(device="cpu").manual_seed(1)
+        for _ in range(3):
+            flat.grad.copy_(torch.randn(flat.grad.shape, generator=g).to(flat.grad.dtype))
+            opt.step()
+        res.append(opt.master.clone())
+    assert torch.equal(res[0], res[1])
+
+
 def test_flat_adamw_bf16_master(gpu_device):
     from bpe_transformer.optim import FlatAdamW, FlatParameters
 
