@@ -82,9 +82,10 @@ def scaled_dot_product_attention(Q: Tensor, K: Tensor, V: Tensor, mask: Tensor |
 
 
 def prerotate_default(head_dim: int) -> bool:
-    """Rotate Q / K once in the QKV activation (``rope_qk_``) instead of inside the attention kernels: the
-    D = 64 forward (v8) then stages K by LDS-DMA with no per-tile rotation.  ``BPE_ROPE_PREROTATE=0`` keeps the
-    fused-RoPE kernels."""
+    """Rotate Q / K once in the QKV activation instead of inside the attention kernels: the D = 64 forward (v8)
+    then stages K by LDS-DMA with no per-tile rotation.  The fused blocks apply that rotation in the QKV GEMM's
+    epilogue (``gemm_qkv_rope``; ``rope_qk_`` in place on the fp8 path and here, for a given qkv tensor).
+    ``BPE_ROPE_PREROTATE=0`` keeps the fused-RoPE attention kernels."""
     return head_dim == 64 and os.environ.get("BPE_ROPE_PREROTATE", "1") == "1"
 
 
