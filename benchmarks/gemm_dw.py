@@ -48,9 +48,36 @@ def sweep():
         del dy, x, g
 
 
+def layouts():
+    """GPT-2 B 128 dW shapes (T = 131072): the 256-tile kernel at its model split count, the ping-pong kernel on
+    the same token-major operands over a split sweep, and the ping-pong kernel on K-major copies of both operands
+    (dY^T, X^T: what the loop reaches when no operand is read transposed), TFLOP/s."""
+    from bpe_transformer.ops.gemm import choose_splits_pp
+    T = 131072
+    for n, k in SHAPES["gpt2"][1]:
+        dy = torch.randn(T, n, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(T, k, device="cuda", dtype=torch.bfloat16)
+        dyt, xt = dy.t().contiguous(), x.t().contiguous()
+        g = torch.zeros(n, k, device="cuda", dtype=torch.bfloat16)
+        fl = 2.0 * n * k * T
+        tf = lambda fn: round(fl / statistics.median(bench(fn) for _ in range(3)) / 1e9)  # noqa: E731
+        row = {"shape": [n, k, T], "hip256": tf(lambda: hip().gemm(dy, False, x, False, g, 1.0,
+                                                                    choose_splits_256(n, k, T), 256)),
+               "pp_model_splits": choose_splits_pp(n, k, T)}
+        for sp in sorted({choose_splits_pp(n, k, T), 4, 8, 12, 16, 24, 32}):
+            if (n // 256) * (k // 256) * sp > 4 * 256:
+                continue
+            row[f"pp_mn_s{sp}"] = tf(lambda: hip().gemm_pp(dy, False, x, False, g, 1.0, sp))
+            row[f"pp_kmajor_s{sp}"] = tf(lambda: hip().gemm_pp(dyt, True, xt, True, g, 1.0, sp))
+        print(json.dumps(row), flush=True)
+        del dy, x, dyt, xt, g
+
+
 def main():
     if "--sweep" in sys.argv:
         return sweep()
+    if "--layouts" in sys.argv:
+        return layouts()
     out = {"variant": os.environ.get("BPE_G256_VARIANT", "0")}
     for model, (T, shapes) in SHAPES.items():
         tot_b = tot_o = 0.0
