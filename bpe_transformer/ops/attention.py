@@ -83,10 +83,12 @@ def scaled_dot_product_attention(Q: Tensor, K: Tensor, V: Tensor, mask: Tensor |
 
 def prerotate_default(head_dim: int) -> bool:
     """Rotate Q / K once in the QKV activation instead of inside the attention kernels: the D = 64 forward (v8)
-    then stages K by LDS-DMA with no per-tile rotation.  The fused blocks apply that rotation in the QKV GEMM's
-    epilogue (``gemm_qkv_rope``; ``rope_qk_`` in place on the fp8 path and here, for a given qkv tensor).
-    ``BPE_ROPE_PREROTATE=0`` keeps the fused-RoPE attention kernels."""
-    return head_dim == 64 and os.environ.get("BPE_ROPE_PREROTATE", "1") == "1"
+    then stages K by LDS-DMA with no per-tile rotation, and the split backward (D = 64 and 128) takes the pre-rotated
+    operands as they are (at D = 128 the in-kernel form costs the backward a rotated copy: B 4 S 2048, forward +
+    backward 0.505 vs 0.618 ms MHA, 0.877 vs 1.048 ms GQA 32:8, ``profiles/bench/attn_d128_split_r4.log``).  The fused
+    blocks apply that rotation in the QKV GEMM's epilogue (``gemm_qkv_rope``; ``rope_qk_`` in place on the fp8 path
+    and here, for a given qkv tensor).  ``BPE_ROPE_PREROTATE=0`` keeps the fused-RoPE attention kernels."""
+    return head_dim in (64, 128) and os.environ.get("BPE_ROPE_PREROTATE", "1") == "1"
 
 
 class _FlashAttnQKVFn(torch.autograd.Function):

@@ -104,7 +104,7 @@ __device__ __forceinline__ u16x8 rope_u16x8(u16x8 v, const float* cs, const floa
     return pack8(x, mul);
 }
 
-// LDS-DMA staging of a 64-row x 128-byte tile (D = 64) into the swizzled image of swz<128>: the DMA writes lane-
+// LDS-DMA staging of a 64-row x 128-byte tile (D = 64; dma_tile64_buf also 256-byte rows, D = 128) into the swizzled image of swz<128>: the DMA writes lane-
 // linearly (wave-instruction i of wave w fills physical chunks 64 (cpw w + i) + lane), so each lane loads the
 // SOURCE chunk the swizzle puts at its physical slot (c = pc ^ sigma(r)).  Rows past the end are loaded clamped
 // (row S - 1): the kernels mask their scores, so those rows only ever meet a zero P / dS.  No registers hold the
@@ -135,34 +135,38 @@ __device__ __forceinline__ void dma_tile64(const __bf16* base, long ld, int r0, 
 // compiled in the device pass only.
 __device__ __forceinline__ int head_bytes(long ld, int S, int D) { return (int)(((long)(S - 1) * ld + D) * 2); }
 
-template <int NW>
+template <int NW, int RB = 128>
 struct DmaVoff {
-    static constexpr int CPW = 512 / (NW * 64);
+    static constexpr int CPW = 4 * RB / (NW * 64);  // wave-instructions per wave: 4 RB chunks of 16 bytes per tile
     unsigned v[CPW];
 };
 
-template <int NW>
-__device__ __forceinline__ DmaVoff<NW> dma_voff(long ld, int w, int l) {
-    DmaVoff<NW> o;
+// RB = 128 (D = 64) or 256 (D = 128): the tile image of swz<RB>, 64 rows of RB bytes
+template <int NW, int RB = 128>
+__device__ __forceinline__ DmaVoff<NW, RB> dma_voff(long ld, int w, int l) {
+    constexpr int CPR = RB / 16;  // chunks per row
+    DmaVoff<NW, RB> o;
 #pragma unroll
-    for (int i = 0; i < DmaVoff<NW>::CPW; ++i) {
-        const int e = 64 * (DmaVoff<NW>::CPW * w + i) + l, r = e >> 3, pc = e & 7;
-        const int sg = (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+    for (int i = 0; i < DmaVoff<NW, RB>::CPW; ++i) {
+        const unsigned e = 64 * (DmaVoff<NW, RB>::CPW * w + i) + l;
+        const int r = e / CPR, pc = e % CPR;
+        const int sg = RB == 128 ? ((((r >> 1) & 1) << 2) | ((r >> 2) & 3)) : (((r & 3) << 2) | ((r >> 2) & 3));
         o.v[i] = (unsigned)((r * ld + ((pc ^ sg) << 3)) * 2);
     }
     return o;
 }
 
-template <int NW>
-__device__ __forceinline__ void dma_tile64_buf(const __bf16* base, int nbytes, const DmaVoff<NW>& vo, int r0, long ld,
-                                               char* img, int w) {
+template <int NW, int RB = 128>
+__device__ __forceinline__ void dma_tile64_buf(const __bf16* base, int nbytes, const DmaVoff<NW, RB>& vo, int r0,
+                                               long ld, char* img, int w) {
 #if defined(__HIP_DEVICE_COMPILE__)  // device pass only: the host pass cannot instantiate the resource type
+    constexpr int CPW = DmaVoff<NW, RB>::CPW;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nbytes, 0x00020000);
     const unsigned soff = (unsigned)((long)r0 * ld * 2);
 #pragma unroll
-    for (int i = 0; i < DmaVoff<NW>::CPW; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + 64 * (DmaVoff<NW>::CPW * w + i) * 16), 16,
-                                                 vo.v[i], soff, 0, 0);
+    for (int i = 0; i < CPW; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + 64 * (CPW * w + i) * 16), 16, vo.v[i], soff,
+                                                 0, 0);
 #endif
 }
 

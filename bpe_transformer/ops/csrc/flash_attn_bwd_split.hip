@@ -1,4 +1,4 @@
-// Flash attention backward, split form (D = 64), gfx950 (MI355X).
+// Flash attention backward, split form (D = 64 and D = 128), gfx950 (MI355X).
 //
 // Parity target: the gradient of reference contracts K7/K10 (`tests/adapters.py:92-184`); checked against
 // autograd of the fp32 oracle (tests/test_kernels_gpu.py).
@@ -27,7 +27,14 @@
 // atomics floor, the 402 MB/layer accumulator (4.8 GB at GPT-2 B 128), the zeroing and the two side passes go.
 // GQA: one dK / dV workgroup per KV head sweeps the G query heads of its group (no partials, no reduce kernel).
 // With RoPE fused into the kernels (ROPE_IN: Q / K rotated on their way to LDS) the tiles are register-staged,
-// 64 rows each.
+// 64 rows each (D = 64 only).
+//
+// D = 128: the same two kernels on 256-byte rows (swz<256>), 64-row tiles (LDS: 64 KiB per workgroup), K / V (dQ
+// kernel) and Q / dO (dK/dV kernel) always by LDS-DMA; the pinned operands and accumulators double, so the dQ
+// kernel reads its K / V fragments per k-step instead of in one batch and the dK/dV kernel (256 accumulator
+// registers per lane for dK^T and dV^T alone) runs one wave per SIMD.  RoPE is applied before (fa_bwd rotates a copy
+// of Q / K when the forward rotated inside its kernel).  This replaces the fused form's fp32 dQ atomics, dQ
+// accumulator, delta pre-pass and convert pass for D = 128 as well, and makes it deterministic.
 #include "fa_common.h"
 #include "kernels.h"
 
@@ -37,11 +44,16 @@ namespace bpe {
 namespace fa {
 namespace split {
 
-constexpr int D = 64, RB = 128, TILE = 64 * RB, KS = 4;
-
-// staged 16-byte chunks per thread and tensor for one 64-row tile (512 chunks)
 // 4 waves x 32 rows per workgroup, 2 workgroups per CU (2 waves per SIMD at <= 256 VGPRs)
-constexpr int NW = 4, CPT = 512 / (NW * 64);
+constexpr int NW = 4;
+
+// per head size: tile row bytes, 64-row tile bytes, 16-deep k-steps over d, 32-wide d tiles of an accumulator, and
+// staged 16-byte chunks per thread and tensor for one register-staged 64-row tile
+template <int D>
+struct Geo {
+    static_assert(D == 64 || D == 128, "split backward: D = 64 or 128");
+    static constexpr int RB = 2 * D, TILE = 64 * RB, KS = D / 16, ND = D / 32, CPT = 4 * RB / (NW * 64);
+};
 
 // Per-workgroup s_memtime stamps (a diagnostic variant build: ops.build --variant stamps -D BPE_FA_STAMPS): slot 0
 // entry, 1 after the prologue barrier, 3 after the tile loop, 5 the tile count; rows 0.. the dQ kernel's workgroups,
@@ -57,21 +69,26 @@ __device__ long long g_stamps[65536 * 8];
 #define FA_STAMP(base, i, v)
 #endif
 
-template <bool CAUSAL, bool ROPE, bool ROPE_IN>
+// (D = 128: 2 waves per SIMD with 7-9 VGPRs spilled measured 0.44 / 0.71 ms against 0.49 / 0.80 ms at one wave
+// per SIMD without spills, B 4 S 2048 H 16 / GQA 32:8, profiles/bench/attn_d128_split_r4.log)
+template <int D, bool CAUSAL, bool ROPE, bool ROPE_IN>
 __global__ void __launch_bounds__(NW * 64, 2)
 fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                  long ld_q, long ld_kv, const __bf16* __restrict__ O, long ld_o, const __bf16* __restrict__ dO,
                  long ld_do, const float* __restrict__ LSE, float* __restrict__ DELTA, __bf16* __restrict__ dQ,
                  long ld_dq, const float* __restrict__ cosT, const float* __restrict__ sinT, int B, int H, int Hkv,
                  int S, float scale_log2, float scale, int group) {
+    using G = Geo<D>;
+    constexpr int RB = G::RB, TILE = G::TILE, KS = G::KS, ND = G::ND, CPT = G::CPT;
+    static_assert(D == 64 || !ROPE_IN, "D = 128: Q / K are rotated before the kernels");
     constexpr int NT = NW * 64, QB = 32 * NW;
     // keys per K / V tile (one barrier each): 128 with LDS-DMA staging (two 64-row images side by side), 64 with
-    // register staging (ROPE_IN: K is rotated on its way to LDS)
+    // register staging (ROPE_IN: K is rotated on its way to LDS) and at D = 128 (64 KiB of LDS already)
     constexpr bool DM = !ROPE_IN;
-    constexpr int KT = DM ? 128 : 64, NSUB = KT / 64, BUF = NSUB * TILE;
+    constexpr int KT = (DM && D == 64) ? 128 : 64, NSUB = KT / 64, BUF = NSUB * TILE;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* Ks = smem;            // [2][KT keys][128 B]  (roped K)
-    char* Vs = smem + 2 * BUF;  // [2][KT keys][128 B]
+    char* Ks = smem;            // [2][KT keys][RB]  (roped K)
+    char* Vs = smem + 2 * BUF;  // [2][KT keys][RB]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
     FA_STAMP(0, 0, 0);
@@ -106,7 +123,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     auto load_tile = [&](int it) {
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
-            const int e = tid + NT * i, r = e >> 3, c = e & 7;
+            const int e = tid + NT * i, r = (unsigned)e / (RB / 16), c = (unsigned)e % (RB / 16);
             const long kk = min(it * 64 + r, S - 1);  // rows past the end: valid memory, zeroed at the write
             kreg[i] = *reinterpret_cast<const u16x8*>(kb + kk * ld_kv + c * 8);
             vreg[i] = *reinterpret_cast<const u16x8*>(vb + kk * ld_kv + c * 8);
@@ -115,7 +132,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     auto write_tile = [&](int it, int buf) {
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
-            const int e = tid + NT * i, r = e >> 3, c = e & 7;
+            const int e = tid + NT * i, r = (unsigned)e / (RB / 16), c = (unsigned)e % (RB / 16);
             const bool ok = it * 64 + r < S;
             u16x8 kv = ok ? kreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
             const u16x8 vv = ok ? vreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -132,7 +149,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     // past the end read as 0 and are masked below)
     const int wu = __builtin_amdgcn_readfirstlane(w);
     const int hbytes = head_bytes(ld_kv, S, D);
-    const DmaVoff<NW> kvo = dma_voff<NW>(ld_kv, wu, l);
+    const DmaVoff<NW, RB> kvo = dma_voff<NW, RB>(ld_kv, wu, l);
     if constexpr (DM) {
 #pragma unroll
         for (int sb = 0; sb < NSUB; ++sb) {
@@ -176,9 +193,9 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         nd[r] = -dsum;
     }
 
-    f32x16 acc[2];
+    f32x16 acc[ND];
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
 
@@ -215,33 +232,55 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
                     char* Kh = Kc + (kq >> 1) * TILE;
                     const char* Vh = Vc + (kq >> 1) * TILE;
                     const int kh = kq & 1;
-                    f32x16 sp = ns, dp = nd;
+                    f32x16 sp, dp;
+                    if constexpr (D == 64) {
+                        sp = ns;
+                        dp = nd;
+                    } else {  // D = 128: no 32 registers held for the row constants
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            sp[r] = nl;
+                            dp[r] = -dsum;
+                        }
+                    }
                     // every operand read of the step is issued ahead of its MFMAs: the K / V rows before the S / dP
                     // chains, the transposed K fragments of the dQ products before the softmax VALU, so their LDS
-                    // latency is paid once per batch (hipcc's own schedule waits lgkmcnt(0) before every MFMA pair)
-                    bf16x8 tk[2][2];  // the transposed K fragments of the dQ products (s, dt)
-                    bf16x8 fk[KS], fv[KS];
+                    // latency is paid once per batch (hipcc's own schedule waits lgkmcnt(0) before every MFMA pair).
+                    // D = 128: the K / V rows per k-step (a batch would hold 64 more registers)
+                    bf16x8 tk[2][ND];  // the transposed K fragments of the dQ products (s, dt)
+                    if constexpr (D == 64) {
+                        bf16x8 fk[KS], fv[KS];
 #pragma unroll
-                    for (int ks = 0; ks < KS; ++ks) {
-                        const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
-                        fk[ks] = lds_row16(Kh, koff);
-                        fv[ks] = lds_row16(Vh, koff);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int ks = 0; ks < KS; ++ks) {
-                        sp = mfma(fk[ks], qf[ks], sp);
-                        dp = mfma(fv[ks], of[ks], dp);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int s = 0; s < 2; ++s)
-#pragma unroll
-                        for (int dt = 0; dt < 2; ++dt) {
-                            const int kr = 32 * kh + 16 * s;
-                            tk[s][dt] = lds_tr_pair(Kh, tr_off<RB>(kr + trow, 32 * dt + tcol),
-                                                    tr_off<RB>(kr + 8 + trow, 32 * dt + tcol));
+                        for (int ks = 0; ks < KS; ++ks) {
+                            const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
+                            fk[ks] = lds_row16(Kh, koff);
+                            fv[ks] = lds_row16(Vh, koff);
                         }
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int ks = 0; ks < KS; ++ks) {
+                            sp = mfma(fk[ks], qf[ks], sp);
+                            dp = mfma(fv[ks], of[ks], dp);
+                        }
+                    } else {
+#pragma unroll
+                        for (int ks = 0; ks < KS; ++ks) {
+                            const int koff = swz<RB>(32 * kh + l31, 2 * ks + hh);
+                            sp = mfma(lds_row16(Kh, koff), qf[ks], sp);
+                            dp = mfma(lds_row16(Vh, koff), of[ks], dp);
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (D == 64) {  // (D = 128 reads them per k-step of the dQ products)
+#pragma unroll
+                        for (int s = 0; s < 2; ++s)
+#pragma unroll
+                            for (int dt = 0; dt < ND; ++dt) {
+                                const int kr = 32 * kh + 16 * s;
+                                tk[s][dt] = lds_tr_pair(Kh, tr_off<RB>(kr + trow, 32 * dt + tcol),
+                                                        tr_off<RB>(kr + 8 + trow, 32 * dt + tcol));
+                            }
+                    }
                     __builtin_amdgcn_sched_barrier(0);
                     // P^T = exp2(S^T c - lse), dS^T = P^T (dP^T - delta); key = row of the accumulator, query = lane
                     if (need_mask) {
@@ -265,8 +304,14 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 #pragma unroll
                         for (int j = 0; j < 8; ++j) db[j] = (__bf16)dp[8 * s + j];
                         const int kr = 32 * kh + 16 * s;
+                        if constexpr (D == 128) {
 #pragma unroll
-                        for (int dt = 0; dt < 2; ++dt) acc[dt] = mfma(tk[s][dt], db, acc[dt]);
+                            for (int dt = 0; dt < ND; ++dt)
+                                tk[s][dt] = lds_tr_pair(Kh, tr_off<RB>(kr + trow, 32 * dt + tcol),
+                                                        tr_off<RB>(kr + 8 + trow, 32 * dt + tcol));
+                        }
+#pragma unroll
+                        for (int dt = 0; dt < ND; ++dt) acc[dt] = mfma(tk[s][dt], db, acc[dt]);
                     }
                 }
             }
@@ -285,7 +330,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     if (q_ok) {
         __bf16* dqp = dQ + ((long)b * S + q) * ld_dq + (long)h * D;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
+        for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int d0 = 32 * dt + 8 * i + 4 * hh;
@@ -306,21 +351,24 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     }
 }
 
-template <bool CAUSAL, bool ROPE, bool ROPE_IN>
-__global__ void __launch_bounds__(NW * 64, 2)
+template <int D, bool CAUSAL, bool ROPE, bool ROPE_IN>
+__global__ void __launch_bounds__(NW * 64, D == 64 ? 2 : 1)
 fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                   long ld_q, long ld_kv, const __bf16* __restrict__ dO, long ld_do, const float* __restrict__ LSE,
                   const float* __restrict__ DELTA, __bf16* __restrict__ dK, __bf16* __restrict__ dV, long ld_dkv,
                   const float* __restrict__ cosT, const float* __restrict__ sinT, int B,
                   int H, int Hkv, int S, float scale_log2, float scale, int group) {
+    using Gm = Geo<D>;
+    constexpr int RB = Gm::RB, TILE = Gm::TILE, KS = Gm::KS, ND = Gm::ND, CPT = Gm::CPT;
+    static_assert(D == 64 || !ROPE_IN, "D = 128: Q / K are rotated before the kernels");
     constexpr int NT = NW * 64, KB = 32 * NW;
     // queries per Q / dO tile (one barrier each): 128 with LDS-DMA staging (two 64-row images side by side), 64
-    // with register staging (ROPE_IN: Q is rotated on its way to LDS)
+    // with register staging (ROPE_IN: Q is rotated on its way to LDS) and at D = 128
     constexpr bool DM = !ROPE_IN;
-    constexpr int QT = DM ? 128 : 64, NSUB = QT / 64, BUF = NSUB * TILE;
+    constexpr int QT = (DM && D == 64) ? 128 : 64, NSUB = QT / 64, BUF = NSUB * TILE;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* Qs = smem;                                            // [2][QT q][128 B]  (roped Q)
-    char* dOs = smem + 2 * BUF;                                 // [2][QT q][128 B]
+    char* Qs = smem;                                            // [2][QT q][RB]  (roped Q)
+    char* dOs = smem + 2 * BUF;                                 // [2][QT q][RB]
     float* lseS = reinterpret_cast<float*>(smem + 4 * BUF);     // [2][QT]  -lse / c
     float* dltS = lseS + 2 * QT;                                // [2][QT]  -delta
 
@@ -370,7 +418,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     // DM: Q / dO tiles by LDS-DMA through per-head buffer resources (no staging registers, no per-tile address
     // VALU); only the row constants go through registers
     const int wu = __builtin_amdgcn_readfirstlane(w);
-    const DmaVoff<NW> qvo = dma_voff<NW>(ld_q, wu, l), ovo = dma_voff<NW>(ld_do, wu, l);
+    const DmaVoff<NW, RB> qvo = dma_voff<NW, RB>(ld_q, wu, l), ovo = dma_voff<NW, RB>(ld_do, wu, l);
     auto load_tile = [&](int it) {
         const int m0 = m0_of(it);
         const __bf16* qb = q_of(it);
@@ -383,7 +431,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
         if constexpr (!DM) {  // DM: the tile itself is DMA'd by the loop body (after these loads)
 #pragma unroll
             for (int i = 0; i < CPT; ++i) {
-                const int e = tid + NT * i, r = e >> 3, c = e & 7;
+                const int e = tid + NT * i, r = (unsigned)e / (RB / 16), c = (unsigned)e % (RB / 16);
                 const long qq = min(m0 + r, S - 1);
                 qreg[i] = *reinterpret_cast<const u16x8*>(qb + qq * ld_q + c * 8);
                 oreg[i] = *reinterpret_cast<const u16x8*>(ob + qq * ld_do + c * 8);
@@ -394,7 +442,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
         const int m0 = m0_of(it);
 #pragma unroll
         for (int i = 0; i < (DM ? 0 : CPT); ++i) {
-            const int e = tid + NT * i, r = e >> 3, c = e & 7;
+            const int e = tid + NT * i, r = (unsigned)e / (RB / 16), c = (unsigned)e % (RB / 16);
             const bool ok = m0 + r < S;
             u16x8 qv = ok ? qreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
             const u16x8 ov = ok ? oreg[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -444,9 +492,9 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
         vf[ks] = __builtin_bit_cast(bf16x8, tv);
     }
 
-    f32x16 dk[2], dv[2];
+    f32x16 dk[ND], dv[ND];
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
 
@@ -533,7 +581,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
                         }
                         const int qr = qt * 32 + 16 * ss;
 #pragma unroll
-                        for (int dt = 0; dt < 2; ++dt) {
+                        for (int dt = 0; dt < ND; ++dt) {
                             const int o0 = tr_off<RB>(qr + trow, dt * 32 + tcol);
                             const int o1 = tr_off<RB>(qr + 8 + trow, dt * 32 + tcol);
                             dv[dt] = mfma(lds_tr_pair(Oh, o0, o1), pb, dv[dt]);
@@ -556,7 +604,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     __bf16* dkp = dK + ((long)b * S + key) * ld_dkv + (long)hk * D;
     __bf16* dvp = dV + ((long)b * S + key) * ld_dkv + (long)hk * D;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int d0 = dt * 32 + 8 * i + 4 * hh;
@@ -585,7 +633,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
 using namespace bpe;
 using namespace bpe::fa;
 
-// Backward form for D = 64: 0 = split (default), 1 = fused (flash_attn_bwd.hip, the atomics form that D = 128 uses);
+// Backward form: 0 = split (default), 1 = fused (flash_attn_bwd.hip, the atomics form);
 // switched at run time by fa_bwd_config (tests compare the two).  The split kernels run at 4 waves, 2 workgroups per
 // CU, with LDS-DMA staging and 128-row tiles (the dQ kernel with batched operand reads).  Measured and removed (same
 // box, op-level, GPT-2 B 128; docs/performance.md, attention): register staging (1.207-1.277 vs 1.178-1.204 ms),
@@ -594,7 +642,8 @@ using namespace bpe::fa;
 // 1.168 ms), the per-query-head dK / dV partials + reduce for GQA (Llama B 32 2.64 vs 2.31 ms).
 static int g_mode = 0;
 
-bool fa_bwd_split_active(int D) { return D == 64 && g_mode == 0; }
+// D = 128 takes the split form for pre-rotated Q / K (rope 2) or no RoPE; fa_bwd rotates a copy for rope 1
+bool fa_bwd_split_active(int D, int rope) { return (D == 64 || (D == 128 && rope != 1)) && g_mode == 0; }
 
 // mode < 0 leaves the form unchanged; returns the form in force BEFORE the call
 int fa_bwd_config(int mode) {
@@ -603,23 +652,24 @@ int fa_bwd_config(int mode) {
     return prev;
 }
 
-template <bool C, bool R, bool RIN>
+template <int D, bool C, bool R, bool RIN>
 static void split_launch(const FaArgs& a, hipStream_t s) {
-    constexpr int NSUB = RIN ? 1 : 2;  // 64-row images per LDS buffer (128-row tiles with LDS-DMA)
+    constexpr int NSUB = (RIN || D == 128) ? 1 : 2;  // 64-row images per LDS buffer (128-row tiles with LDS-DMA)
+    constexpr int TILE = split::Geo<D>::TILE;
     const int nblk = (a.S + 32 * split::NW - 1) / (32 * split::NW);
-    split::fa_bwd_dq_kernel<C, R, RIN><<<nblk * a.B * a.H, split::NW * 64, 4 * split::TILE * NSUB, s>>>(
+    split::fa_bwd_dq_kernel<D, C, R, RIN><<<nblk * a.B * a.H, split::NW * 64, 4 * TILE * NSUB, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do, a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin,
         a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
     // Q / dO buffers + the -lse / -delta rows
-    const int lds = 4 * split::TILE * NSUB + 16 * 64 * NSUB;
-    split::fa_bwd_dkv_kernel<C, R, RIN><<<nblk * a.B * a.Hkv, split::NW * 64, lds, s>>>(
+    const int lds = 4 * TILE * NSUB + 16 * 64 * NSUB;
+    split::fa_bwd_dkv_kernel<D, C, R, RIN><<<nblk * a.B * a.Hkv, split::NW * 64, lds, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.cos,
         a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.Hkv));
 }
 
 // whether a GQA backward of head size D needs the fp32 dK / dV partials buffer (FaArgs::dkv_part): only the fused
 // backward does (the split dK/dV kernel sweeps the query heads of its KV head)
-bool fa_dkv_partials_needed(int D) { return !fa_bwd_split_active(D); }
+bool fa_dkv_partials_needed(int D, int rope) { return !fa_bwd_split_active(D, rope); }
 
 // copy the last launch's stamps out (BPE_FA_STAMPS builds; false otherwise)
 bool fa_read_stamps(long long* host, int n) {
@@ -635,16 +685,26 @@ bool fa_read_stamps(long long* host, int n) {
 }
 
 bool launch_fa_bwd_split(const FaArgs& a, hipStream_t s) {
-    if (!fa_bwd_split_active(a.D)) return false;
+    if (!fa_bwd_split_active(a.D, a.rope)) return false;
     // rope: 0 none, 1 rotate Q / K on load and dQ / dK on output, 2 outputs only (Q / K pre-rotated)
+    if (a.D == 128) {
+        if (a.causal) {
+            if (a.rope == 2) split_launch<128, true, true, false>(a, s);
+            else split_launch<128, true, false, false>(a, s);
+        } else {
+            if (a.rope == 2) split_launch<128, false, true, false>(a, s);
+            else split_launch<128, false, false, false>(a, s);
+        }
+        return true;
+    }
     if (a.causal) {
-        if (a.rope == 1) split_launch<true, true, true>(a, s);
-        else if (a.rope == 2) split_launch<true, true, false>(a, s);
-        else split_launch<true, false, false>(a, s);
+        if (a.rope == 1) split_launch<64, true, true, true>(a, s);
+        else if (a.rope == 2) split_launch<64, true, true, false>(a, s);
+        else split_launch<64, true, false, false>(a, s);
     } else {
-        if (a.rope == 1) split_launch<false, true, true>(a, s);
-        else if (a.rope == 2) split_launch<false, true, false>(a, s);
-        else split_launch<false, false, false>(a, s);
+        if (a.rope == 1) split_launch<64, false, true, true>(a, s);
+        else if (a.rope == 2) split_launch<64, false, true, false>(a, s);
+        else split_launch<64, false, false, false>(a, s);
     }
     return true;
 }

@@ -162,9 +162,10 @@ bool launch_fa_fwd_v4(const FaArgs& a, hipStream_t s);
 int fa_fwd_config(int ver);  // the D = 64 forward: 8 (default) or 2 (fa_fwd_kernel); ver <= 0 leaves it unchanged;
                              // returns the version in force before the call
 void launch_fa_bwd(const FaArgs& a, hipStream_t s);
-// true when launch_fa_bwd takes the split form for head dim D (no fp32 dQ accumulator, no pre / convert passes)
-bool fa_bwd_split_active(int D);
-// D = 64 backward form 0 split / 1 fused; negative = unchanged; returns the form in force before the call
+// true when launch_fa_bwd takes the split form for head dim D and FaArgs::rope mode (no fp32 dQ accumulator, no pre
+// / convert passes): D = 64 always, D = 128 unless rope == 1 (the in-kernel rotation; fa_bwd pre-rotates a copy)
+bool fa_bwd_split_active(int D, int rope = 0);
+// backward form 0 split / 1 fused; negative = unchanged; returns the form in force before the call
 int fa_bwd_config(int mode);
 // per-workgroup s_memtime stamps of the last split-backward launch (BPE_FA_STAMPS builds only; false otherwise)
 bool fa_read_stamps(long long* host, int n);
@@ -181,4 +182,4 @@ void launch_gemm_fp8_splitk(const void* A, long lda, const void* B, long ldb, vo
 void launch_gemm_pp_rope(const void* X, long ldx, const void* W, long ldw, void* C, long ldc, int M, int N, int R,
                          const float* cosT, const float* sinT, int S, int D, int rot_cols, hipStream_t s);
 // whether FaArgs::dkv_part (GQA fp32 dK / dV partials of the fused backward) must be set
-bool fa_dkv_partials_needed(int D);
+bool fa_dkv_partials_needed(int D, int rope = 0);

@@ -664,7 +664,7 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
 }
 
 // whether fa_bwd uses (and fa_fwd should zero) the fp32 dQ accumulator for head dim D
-bool fa_bwd_needs_dq_acc(int64_t D) { return !fa_bwd_split_active((int)D); }
+bool fa_bwd_needs_dq_acc(int64_t D) { return !fa_bwd_split_active((int)D, 2); }
 int64_t fa_fwd_config_op(int64_t ver) { return fa_fwd_config((int)ver); }
 int64_t fa_bwd_config_op(int64_t mode) { return fa_bwd_config((int)mode); }
 int64_t gpp_persist_config_op(int64_t mode) { return gpp_persist_config((int)mode); }
@@ -702,23 +702,40 @@ at::Tensor fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor&
     const int64_t W = (H + 2 * Hkv) * D;
     auto dqkv = at::empty({B * S, W}, q.options());
     auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+    int rope = use_rope ? (prerotated ? 2 : 1) : 0;
+    // D = 128 with the forward's in-kernel rotation: the split kernels take pre-rotated Q / K, so rotate a copy of
+    // [Q | K | V] (the kernels then un-rotate dQ / dK on output, as for the pre-rotated forward)
+    at::Tensor qkv_rot;
+    const __bf16 *qp = (const __bf16*)q.data_ptr(), *kp = (const __bf16*)k.data_ptr(), *vp = (const __bf16*)v.data_ptr();
+    int64_t ld_q = q.stride(0), ld_kv = k.stride(0);
+    if (D == 128 && rope == 1 && fa_bwd_split_active((int)D, 2)) {
+        TORCH_CHECK(k.stride(0) == v.stride(0), "flash attention: k and v must share a row stride");
+        qkv_rot = at::cat({q, k, v}, 1);
+        launch_rope_qk(qkv_rot.data_ptr(), W, cos.data_ptr<float>(), sin.data_ptr<float>(), B * S, (int)S, (int)H,
+                       (int)Hkv, (int)D, cur_stream());
+        qp = (const __bf16*)qkv_rot.data_ptr();
+        kp = qp + H * D;
+        vp = qp + (H + Hkv) * D;
+        ld_q = ld_kv = W;
+        rope = 2;
+    }
     // rows padded to 64 per batch; zeroed by the forward when it was handed this buffer (fa_fwd dq_acc)
-    const bool split = fa_bwd_split_active((int)D);  // the split form needs no fp32 dQ accumulator
+    const bool split = fa_bwd_split_active((int)D, rope);  // the split form needs no fp32 dQ accumulator
     const bool pre_zeroed = !split && dq_acc_in.has_value() && dq_acc_in->defined();
     if (pre_zeroed) check_dq_acc(*dq_acc_in, q, B, S, H, D);
     at::Tensor dq_acc;
     if (!split)
         dq_acc = pre_zeroed ? *dq_acc_in : at::empty({B * ((S + 63) / 64 * 64), H * D}, q.options().dtype(at::kFloat));
     at::Tensor dkv_part;
-    const bool need_part = Hkv < H && fa_dkv_partials_needed((int)D);  // GQA per-query-head partials (+ reduce)
+    const bool need_part = Hkv < H && fa_dkv_partials_needed((int)D, rope);  // GQA per-query-head partials (+ reduce)
     if (need_part) dkv_part = at::empty({B * S, H * 2 * D}, q.options().dtype(at::kFloat));
     FaArgs a{};
-    a.q = (const __bf16*)q.data_ptr(); a.k = (const __bf16*)k.data_ptr(); a.v = (const __bf16*)v.data_ptr();
-    a.ld_q = q.stride(0); a.ld_kv = k.stride(0);
+    a.q = qp; a.k = kp; a.v = vp;
+    a.ld_q = ld_q; a.ld_kv = ld_kv;
     a.o = (__bf16*)o.data_ptr(); a.ld_o = o.stride(0); a.lse = lse.data_ptr<float>();
     a.cos = use_rope ? cos.data_ptr<float>() : nullptr; a.sin = use_rope ? sin.data_ptr<float>() : nullptr;
     a.B = (int)B; a.H = (int)H; a.Hkv = (int)Hkv; a.S = (int)S; a.D = (int)D;
-    a.causal = causal; a.rope = use_rope ? (prerotated ? 2 : 1) : 0; a.scale = (float)scale;
+    a.causal = causal; a.rope = rope; a.scale = (float)scale;
     a.dout = (const __bf16*)d.data_ptr(); a.ld_do = d.stride(0);
     a.delta = delta.data_ptr<float>(); a.dq_acc = split ? nullptr : dq_acc.data_ptr<float>();
     a.dq_zeroed = pre_zeroed ? 1 : 0;

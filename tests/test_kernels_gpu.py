@@ -461,15 +461,15 @@ def test_gemm_swiglu_fwd(gpu_device, gpp_mode, M, d, F):
     assert rel(a.cpu(), (g * torch.sigmoid(g) * u).cpu()) < 2e-2
 
 
-@pytest.mark.parametrize("H,Hkv", [(8, 2), (4, 4)])
-def test_gemm_qkv_rope(gpu_device, gpp_mode, H, Hkv):
+@pytest.mark.parametrize("H,Hkv,D", [(8, 2, 64), (4, 4, 64), (4, 2, 128)])
+def test_gemm_qkv_rope(gpu_device, gpp_mode, H, Hkv, D):
     """QKV projection with RoPE in the GEMM epilogue vs the unfused pair (matmul, then rope_qk_ in place).  Small
     integer operands make every product exact, so the two must agree bitwise (the RoPE arithmetic is the same
     fp32 formula on the same bf16 values); the partly rotated tile (Q / K end inside a 256-column tile) and the
     untouched V columns are both covered."""
     from bpe_transformer.ops import reference as R
     h = torch.ops.bpe_hip
-    B, S, D, d = 2, 256, 64, 256
+    B, S, d = 2, 256, 256
     N = (H + 2 * Hkv) * D
     g = torch.Generator(device="cpu").manual_seed(H * 10 + Hkv)
     x = torch.randint(-2, 3, (B * S, d), generator=g).to(torch.bfloat16).to(gpu_device)
@@ -663,8 +663,22 @@ def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal
     """The split backward (dQ kernel + dK/dV kernel: LDS-DMA 128-row tiles, or register-staged 64-row tiles with
     RoPE fused, rope == "fused") against the fp32 oracle's autograd and against the fused atomics backward on the
     same forward outputs: dQ, dK, dV each; and bitwise deterministic."""
+    _split_vs_fused(gpu_device, S, H, Hkv, 64, rope, causal)
+
+
+@pytest.mark.parametrize("S", [1024, 200, 64])
+@pytest.mark.parametrize("H,Hkv", [(4, 4), (8, 2)])
+@pytest.mark.parametrize("rope", ["fused", "prerotated", None])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_bwd_split_d128(gpu_device, S, H, Hkv, rope, causal):
+    """The split backward at D = 128 (256-byte rows, 64-row LDS-DMA tiles; rope "fused": fa_bwd rotates a copy of Q /
+    K and runs the pre-rotated kernels) against the oracle and the fused atomics form, and bitwise deterministic."""
+    _split_vs_fused(gpu_device, S, H, Hkv, 128, rope, causal)
+
+
+def _split_vs_fused(gpu_device, S, H, Hkv, D, rope, causal):
     h = torch.ops.bpe_hip
-    B, D = 2, 64
+    B = 2
     torch.manual_seed(11)
     qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device=gpu_device, dtype=torch.bfloat16)
     use_rope = rope is not None
@@ -677,7 +691,8 @@ def test_flash_bwd_split_vs_fused_and_oracle(gpu_device, S, H, Hkv, rope, causal
     scale = D ** -0.5
     o, lse = h.fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)
     do = torch.randn_like(o)
-    assert h.fa_bwd_config(-1) == 0, "the default D = 64 backward is the split form"
+    assert h.fa_bwd_config(-1) == 0, "the default backward is the split form"
+    assert not h.fa_bwd_needs_dq_acc(D), "the split form takes no fp32 dQ accumulator"
     try:
         got = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)
         again = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, use_rope, scale, pre)

@@ -30,8 +30,10 @@ def test_forward_matches_oracle(gpu_device):
     assert err < 5e-2, err
 
 
-def test_loss_and_grads_match_oracle(gpu_device):
-    ref, gpu = _pair(gpu_device)
+@pytest.mark.parametrize("heads", [4, 2])
+def test_loss_and_grads_match_oracle(gpu_device, heads):
+    """Head size 64 (4 heads) and 128 (2 heads: the D = 128 split backward, RoPE in the QKV GEMM epilogue)."""
+    ref, gpu = _pair(gpu_device, num_heads=heads)
     ids = torch.randint(0, 1000, (2, 128))
     tgt = torch.randint(0, 1000, (2, 128))
     l_ref = ref.loss(ids, tgt)
@@ -150,14 +152,16 @@ def test_fp8_engine_reduces_loss(gpu_device):
     assert model.fp8_state.pos == 31
 
 
-def test_forward_and_backward_are_bitwise_deterministic(gpu_device):
-    """Every kernel of the step is run-to-run deterministic at D = 64: the forward (attention, norms, CE, GEMM
-    routing) and -- since the split attention backward has no dQ atomics (csrc/flash_attn_bwd_split.hip) and the
-    split-K weight gradients reduce their fp32 slabs in a fixed order -- every gradient as well."""
+@pytest.mark.parametrize("heads", [4, 2])
+def test_forward_and_backward_are_bitwise_deterministic(gpu_device, heads):
+    """Every kernel of the step is run-to-run deterministic at D = 64 and D = 128: the forward (attention, norms, CE,
+    GEMM routing) and -- since the split attention backward has no dQ atomics (csrc/flash_attn_bwd_split.hip) and
+    the split-K weight gradients reduce their fp32 slabs in a fixed order -- every gradient as well."""
     import torch.ops
 
-    assert torch.ops.bpe_hip.fa_bwd_config(-1) == 0, "the default D = 64 backward is the split form"
-    _, gpu = _pair(gpu_device)
+    assert torch.ops.bpe_hip.fa_bwd_config(-1) == 0, "the default backward is the split form"
+    assert not torch.ops.bpe_hip.fa_bwd_needs_dq_acc(256 // heads)
+    _, gpu = _pair(gpu_device, num_heads=heads)
     ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
     tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
     with torch.no_grad():
