@@ -5,14 +5,16 @@ One ``autograd.Function`` per transformer block instead of ~10 autograd nodes:
 forward (x = xr + xd: the previous block's residual and its not-yet-added FFN output)::
 
     x, h1 = add_rmsnorm(xr, xd; ln1)  HIP (the residual add fused into the norm)
-    qkv = h1 @ [Wq;Wk;Wv]^T, RoPE     our persistent ping-pong GEMM with RoPE on Q / K in its epilogue (D = 64;
-                                      D = 128 rotates inside attention; fp8: ops/fp8.py + the in-place rope_qk_)
+    qkv = h1 @ [Wq;Wk;Wv]^T, RoPE     our persistent ping-pong GEMM with RoPE on Q / K in its epilogue (D = 64
+                                      and 128; fp8: ops/fp8.py + the in-place rope_qk_)
     o = flash_attn(qkv)               HIP (csrc/flash_attn_fwd_v4.hip)
     g1 = o @ Wo^T                     hipBLASLt
     xm, h2 = add_rmsnorm(x, g1; ln2)  HIP
     gu, a = h2 @ [W1;W3]^T, silu(g)*u our ping-pong GEMM with the gate in its epilogue (csrc/gemm_pp.hip,
                                       d_model <= 1024; else hipBLASLt + the HIP gate kernel)
     g2 = a @ W2^T                     hipBLASLt; the block returns (xm, g2), added by the next norm
+    (fp8 with fp8 weight gradients: the gate writes a only as fp8 in both layouts, and its backward writes the
+    gate gradient only as e5m2 in both layouts: ops/fp8.py swiglu_fwd_cast_t / swiglu_bwd_cast_t)
 
 backward: the mirror image, with
   * the SwiGLU backward fused into the epilogue of the dY @ W2 GEMM (our
@@ -46,6 +48,7 @@ from torch import Tensor
 
 from ..ops._ext import ops as hip
 from ..ops.attention import prerotate_default
+from ..ops.fp8 import swiglu_bwd_cast_t, swiglu_cast_ok, swiglu_fwd_cast_t
 from ..ops.gemm import accumulate_weight_grad
 
 
@@ -90,6 +93,9 @@ def _fuse_swiglu_fwd(x: Tensor, w13: Tensor) -> bool:
 
 
 _FUSE_QKV_ROPE = True  # module flag (tests and A/B runs compare the unfused path)
+# fp8 weight-gradient path: SwiGLU forward / backward write their outputs only as fp8 in both layouts (one pass with
+# the cast, csrc/fp8.hip swiglu_cast_fp8_t) instead of bf16 plus a cast pass (module flag for tests and A/B runs)
+_FP8_SWIGLU_CAST = True
 
 
 def _fuse_qkv_rope(x: Tensor, w: Tensor, S: int) -> bool:
@@ -144,10 +150,10 @@ class FusedBlockFn(torch.autograd.Function):
             w8s = []
             xt8s = [] if wg else None
 
-            def mm(x, w, i):
+            def mm(x, w, i, xq=None):
                 if not keep:
                     return st.matmul(x, w, s0 + i, s0 + 4 + i)
-                y, w8t, xt8 = st.matmul(x, w, s0 + i, s0 + 4 + i, keep_w8=True, keep_xt=wg)
+                y, w8t, xt8 = st.matmul(x, w, s0 + i, s0 + 4 + i, keep_w8=True, keep_xt=wg, xq=xq)
                 w8s.append(w8t)
                 if wg:
                     xt8s.append(xt8)
@@ -177,8 +183,13 @@ class FusedBlockFn(torch.autograd.Function):
             gu, a = hip().gemm_swiglu_fwd(h2, w_13)  # the gate in the GEMM epilogue: no second pass over gu
         else:
             gu = mm(h2, w_13, 2) if fp8 is not None else torch.matmul(h2, w_13.t())
-            a = hip().swiglu_fwd(gu)
-        g2 = mm(a, w2.detach(), 3) if fp8 is not None else torch.matmul(a, w2.t())
+            a = None if xt8s is not None and _FP8_SWIGLU_CAST and swiglu_cast_ok(gu) else hip().swiglu_fwd(gu)
+        if a is None:
+            # fp8 weight gradients: a = silu(g) u is written only as the W2 GEMM's fp8 operand, in both layouts,
+            # by one pass over gu (no bf16 a, no separate cast)
+            g2 = mm(None, w2.detach(), 3, xq=swiglu_fwd_cast_t(fp8[0], gu, fp8[1] + 3))
+        else:
+            g2 = mm(a, w2.detach(), 3) if fp8 is not None else torch.matmul(a, w2.t())
         ctx.w8s = w8s if w8s else None
         ctx.xt8s = xt8s
         ctx.has_xd = xd is not None
@@ -262,16 +273,17 @@ class FusedBlockFn(torch.autograd.Function):
                 return torch.matmul(g_out, hip().transpose_bf16(w).t())
             return torch.matmul(g_out, w)
 
-        def proj(g_out: Tensor, ws: list[Tensor], i: int, x_in: Tensor | None) -> Tensor:
+        def proj(g_out: Tensor | None, ws: list[Tensor], i: int, x_in: Tensor | None, gq=None) -> Tensor:
             """Both gradients of projection i: returns dX = g_out @ W, accumulates dW = g_out^T x_in.  With fp8
-            weight gradients both come from one e5m2 cast of g_out (ops/fp8.py ``grads``)."""
+            weight gradients both come from one e5m2 cast of g_out (ops/fp8.py ``grads``), or from ``gq`` = g_out
+            already quantised in both layouts by its producer."""
             if xt8s is not None:
                 from ..ops.fp8 import grads as fp8_grads
 
                 # accumulated straight into the flat gradient buffer when the stacked weights are adjacent there
                 view = _adjacent_view([p.main_grad for p in ws]) if main else None
                 dxv, dw = fp8_grads(fp8[2], g_out, fp8[3] + i, w8s[i], fp8[0], fp8[1] + 4 + i, xt8s[i], fp8[0],
-                                    fp8[1] + i, dw_out=view)
+                                    fp8[1] + i, dw_out=view, gq=gq)
                 if view is None:
                     acc_dw(ws, dw)
                 else:
@@ -282,14 +294,20 @@ class FusedBlockFn(torch.autograd.Function):
             return dx(g_out, ws, i)
 
         # ---- FFN
+        dgu_q = None
         if w8s is None and _fuse_swiglu_bwd(dy, w2, gu):
             acc_weight([w2], dy, a)
             # da = dy @ W2 with the SwiGLU backward in the GEMM epilogue (csrc/gemm_pp.hip): da never reaches HBM
             dgu = hip().gemm_swiglu_bwd(dy, w2.detach(), gu)
         else:
             da = proj(dy, [w2], 3, a)
-            dgu = hip().swiglu_bwd(da, gu)
-        dh2 = proj(dgu, [w1, w3], 2, h2)
+            if xt8s is not None and _FP8_SWIGLU_CAST and swiglu_cast_ok(gu):
+                # the gate gradient straight to e5m2 in both layouts (the W13 projection's operands): no bf16 dgu
+                dgu = None
+                dgu_q = swiglu_bwd_cast_t(fp8[2], da, gu, fp8[3] + 2)
+            else:
+                dgu = hip().swiglu_bwd(da, gu)
+        dh2 = proj(dgu, [w1, w3], 2, h2, gq=dgu_q)
         dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dxm_out)
         # ---- attention
         do = proj(dxm, [wo], 1, o)

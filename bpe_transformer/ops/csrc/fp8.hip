@@ -131,6 +131,90 @@ __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const __bf16* __restric
     if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
 
+// SwiGLU with the two-layout fp8 cast fused in (the fp8 weight-gradient path, where no bf16 copy of these tensors
+// is kept): MODE 0 forms a = silu(g) u from gu = [g | u] ([M][2F]) and writes a8 [M][F] and a8t [F][M] (FMT e4m3, the
+// W2 projection's input); MODE 1 forms the gate gradient [dg | du] from dout = dA [M][F] and gu and writes dgu8
+// [M][2F] and dgu8t [2F][M] (FMT e5m2, the W13 projection's output gradient).  Each value is rounded to bf16 exactly
+// as swiglu_fwd / swiglu_bwd (activations.hip) store it before it is scaled and converted, so the outputs and the
+// amax equal those of the two-pass form (SwiGLU kernel, then cast_fp8_t) while the bf16 tensor's write and re-read
+// disappear.  64 x 64 tiles of (tokens, F columns) through LDS as in cast_fp8_t_kernel.
+template <int MODE, int FMT>
+__global__ void __launch_bounds__(256) swiglu_cast_fp8_t_kernel(const __bf16* __restrict__ gu,
+                                                                const __bf16* __restrict__ dout, int M, int F,
+                                                                const float* __restrict__ scale,
+                                                                uint8_t* __restrict__ o8, uint8_t* __restrict__ o8t,
+                                                                unsigned* __restrict__ amax_bits) {
+    constexpr int NO = MODE == 0 ? 1 : 2;  // output column blocks per tile: a, or dg and du
+    __shared__ uint8_t tile[NO][64][68];
+    __shared__ float red[4];
+    const int tid = threadIdx.x;
+    const int tiles_f = F / 64, ntiles = (M / 64) * tiles_f;
+    const long W = (long)NO * F;  // output row length
+    const float sc = *scale;
+    const int r = tid >> 2, c = (tid & 3) * 16;
+    float am = 0.f;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int m0 = (t / tiles_f) * 64, f0 = (t % tiles_f) * 64;
+        const __bf16* row = gu + (long)(m0 + r) * 2 * F + f0 + c;
+        const u16x8 g0 = *reinterpret_cast<const u16x8*>(row), g1 = *reinterpret_cast<const u16x8*>(row + 8);
+        const u16x8 u0 = *reinterpret_cast<const u16x8*>(row + F), u1 = *reinterpret_cast<const u16x8*>(row + F + 8);
+        u16x8 d0{}, d1{};
+        if constexpr (MODE == 1) {
+            const __bf16* dr = dout + (long)(m0 + r) * F + f0 + c;
+            d0 = *reinterpret_cast<const u16x8*>(dr);
+            d1 = *reinterpret_cast<const u16x8*>(dr + 8);
+        }
+        float v[NO][16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float g = bf2f(j < 8 ? g0[j] : g1[j - 8]), u = bf2f(j < 8 ? u0[j] : u1[j - 8]);
+            const float sg = fast_sigmoid(g);
+            if constexpr (MODE == 0) {
+                v[0][j] = bf2f(f2bf(g * sg * u));
+            } else {
+                const float d = bf2f(j < 8 ? d0[j] : d1[j - 8]);
+                const float silu = g * sg;
+                v[1][j] = bf2f(f2bf(d * silu));                            // du
+                v[0][j] = bf2f(f2bf(d * u * sg * (1.f + g * (1.f - sg))));  // dg
+            }
+        }
+        uint4 q[NO];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[o][j]));
+            q[o].x = pack4_fp8<FMT>(v[o][0] * sc, v[o][1] * sc, v[o][2] * sc, v[o][3] * sc);
+            q[o].y = pack4_fp8<FMT>(v[o][4] * sc, v[o][5] * sc, v[o][6] * sc, v[o][7] * sc);
+            q[o].z = pack4_fp8<FMT>(v[o][8] * sc, v[o][9] * sc, v[o][10] * sc, v[o][11] * sc);
+            q[o].w = pack4_fp8<FMT>(v[o][12] * sc, v[o][13] * sc, v[o][14] * sc, v[o][15] * sc);
+            *reinterpret_cast<uint4*>(o8 + (long)(m0 + r) * W + (long)o * F + f0 + c) = q[o];
+        }
+        __syncthreads();  // the previous tile's transposed reads are done
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            const unsigned qq[4] = {q[o].x, q[o].y, q[o].z, q[o].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) *reinterpret_cast<unsigned*>(&tile[o][r][c + 4 * j]) = qq[j];
+        }
+        __syncthreads();
+        // transposed: thread -> output row (o F + f0 + r), 16 consecutive tokens m0 + c ..
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            unsigned w4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                unsigned x = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x |= (unsigned)tile[o][c + 4 * j + e][r] << (8 * e);
+                w4[j] = x;
+            }
+            *reinterpret_cast<uint4*>(o8t + ((long)o * F + f0 + r) * M + m0 + c) = uint4{w4[0], w4[1], w4[2], w4[3]};
+        }
+    }
+    am = block_max(am, red);
+    if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
+}
+
 // amax_cur [n] (float bits, zeroed here after use), hist [n][H], scale/inv [n]
 __global__ void __launch_bounds__(256) update_scales_kernel(unsigned* __restrict__ amax_cur, float* __restrict__ hist,
                                                             float* __restrict__ scale, float* __restrict__ inv_scale,
@@ -174,6 +258,18 @@ void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8
     else
         cast_fp8_t_kernel<1><<<grid, 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8, (uint8_t*)w8t,
                                                   amax_bits);
+}
+
+void launch_swiglu_cast_fp8_t(int mode, const void* gu, const void* dout, int M, int F, const float* scale, void* o8,
+                              void* o8t, unsigned* amax_bits, hipStream_t s) {
+    const int ntiles = (M / 64) * (F / 64);
+    const int grid = ntiles < 2048 ? ntiles : 2048;
+    if (mode == 0)
+        swiglu_cast_fp8_t_kernel<0, 0><<<grid, 256, 0, s>>>((const __bf16*)gu, nullptr, M, F, scale, (uint8_t*)o8,
+                                                            (uint8_t*)o8t, amax_bits);
+    else
+        swiglu_cast_fp8_t_kernel<1, 1><<<grid, 256, 0, s>>>((const __bf16*)gu, (const __bf16*)dout, M, F, scale,
+                                                            (uint8_t*)o8, (uint8_t*)o8t, amax_bits);
 }
 
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,

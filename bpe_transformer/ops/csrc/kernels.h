@@ -58,7 +58,11 @@ void launch_cast_fp8(int dtype, int fmt, const void* x, size_t n, const float* s
 // dst[C, R] = src[R, C]^T, bf16, R and C multiples of 64 (16-byte aligned rows)
 void launch_transpose_bf16(const void* src, long ld_src, void* dst, long ld_dst, int R, int C, hipStream_t s);
 void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8, void* w8t, unsigned* amax_bits,
-                       int fmt, hipStream_t s);  // bf16 W [N][K] -> e4m3 w8 [N][K] and w8t [K][N]
+                       int fmt, hipStream_t s);
+// SwiGLU + two-layout fp8 cast (fp8.hip): mode 0 a = silu(g) u -> a8 [M][F], a8t [F][M] (e4m3); mode 1 the gate
+// gradient from dout [M][F] -> dgu8 [M][2F], dgu8t [2F][M] (e5m2); gu = [g | u] [M][2F]; M, F multiples of 64
+void launch_swiglu_cast_fp8_t(int mode, const void* gu, const void* dout, int M, int F, const float* scale, void* o8,
+                              void* o8t, unsigned* amax_bits, hipStream_t s);  // bf16 W [N][K] -> e4m3 w8 [N][K] and w8t [K][N]
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,
                           float margin, int fmt, hipStream_t s);
 

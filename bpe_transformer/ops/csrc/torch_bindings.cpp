@@ -567,6 +567,31 @@ void cast_fp8_t(const at::Tensor& w, const at::Tensor& scale, at::Tensor w8, at:
                       reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), e5 ? 1 : 0, cur_stream());
 }
 
+// SwiGLU with the two-layout fp8 cast fused: without dout, a = silu(g) u of gu = [g | u] [M, 2F] -> e4m3 o8 [M, F]
+// and o8t [F, M]; with dout = dA [M, F], the gate gradient [dg | du] -> e5m2 o8 [M, 2F] and o8t [2F, M]
+void swiglu_cast_fp8_t(const at::Tensor& gu, const c10::optional<at::Tensor>& dout, const at::Tensor& scale,
+                       at::Tensor o8, at::Tensor o8t, at::Tensor amax_bits) {
+    check_cuda(gu, "gu");
+    TORCH_CHECK(gu.dim() == 2 && gu.is_contiguous() && gu.scalar_type() == at::kBFloat16, "swiglu_cast_fp8_t: bf16 gu");
+    const int M = (int)gu.size(0), F = (int)(gu.size(1) / 2);
+    TORCH_CHECK(gu.size(1) == 2 * F && M % 64 == 0 && F % 64 == 0, "swiglu_cast_fp8_t: M and F multiples of 64");
+    const bool bwd = dout.has_value() && dout->defined();
+    const int W = bwd ? 2 * F : F;
+    if (bwd)
+        TORCH_CHECK(dout->is_contiguous() && dout->scalar_type() == at::kBFloat16 && dout->size(0) == M &&
+                        dout->size(1) == F && dout->device() == gu.device(), "swiglu_cast_fp8_t: dout bf16 [M, F]");
+    const auto fmt = bwd ? at::kFloat8_e5m2 : at::kFloat8_e4m3fn;
+    TORCH_CHECK(o8.is_contiguous() && o8t.is_contiguous() && o8.scalar_type() == fmt && o8t.scalar_type() == fmt &&
+                    o8.dim() == 2 && o8.size(0) == M && o8.size(1) == W && o8t.dim() == 2 && o8t.size(0) == W &&
+                    o8t.size(1) == M, "swiglu_cast_fp8_t: outputs [M, W] and [W, M] (e4m3 forward, e5m2 backward)");
+    TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1 && amax_bits.scalar_type() == at::kInt &&
+                    amax_bits.numel() == 1, "swiglu_cast_fp8_t: one fp32 scale and one int32 amax slot");
+    DevGuard g(gu.device());
+    launch_swiglu_cast_fp8_t(bwd ? 1 : 0, gu.data_ptr(), bwd ? dout->data_ptr() : nullptr, M, F,
+                             scale.data_ptr<float>(), o8.data_ptr(), o8t.data_ptr(),
+                             reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
+}
+
 void update_scales(at::Tensor amax_bits, at::Tensor hist, at::Tensor scale, at::Tensor inv_scale, int64_t pos,
                    double margin, int64_t fmt) {
     check_cuda(hist, "hist");
@@ -963,6 +988,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
     m.def("transpose_bf16(Tensor w) -> Tensor");
     m.def("cast_fp8_t(Tensor w, Tensor scale, Tensor(a!) w8, Tensor(b!) w8t, Tensor(c!) amax_bits) -> ()");
+    m.def("swiglu_cast_fp8_t(Tensor gu, Tensor? dout, Tensor scale, Tensor(a!) o8, Tensor(b!) o8t, "
+          "Tensor(c!) amax_bits) -> ()");
     m.def("update_scales(Tensor(a!) amax_bits, Tensor(b!) hist, Tensor(c!) scale, Tensor(d!) inv_scale, int pos, "
           "float margin, int fmt=0) -> ()");
     m.def("masked_sdpa(Tensor q, Tensor k, Tensor v, Tensor? mask, float scale) -> Tensor");
@@ -1008,6 +1035,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("cast_fp8", &cast_fp8);
     m.impl("transpose_bf16", &transpose_bf16);
     m.impl("cast_fp8_t", &cast_fp8_t);
+    m.impl("swiglu_cast_fp8_t", &swiglu_cast_fp8_t);
     m.impl("update_scales", &update_scales);
     m.impl("masked_sdpa", &masked_sdpa);
     m.impl("softmax_fwd", &softmax_fwd);

@@ -137,14 +137,18 @@ class Fp8State:
         ops().cast_fp8_t(w, self.scale[slot : slot + 1], w8, w8t, self.amax[slot : slot + 1])
         return w8, w8t
 
-    def matmul(self, x: Tensor, w: Tensor, x_slot: int, w_slot: int, keep_w8: bool = False,
-               keep_xt: bool = False):
+    def matmul(self, x: Tensor | None, w: Tensor, x_slot: int, w_slot: int, keep_w8: bool = False,
+               keep_xt: bool = False, xq: tuple[Tensor, Tensor] | None = None):
         """``x @ w.T`` in fp8 with bf16 output; x: [M, K] bf16, w: [N, K] bf16.  Without flags returns y.  With
         ``keep_w8`` / ``keep_xt`` returns ``(y, w8t, xt8)``: the quantised weight in the [K, N] layout the
         input-gradient GEMM needs and the quantised activation in the [K, M] layout of the weight-gradient GEMM
-        (each written by the same cast pass as the forward operand; None when not asked for)."""
+        (each written by the same cast pass as the forward operand; None when not asked for).  ``xq`` = (x8, xt8):
+        x already quantised in both layouts by its producer in slot ``x_slot`` (``swiglu_fwd_cast_t``); x is then
+        not read."""
         xt8 = None
-        if keep_xt:
+        if xq is not None:
+            x8, xt8 = xq
+        elif keep_xt:
             x8, xt8 = self.cast_t(x, x_slot) if _t_ok(x) else (self.cast(x, x_slot), None)
             if xt8 is None:
                 xt8 = x8.t().contiguous()
@@ -195,20 +199,25 @@ def wgrad_acc(g8t: Tensor, xt8: Tensor, sg: Tensor, sx: Tensor, out: Tensor) -> 
     out.add_(torch._scaled_mm(g8t, xt8.t(), scale_a=sg, scale_b=sx, out_dtype=torch.bfloat16))
 
 
-def grads(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8State, w_slot: int,
-          xt8: Tensor | None = None, x_state: Fp8State | None = None, x_slot: int = 0, dw_out: Tensor | None = None):
+def grads(g_state: Fp8State, g: Tensor | None, g_slot: int, w8t: Tensor, w_state: Fp8State, w_slot: int,
+          xt8: Tensor | None = None, x_state: Fp8State | None = None, x_slot: int = 0, dw_out: Tensor | None = None,
+          gq: tuple[Tensor, Tensor] | None = None):
     """Input gradient ``g @ W`` and, with ``xt8``, weight gradient ``g^T @ X`` of one projection from ONE e5m2 cast
     of g: (dX, dW or None).  dW = g8t [N, tokens] x xt8 [K, tokens] -> [N, K], both operands contiguous along the
     token reduction; its scale is g's inverse scale times X's (slot ``x_slot`` of ``x_state``).  With ``dw_out``
-    the weight gradient is accumulated into it (:func:`wgrad_acc`) and None is returned in its place."""
+    the weight gradient is accumulated into it (:func:`wgrad_acc`) and None is returned in its place.  ``gq`` =
+    (g8, g8t): g already quantised in both layouts in slot ``g_slot`` by its producer (``swiglu_bwd_cast_t``)."""
     if xt8 is None:
         return dgrad(g_state, g, g_slot, w8t, w_state, w_slot), None
-    g = g.contiguous()
-    if _t_ok(g):
-        g8, g8t = g_state.cast_t(g, g_slot)
+    if gq is not None:
+        g8, g8t = gq
     else:
-        g8 = g_state.cast(g, g_slot)
-        g8t = g8.t().contiguous()
+        g = g.contiguous()
+        if _t_ok(g):
+            g8, g8t = g_state.cast_t(g, g_slot)
+        else:
+            g8 = g_state.cast(g, g_slot)
+            g8t = g8.t().contiguous()
     gi = g_state.inv_scale[g_slot]
     dx = mm_fp8(g8, w8t, gi, w_state.inv_scale[w_slot])
     if dw_out is not None:
@@ -216,6 +225,32 @@ def grads(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8St
         return dx, None
     dw = mm_fp8(g8t, xt8, gi, x_state.inv_scale[x_slot])
     return dx, dw
+
+
+def swiglu_cast_ok(gu: Tensor) -> bool:
+    """gu = [g | u] that the fused SwiGLU + two-layout cast takes: bf16, contiguous, tokens and F multiples of 64."""
+    return (gu.dtype == torch.bfloat16 and gu.dim() == 2 and gu.is_contiguous() and gu.shape[0] % 64 == 0
+            and gu.shape[1] % 128 == 0)
+
+
+def swiglu_fwd_cast_t(state: Fp8State, gu: Tensor, slot: int) -> tuple[Tensor, Tensor]:
+    """a = silu(g) * u of gu = [g | u] ([M, 2F] bf16), written only in fp8 (this state's format, e4m3) in both layouts
+    (a8 [M, F], a8t [F, M]; slot ``slot``): one pass instead of ``swiglu_fwd`` plus ``cast_t`` (csrc/fp8.hip)."""
+    M, F = gu.shape[0], gu.shape[1] // 2
+    a8 = torch.empty(M, F, dtype=state.dtype, device=gu.device)
+    a8t = torch.empty(F, M, dtype=state.dtype, device=gu.device)
+    ops().swiglu_cast_fp8_t(gu, None, state.scale[slot : slot + 1], a8, a8t, state.amax[slot : slot + 1])
+    return a8, a8t
+
+
+def swiglu_bwd_cast_t(state: Fp8State, da: Tensor, gu: Tensor, slot: int) -> tuple[Tensor, Tensor]:
+    """The SwiGLU gate gradient [dg | du] from da [M, F] and gu [M, 2F], written only in fp8 (e5m2) in both layouts
+    (dgu8 [M, 2F], dgu8t [2F, M]; slot ``slot``): one pass instead of ``swiglu_bwd`` plus ``cast_t``."""
+    M, F2 = gu.shape
+    g8 = torch.empty(M, F2, dtype=state.dtype, device=gu.device)
+    g8t = torch.empty(F2, M, dtype=state.dtype, device=gu.device)
+    ops().swiglu_cast_fp8_t(gu, da.contiguous(), state.scale[slot : slot + 1], g8, g8t, state.amax[slot : slot + 1])
+    return g8, g8t
 
 
 def quantize_reference(x: Tensor, scale: float, fmt: str = "e4m3") -> Tensor:

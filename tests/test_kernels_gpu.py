@@ -866,6 +866,42 @@ def test_cast_fp8_transposed(gpu_device, N, K, fmt):
     assert am == float(w.float().abs().max())
 
 
+@pytest.mark.parametrize("M,F", [(256, 192), (1024, 512)])
+def test_swiglu_cast_fp8_transposed(gpu_device, M, F):
+    """SwiGLU with the two-layout fp8 cast fused (fp8.hip swiglu_cast_fp8_t): forward a = silu(g) u as e4m3 [M, F] and
+    [F, M], backward [dg | du] as e5m2 [M, 2F] and [2F, M] -- against the two-pass form (swiglu_fwd / swiglu_bwd to
+    bf16, then cast_fp8_t) on the same scale: the kernels round to bf16 first, so the bytes and the amax agree (up to
+    the rare value whose bf16 rounding the compiler's fused multiply-adds move by one ulp)."""
+    from bpe_transformer.ops.fp8 import Fp8State, swiglu_bwd_cast_t, swiglu_fwd_cast_t
+    h = torch.ops.bpe_hip
+    torch.manual_seed(7)
+    gu = torch.randn(M, 2 * F, device=gpu_device, dtype=torch.bfloat16) * 2
+    da = torch.randn(M, F, device=gpu_device, dtype=torch.bfloat16) * 0.01
+
+    def two_pass(x, fmt, scale):
+        amax = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+        x8 = torch.empty(x.shape, dtype=fmt, device=gpu_device)
+        x8t = torch.empty(x.shape[1], x.shape[0], dtype=fmt, device=gpu_device)
+        h.cast_fp8_t(x, scale, x8, x8t, amax)
+        return x8, x8t, amax.view(torch.float32).item()
+
+    for fwd in (True, False):
+        st = Fp8State(1, gpu_device, fmt="e4m3" if fwd else "e5m2")
+        st.scale.fill_(8.0 if fwd else 2048.0)
+        if fwd:
+            o8, o8t = swiglu_fwd_cast_t(st, gu, 0)
+            r8, r8t, ram = two_pass(h.swiglu_fwd(gu), st.dtype, st.scale[:1])
+        else:
+            o8, o8t = swiglu_bwd_cast_t(st, da, gu, 0)
+            r8, r8t, ram = two_pass(h.swiglu_bwd(da, gu), st.dtype, st.scale[:1])
+        assert torch.equal(o8t.view(torch.uint8), o8.view(torch.uint8).t().contiguous())
+        diff = (o8.view(torch.uint8) != r8.view(torch.uint8)).float().mean().item()
+        assert diff < 1e-3, (fwd, diff)
+        assert rel(o8.float(), r8.float()) < 1e-2
+        am = st.amax.view(torch.float32).item()
+        assert abs(am - ram) <= 1e-2 * ram, (fwd, am, ram)
+
+
 def test_fp8_grads_weight_gradient(gpu_device):
     """ops.fp8.grads: one e5m2 cast of the output gradient serves dX = g W and dW = g^T X; both against the fp32
     products of the dequantised operands (the weight-gradient GEMM reduces over all tokens: M = N_out, K = T)."""

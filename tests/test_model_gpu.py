@@ -136,6 +136,32 @@ def test_fp8_close_to_bf16(gpu_device, dgrad, wgrad):
         assert e < (0.2 if dgrad else 0.15), (n, float(e))
 
 
+def test_fp8_swiglu_cast_fused_matches_two_pass(gpu_device, monkeypatch):
+    """fp8 weight-gradient path: the SwiGLU gate and its backward writing only fp8 in both layouts (one pass with the
+    cast) give the loss and gradients of the two-pass form (bf16 a / dgu, then the two-layout cast)."""
+    from bpe_transformer.models import fused_block
+
+    assert fused_block._FP8_SWIGLU_CAST
+    _, a = _pair(gpu_device)
+    a.enable_fp8(dgrad=True, wgrad=True)
+    ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    a.loss(ids, tgt).backward()  # calibration
+    for s_ in a.fp8_states():
+        s_.update()
+    a.zero_grad()
+    b = copy.deepcopy(a)
+    la = a.loss(ids, tgt)
+    la.backward()
+    monkeypatch.setattr(fused_block, "_FP8_SWIGLU_CAST", False)
+    lb = b.loss(ids, tgt)
+    lb.backward()
+    assert abs(la.item() - lb.item()) < 1e-3, (la.item(), lb.item())
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        e = (pb.grad.float() - pa.grad.float()).norm() / pa.grad.float().norm().clamp_min(1e-12)
+        assert e < 2e-2, (n, float(e))
+
+
 def test_fp8_engine_reduces_loss(gpu_device):
     from bpe_transformer.train.engine import TrainEngine
 
