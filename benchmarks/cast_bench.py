@@ -1,0 +1,51 @@
+"""fp8 cast kernels at the fp8 Llama config's tensor shapes (65 536 tokens): the two-layout cast (cast_fp8_t), the
+plain row-major cast (cast_fp8) and a bf16 copy for the HBM reference, in effective TB/s (bytes read + written).
+
+    python benchmarks/cast_bench.py
+"""
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from bpe_transformer.ops._ext import ops  # noqa: E402
+
+
+def timeit(fn, iters=10):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    h = ops()
+    for T, N in [(65536, 2048), (65536, 2560), (65536, 11264), (2560, 2048)]:
+        x = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+        s = torch.ones(1, device="cuda")
+        am = torch.zeros(1, dtype=torch.int32, device="cuda")
+        o8 = torch.empty(T, N, dtype=torch.float8_e5m2, device="cuda")
+        o8t = torch.empty(N, T, dtype=torch.float8_e5m2, device="cuda")
+        y = torch.empty_like(x)
+        arms = {"cast_t": (lambda: h.cast_fp8_t(x, s, o8, o8t, am), 4),
+                "cast": (lambda: h.cast_fp8(x, s, o8, am), 3),
+                "bf16_copy": (lambda: y.copy_(x), 4)}
+        t = {k: [] for k in arms}
+        for _ in range(3):
+            for k, (fn, _) in arms.items():
+                t[k].append(timeit(fn))
+        for k, (_, bpe) in arms.items():
+            m = statistics.median(t[k])
+            print(json.dumps({"shape": [T, N], "op": k, "us": round(m * 1e3, 1),
+                              "TBps": round(T * N * bpe / m / 1e9, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

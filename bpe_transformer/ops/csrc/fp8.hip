@@ -131,6 +131,93 @@ __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const __bf16* __restric
     if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
 
+// The same two-layout cast on 128 x 128 tiles (N, K multiples of 128): every output row segment a thread group writes
+// is a whole 128-byte line in both layouts (the 64 x 64 kernel writes 64-byte halves, 3.4-3.5 TB/s effective against
+// 5.4-5.5 for the one-layout cast, profiles/bench/cast_bench_r4.log), and each thread keeps eight 16-byte loads in
+// flight.  Transposed reads: a thread takes one 32-bit word (4 k values) from each of 16 tile rows and turns every 4
+// x 4 byte block around with v_perm_b32, so it stores 16 consecutive n for each of its 4 output rows.
+template <int FMT>
+__global__ void __launch_bounds__(256) cast_fp8_t128_kernel(const __bf16* __restrict__ w, int N, int K,
+                                                            const float* __restrict__ scale, uint8_t* __restrict__ w8,
+                                                            uint8_t* __restrict__ w8t,
+                                                            unsigned* __restrict__ amax_bits) {
+    constexpr int TS = 132;  // LDS row stride (bytes): 33 words, so a 32-lane half's column reads hit 32 banks
+    __shared__ __attribute__((aligned(16))) uint8_t tile[128 * TS];
+    __shared__ float red[4];
+    const int tid = threadIdx.x;
+    const int tiles_k = K / 128, ntiles = (N / 128) * tiles_k;
+    const float sc = *scale;
+    const int r = tid >> 1, hc = (tid & 1) * 64;  // load / row-major phase: tile row r, columns hc .. hc + 63
+    // transposed phase: output rows 4 kq .. +3, tile rows 16 ns .. +15; the 8 ns of one kq are adjacent lanes, so
+    // one store instruction of a wave writes 8 whole 128-byte output rows
+    const int kq = tid >> 3, ns = tid & 7;
+    // LDS word column c of tile row n sits at c ^ sw(n): the column reads of a 32-lane half (4 kq x 8 ns) then hit
+    // 32 distinct banks
+    auto sw = [](int n) { return ((n >> 4) & 7) << 2; };
+    float am = 0.f;
+    // the next tile's rows are loaded as soon as this tile's are converted, so they are in flight through the
+    // stores and the LDS transpose; the LDS hand-offs use raw barriers behind lgkmcnt(0) only (__syncthreads would
+    // also wait for those loads)
+    u16x8 a[8];
+    auto load = [&](int tt) {
+        const int n0 = (tt / tiles_k) * 128, k0 = (tt % tiles_k) * 128;
+        const __bf16* src = w + (long)(n0 + r) * K + k0 + hc;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const u16x8*>(src + 8 * i);
+    };
+    if (blockIdx.x < ntiles) load(blockIdx.x);
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int n0 = (t / tiles_k) * 128, k0 = (t % tiles_k) * 128;
+        unsigned q[16];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                v[j] = bf2f(a[i][j]);
+                am = fmaxf(am, fabsf(v[j]));
+            }
+            q[2 * i] = pack4_fp8<FMT>(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc);
+            q[2 * i + 1] = pack4_fp8<FMT>(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc);
+        }
+        if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);
+        uint8_t* dst = w8 + (long)(n0 + r) * K + k0 + hc;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<uint4*>(dst + 16 * i) = uint4{q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]};
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous tile's transposed reads are done
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) *reinterpret_cast<unsigned*>(&tile[r * TS + 4 * ((hc / 4 + i) ^ sw(r))]) = q[i];
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this thread's tile words are written
+        __builtin_amdgcn_s_barrier();
+        unsigned o[4][4];  // [k offset e][n group g]: bytes n = 16 ns + 4 g .. +3 of output row 4 kq + e
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = 16 * ns + 4 * g, cw = 4 * (kq ^ sw(n));  // sw is the same for the 16 rows of ns
+            const unsigned x0 = *reinterpret_cast<const unsigned*>(&tile[(n + 0) * TS + cw]);
+            const unsigned x1 = *reinterpret_cast<const unsigned*>(&tile[(n + 1) * TS + cw]);
+            const unsigned x2 = *reinterpret_cast<const unsigned*>(&tile[(n + 2) * TS + cw]);
+            const unsigned x3 = *reinterpret_cast<const unsigned*>(&tile[(n + 3) * TS + cw]);
+            // v_perm_b32(s0, s1, sel): selector byte 0-3 takes that byte of s1, 4-7 byte (sel - 4) of s0
+            const unsigned lo01 = __builtin_amdgcn_perm(x1, x0, 0x05010400u);  // x0.0 x1.0 x0.1 x1.1
+            const unsigned hi01 = __builtin_amdgcn_perm(x1, x0, 0x07030602u);  // x0.2 x1.2 x0.3 x1.3
+            const unsigned lo23 = __builtin_amdgcn_perm(x3, x2, 0x05010400u);
+            const unsigned hi23 = __builtin_amdgcn_perm(x3, x2, 0x07030602u);
+            o[0][g] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);  // x0.0 x1.0 x2.0 x3.0
+            o[1][g] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+            o[2][g] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+            o[3][g] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            *reinterpret_cast<uint4*>(w8t + (long)(k0 + 4 * kq + e) * N + n0 + 16 * ns) =
+                uint4{o[e][0], o[e][1], o[e][2], o[e][3]};
+    }
+    am = block_max(am, red);
+    if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
+}
+
 // SwiGLU with the two-layout fp8 cast fused in (the fp8 weight-gradient path, where no bf16 copy of these tensors
 // is kept): MODE 0 forms a = silu(g) u from gu = [g | u] ([M][2F]) and writes a8 [M][F] and a8t [F][M] (FMT e4m3, the
 // W2 projection's input); MODE 1 forms the gate gradient [dg | du] from dout = dA [M][F] and gu and writes dgu8
@@ -248,8 +335,23 @@ void launch_cast_fp8(int dtype, int fmt, const void* x, size_t n, const float* s
 #undef CAST
 }
 
+#ifndef BPE_CAST_T128
+#define BPE_CAST_T128 1
+#endif
+
 void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8, void* w8t, unsigned* amax_bits,
                        int fmt, hipStream_t s) {
+    if (BPE_CAST_T128 && N % 128 == 0 && K % 128 == 0) {
+        const int nt = (N / 128) * (K / 128);
+        const int g = nt < 2048 ? nt : 2048;
+        if (fmt == 0)
+            cast_fp8_t128_kernel<0><<<g, 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8, (uint8_t*)w8t,
+                                                      amax_bits);
+        else
+            cast_fp8_t128_kernel<1><<<g, 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8, (uint8_t*)w8t,
+                                                      amax_bits);
+        return;
+    }
     const int ntiles = (N / 64) * (K / 64);
     const int grid = ntiles < 2048 ? ntiles : 2048;
     if (fmt == 0)

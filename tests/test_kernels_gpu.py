@@ -846,7 +846,9 @@ def test_cast_fp8_and_amax(gpu_device, dtype, n, fmt):
     assert amax.view(torch.float32).item() == x.float().abs().max().item()
 
 
-@pytest.mark.parametrize("N,K", [(192, 320), (4096, 1024)])  # the second: more tiles than the grid (stride loop)
+# (192, 320): the 64 x 64 kernel; the others the 128 x 128 one, (4096, 1024) / (8192, 4096) with more tiles than the
+# grid (stride loop)
+@pytest.mark.parametrize("N,K", [(192, 320), (4096, 1024), (384, 256), (8192, 4096)])
 @pytest.mark.parametrize("fmt", [torch.float8_e4m3fn, torch.float8_e5m2])
 def test_cast_fp8_transposed(gpu_device, N, K, fmt):
     """Two-layout cast (weights; activations and gradients of the fp8 weight-gradient GEMM): both layouts from one
