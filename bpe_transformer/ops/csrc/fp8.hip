@@ -131,6 +131,49 @@ __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const __bf16* __restric
     if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
 
+// 128 x 128 fp8 tile transpose through LDS (the two-layout casts below).  Row-major phase: thread t holds the 64
+// bytes of tile row t >> 1, columns 64 (t & 1) .., as 16 words q.  Transposed phase: thread t emits output rows
+// 4 kq .. 4 kq + 3 (kq = t >> 3) over tile rows 16 ns .. 16 ns + 15 (ns = t & 7): the 8 ns of one kq are adjacent
+// lanes, so one store instruction of a wave writes 8 whole 128-byte output rows.  LDS word column c of tile row n
+// sits at c ^ sw(n), so the column reads of a 32-lane half (4 kq x 8 ns) hit 32 distinct banks.
+constexpr int T128_TS = 132;  // LDS row stride (bytes): 33 words
+__device__ __forceinline__ int t128_sw(int n) { return ((n >> 4) & 7) << 2; }
+
+__device__ __forceinline__ void t128_put(uint8_t* tile, const unsigned (&q)[16], int r, int hc) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) *reinterpret_cast<unsigned*>(&tile[r * T128_TS + 4 * ((hc / 4 + i) ^ t128_sw(r))]) = q[i];
+}
+
+// dst = output row 4 kq of the transposed tile at column 16 ns; ld = output row stride (bytes)
+__device__ __forceinline__ void t128_get_store(const uint8_t* tile, int kq, int ns, uint8_t* dst, long ld) {
+    unsigned o[4][4];  // [k offset e][n group g]: bytes n = 16 ns + 4 g .. +3 of output row 4 kq + e
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int n = 16 * ns + 4 * g, cw = 4 * (kq ^ t128_sw(n));  // sw is the same for the 16 rows of ns
+        const unsigned x0 = *reinterpret_cast<const unsigned*>(&tile[(n + 0) * T128_TS + cw]);
+        const unsigned x1 = *reinterpret_cast<const unsigned*>(&tile[(n + 1) * T128_TS + cw]);
+        const unsigned x2 = *reinterpret_cast<const unsigned*>(&tile[(n + 2) * T128_TS + cw]);
+        const unsigned x3 = *reinterpret_cast<const unsigned*>(&tile[(n + 3) * T128_TS + cw]);
+        // v_perm_b32(s0, s1, sel): selector byte 0-3 takes that byte of s1, 4-7 byte (sel - 4) of s0
+        const unsigned lo01 = __builtin_amdgcn_perm(x1, x0, 0x05010400u);  // x0.0 x1.0 x0.1 x1.1
+        const unsigned hi01 = __builtin_amdgcn_perm(x1, x0, 0x07030602u);  // x0.2 x1.2 x0.3 x1.3
+        const unsigned lo23 = __builtin_amdgcn_perm(x3, x2, 0x05010400u);
+        const unsigned hi23 = __builtin_amdgcn_perm(x3, x2, 0x07030602u);
+        o[0][g] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);  // x0.0 x1.0 x2.0 x3.0
+        o[1][g] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+        o[2][g] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+        o[3][g] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) *reinterpret_cast<uint4*>(dst + e * ld) = uint4{o[e][0], o[e][1], o[e][2], o[e][3]};
+}
+
+// raw barrier behind lgkmcnt(0) only: LDS hand-off without waiting for outstanding global loads / stores
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+}
+
 // The same two-layout cast on 128 x 128 tiles (N, K multiples of 128): every output row segment a thread group writes
 // is a whole 128-byte line in both layouts (the 64 x 64 kernel writes 64-byte halves, 3.4-3.5 TB/s effective against
 // 5.4-5.5 for the one-layout cast, profiles/bench/cast_bench_r4.log), and each thread keeps eight 16-byte loads in
@@ -141,19 +184,13 @@ __global__ void __launch_bounds__(256) cast_fp8_t128_kernel(const __bf16* __rest
                                                             const float* __restrict__ scale, uint8_t* __restrict__ w8,
                                                             uint8_t* __restrict__ w8t,
                                                             unsigned* __restrict__ amax_bits) {
-    constexpr int TS = 132;  // LDS row stride (bytes): 33 words, so a 32-lane half's column reads hit 32 banks
-    __shared__ __attribute__((aligned(16))) uint8_t tile[128 * TS];
+    __shared__ __attribute__((aligned(16))) uint8_t tile[128 * T128_TS];
     __shared__ float red[4];
     const int tid = threadIdx.x;
     const int tiles_k = K / 128, ntiles = (N / 128) * tiles_k;
     const float sc = *scale;
     const int r = tid >> 1, hc = (tid & 1) * 64;  // load / row-major phase: tile row r, columns hc .. hc + 63
-    // transposed phase: output rows 4 kq .. +3, tile rows 16 ns .. +15; the 8 ns of one kq are adjacent lanes, so
-    // one store instruction of a wave writes 8 whole 128-byte output rows
-    const int kq = tid >> 3, ns = tid & 7;
-    // LDS word column c of tile row n sits at c ^ sw(n): the column reads of a 32-lane half (4 kq x 8 ns) then hit
-    // 32 distinct banks
-    auto sw = [](int n) { return ((n >> 4) & 7) << 2; };
+    const int kq = tid >> 3, ns = tid & 7;  // transposed phase (t128_get_store)
     float am = 0.f;
     // the next tile's rows are loaded as soon as this tile's are converted, so they are in flight through the
     // stores and the LDS transpose; the LDS hand-offs use raw barriers behind lgkmcnt(0) only (__syncthreads would
@@ -185,34 +222,10 @@ __global__ void __launch_bounds__(256) cast_fp8_t128_kernel(const __bf16* __rest
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             *reinterpret_cast<uint4*>(dst + 16 * i) = uint4{q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]};
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous tile's transposed reads are done
-        __builtin_amdgcn_s_barrier();
-#pragma unroll
-        for (int i = 0; i < 16; ++i) *reinterpret_cast<unsigned*>(&tile[r * TS + 4 * ((hc / 4 + i) ^ sw(r))]) = q[i];
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this thread's tile words are written
-        __builtin_amdgcn_s_barrier();
-        unsigned o[4][4];  // [k offset e][n group g]: bytes n = 16 ns + 4 g .. +3 of output row 4 kq + e
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int n = 16 * ns + 4 * g, cw = 4 * (kq ^ sw(n));  // sw is the same for the 16 rows of ns
-            const unsigned x0 = *reinterpret_cast<const unsigned*>(&tile[(n + 0) * TS + cw]);
-            const unsigned x1 = *reinterpret_cast<const unsigned*>(&tile[(n + 1) * TS + cw]);
-            const unsigned x2 = *reinterpret_cast<const unsigned*>(&tile[(n + 2) * TS + cw]);
-            const unsigned x3 = *reinterpret_cast<const unsigned*>(&tile[(n + 3) * TS + cw]);
-            // v_perm_b32(s0, s1, sel): selector byte 0-3 takes that byte of s1, 4-7 byte (sel - 4) of s0
-            const unsigned lo01 = __builtin_amdgcn_perm(x1, x0, 0x05010400u);  // x0.0 x1.0 x0.1 x1.1
-            const unsigned hi01 = __builtin_amdgcn_perm(x1, x0, 0x07030602u);  // x0.2 x1.2 x0.3 x1.3
-            const unsigned lo23 = __builtin_amdgcn_perm(x3, x2, 0x05010400u);
-            const unsigned hi23 = __builtin_amdgcn_perm(x3, x2, 0x07030602u);
-            o[0][g] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);  // x0.0 x1.0 x2.0 x3.0
-            o[1][g] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
-            o[2][g] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
-            o[3][g] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            *reinterpret_cast<uint4*>(w8t + (long)(k0 + 4 * kq + e) * N + n0 + 16 * ns) =
-                uint4{o[e][0], o[e][1], o[e][2], o[e][3]};
+        lds_barrier();  // the previous tile's transposed reads are done
+        t128_put(tile, q, r, hc);
+        lds_barrier();
+        t128_get_store(tile, kq, ns, w8t + (long)(k0 + 4 * kq) * N + n0 + 16 * ns, N);
     }
     am = block_max(am, red);
     if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
@@ -302,6 +315,83 @@ __global__ void __launch_bounds__(256) swiglu_cast_fp8_t_kernel(const __bf16* __
     if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
 
+// The SwiGLU + two-layout cast on 128 x 128 tiles (M and F multiples of 128; the t128 helpers above): whole 128-byte
+// output lines in both layouts, as cast_fp8_t128_kernel.  Values, rounding and amax as swiglu_cast_fp8_t_kernel.
+template <int MODE, int FMT>
+__global__ void __launch_bounds__(256) swiglu_cast_fp8_t128_kernel(const __bf16* __restrict__ gu,
+                                                                   const __bf16* __restrict__ dout, int M, int F,
+                                                                   const float* __restrict__ scale,
+                                                                   uint8_t* __restrict__ o8, uint8_t* __restrict__ o8t,
+                                                                   unsigned* __restrict__ amax_bits) {
+    constexpr int NO = MODE == 0 ? 1 : 2;  // output column blocks per tile: a, or dg and du
+    __shared__ __attribute__((aligned(16))) uint8_t tile[NO][128 * T128_TS];
+    __shared__ float red[4];
+    const int tid = threadIdx.x;
+    const int tiles_f = F / 128, ntiles = (M / 128) * tiles_f;
+    const long W = (long)NO * F;  // output row length
+    const float sc = *scale;
+    const int r = tid >> 1, hc = (tid & 1) * 64;
+    const int kq = tid >> 3, ns = tid & 7;
+    float am = 0.f;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int m0 = (t / tiles_f) * 128, f0 = (t % tiles_f) * 128;
+        const __bf16* row = gu + (long)(m0 + r) * 2 * F + f0 + hc;
+        u16x8 g[8], u[8], d[MODE == 1 ? 8 : 1];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            g[i] = *reinterpret_cast<const u16x8*>(row + 8 * i);
+            u[i] = *reinterpret_cast<const u16x8*>(row + F + 8 * i);
+        }
+        if constexpr (MODE == 1) {
+            const __bf16* dr = dout + (long)(m0 + r) * F + f0 + hc;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) d[i] = *reinterpret_cast<const u16x8*>(dr + 8 * i);
+        }
+        unsigned q[NO][16];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float v[NO][8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float gg = bf2f(g[i][j]), uu = bf2f(u[i][j]);
+                const float sg = fast_sigmoid(gg);
+                if constexpr (MODE == 0) {
+                    v[0][j] = bf2f(f2bf(gg * sg * uu));
+                } else {
+                    const float dd = bf2f(d[i][j]);
+                    const float silu = gg * sg;
+                    v[1][j] = bf2f(f2bf(dd * silu));                               // du
+                    v[0][j] = bf2f(f2bf(dd * uu * sg * (1.f + gg * (1.f - sg))));  // dg
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < NO; ++o) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v[o][j]));
+                q[o][2 * i] = pack4_fp8<FMT>(v[o][0] * sc, v[o][1] * sc, v[o][2] * sc, v[o][3] * sc);
+                q[o][2 * i + 1] = pack4_fp8<FMT>(v[o][4] * sc, v[o][5] * sc, v[o][6] * sc, v[o][7] * sc);
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            uint8_t* dst = o8 + (long)(m0 + r) * W + (long)o * F + f0 + hc;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<uint4*>(dst + 16 * i) =
+                    uint4{q[o][4 * i], q[o][4 * i + 1], q[o][4 * i + 2], q[o][4 * i + 3]};
+        }
+        lds_barrier();  // the previous tile's transposed reads are done
+#pragma unroll
+        for (int o = 0; o < NO; ++o) t128_put(tile[o], q[o], r, hc);
+        lds_barrier();
+#pragma unroll
+        for (int o = 0; o < NO; ++o)
+            t128_get_store(tile[o], kq, ns, o8t + ((long)o * F + f0 + 4 * kq) * M + m0 + 16 * ns, M);
+    }
+    am = block_max(am, red);
+    if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
+}
+
 // amax_cur [n] (float bits, zeroed here after use), hist [n][H], scale/inv [n]
 __global__ void __launch_bounds__(256) update_scales_kernel(unsigned* __restrict__ amax_cur, float* __restrict__ hist,
                                                             float* __restrict__ scale, float* __restrict__ inv_scale,
@@ -324,6 +414,11 @@ __global__ void __launch_bounds__(256) update_scales_kernel(unsigned* __restrict
 
 using namespace bpe;
 
+// 1: the 128 x 128 tile kernels where the shape allows (a variant build with 0 keeps the 64 x 64 ones for A/B)
+#ifndef BPE_CAST_T128
+#define BPE_CAST_T128 1
+#endif
+
 void launch_cast_fp8(int dtype, int fmt, const void* x, size_t n, const float* scale, void* out,
                      unsigned* amax_bits, hipStream_t s) {
     if (n == 0) return;
@@ -334,10 +429,6 @@ void launch_cast_fp8(int dtype, int fmt, const void* x, size_t n, const float* s
     else { if (fmt == 0) CAST(float, 0); else CAST(float, 1); }
 #undef CAST
 }
-
-#ifndef BPE_CAST_T128
-#define BPE_CAST_T128 1
-#endif
 
 void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8, void* w8t, unsigned* amax_bits,
                        int fmt, hipStream_t s) {
@@ -364,6 +455,17 @@ void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8
 
 void launch_swiglu_cast_fp8_t(int mode, const void* gu, const void* dout, int M, int F, const float* scale, void* o8,
                               void* o8t, unsigned* amax_bits, hipStream_t s) {
+    if (BPE_CAST_T128 && M % 128 == 0 && F % 128 == 0) {
+        const int nt = (M / 128) * (F / 128);
+        const int g = nt < 2048 ? nt : 2048;
+        if (mode == 0)
+            swiglu_cast_fp8_t128_kernel<0, 0><<<g, 256, 0, s>>>((const __bf16*)gu, nullptr, M, F, scale,
+                                                                (uint8_t*)o8, (uint8_t*)o8t, amax_bits);
+        else
+            swiglu_cast_fp8_t128_kernel<1, 1><<<g, 256, 0, s>>>((const __bf16*)gu, (const __bf16*)dout, M, F, scale,
+                                                                (uint8_t*)o8, (uint8_t*)o8t, amax_bits);
+        return;
+    }
     const int ntiles = (M / 64) * (F / 64);
     const int grid = ntiles < 2048 ? ntiles : 2048;
     if (mode == 0)
