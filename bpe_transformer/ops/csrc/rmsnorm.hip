@@ -235,6 +235,96 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const T* __restrict__ 
     }
 }
 
+// Half-wave rows (N / V a multiple of 32 and at most 128, e.g. d_model 768 in bf16: 96 vectors): each 32-lane half
+// of a wave owns one row, lane vectors (lane & 31) + 32 c.  At N = 768 the one-wave-per-row kernel above leaves half
+// of its lanes idle in its second chunk; here every lane holds 3 vectors per tensor and a wave has two rows' loads in
+// flight (plus the next two prefetched).  Same arithmetic per element; the row dot product is summed over 32 lanes.
+template <typename T, int C>
+__global__ void __launch_bounds__(256) rmsnorm_bwd_hw_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                             const T* __restrict__ w,
+                                                             const float* __restrict__ rstd, T* __restrict__ dx,
+                                                             float* __restrict__ dw_partial,
+                                                             const T* __restrict__ dres, int M, int N) {
+    constexpr int V = Vec<T>::N;
+    extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][N]
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hl = lane & 31, half = lane >> 5;
+    float dwacc[C][V], wv[C][V];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        Vec<T> g;
+        g.load(w + (c * 32 + hl) * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) { dwacc[c][j] = 0.f; wv[c][j] = g.v[j]; }
+    }
+    typedef typename RawV<T>::type R;
+    R xa[C], ga[C], ra[C];
+    float rcur = 0.f;
+    auto load_row = [&](int row, R* xo, R* go, R* ro, float& rr) {
+        rr = rstd[row];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const size_t off = (size_t)row * N + (c * 32 + hl) * V;
+            xo[c] = ld_stream(reinterpret_cast<const R*>(x + off));
+            go[c] = ld_stream(reinterpret_cast<const R*>(dy + off));
+            ro[c] = dres ? ld_stream(reinterpret_cast<const R*>(dres + off)) : R{};
+        }
+    };
+    // rows 2 (4 b + w) + half, stride 8 gridDim.x; M is even whenever this kernel runs (rows come in pairs)
+    const int stride = gridDim.x * 8;
+    int row = (blockIdx.x * 4 + wid) * 2 + half;
+    if (row < M) load_row(row, xa, ga, ra, rcur);
+    for (; row < M; row += stride) {
+        R xb[C], gb[C], rb[C];
+        float rnext = 0.f;
+        if (row + stride < M) load_row(row + stride, xb, gb, rb, rnext);
+        const float r = rcur;
+        float dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int j = 0; j < V; ++j)
+                dot += RawV<T>::get(ga[c], j) * wv[c][j] * (RawV<T>::get(xa[c], j) * r);
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);  // within the 32-lane half
+        dot /= (float)N;
+        T* dxr = dx + (size_t)row * N;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            Vec<T> o;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const float xh = RawV<T>::get(xa[c], j) * r, g = RawV<T>::get(ga[c], j);
+                o.v[j] = r * (g * wv[c][j] - xh * dot) + RawV<T>::get(ra[c], j);
+                dwacc[c][j] += g * xh;
+            }
+            o.store_s(dxr + (c * 32 + hl) * V);
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            xa[c] = xb[c];
+            ga[c] = gb[c];
+            ra[c] = rb[c];
+        }
+        rcur = rnext;
+    }
+    // both halves of a wave accumulated the same columns: add them, then the 4 waves through LDS
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int j = 0; j < V; ++j) dwacc[c][j] += __shfl_xor(dwacc[c][j], 32, 64);
+    if (half == 0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int j = 0; j < V; ++j) lds[wid * N + (c * 32 + hl) * V + j] = dwacc[c][j];
+    }
+    __syncthreads();
+    for (int col = threadIdx.x; col < N; col += 256) {
+        float s = lds[col] + lds[N + col] + lds[2 * N + col] + lds[3 * N + col];
+        dw_partial[(size_t)blockIdx.x * N + col] = s;
+    }
+}
+
 // Wide rows (N / V >= 256, e.g. d_model 2048 in bf16): the 4 waves of a block share each row -- thread t owns
 // vectors t + 256 c -- and the block processes RPI rows at a time, so every thread keeps only C2 (usually 1)
 // vectors per row in registers.  The one-wave-per-row kernel above needs C = 4 chunks per lane there (182
@@ -373,9 +463,15 @@ void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float*
                                                          eps);
 }
 
+// 1: the half-wave-row backward where the row width allows (a variant build with 0 keeps the one-wave-per-row kernel)
+#ifndef BPE_RMS_BWD_HW
+#define BPE_RMS_BWD_HW 1
+#endif
+
+// returns the grid it launched (the partial rows colsum_kernel then sums; at most the grid it was given)
 template <typename T>
-static void rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* rstd, T* dx, float* partial,
-                             const T* dres, int grid, int M, int N, hipStream_t s) {
+static int rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* rstd, T* dx, float* partial,
+                            const T* dres, int grid, int M, int N, hipStream_t s) {
     constexpr int V = Vec<T>::N;
     if (N / V >= 256 && (N / V) % 256 == 0 && N / V <= 1024) {
         switch (N / V / 256) {
@@ -384,17 +480,27 @@ static void rms_bwd_dispatch(const T* dy, const T* x, const T* w, const float* r
             case 3: rmsnorm_bwd_wide_kernel<T, 3, 1><<<grid, 256, 0, s>>>(dy, x, w, rstd, dx, partial, dres, M, N); break;
             default: rmsnorm_bwd_wide_kernel<T, 4, 1><<<grid, 256, 0, s>>>(dy, x, w, rstd, dx, partial, dres, M, N); break;
         }
-        return;
+        return grid;
+    }
+    const size_t lds = (size_t)4 * N * sizeof(float);
+    if (BPE_RMS_BWD_HW && M % 2 == 0 && (N / V) % 32 == 0 && N / V >= 64 && N / V <= 128) {
+        grid = grid < 512 ? grid : 512;  // one resident round: 2 workgroups per CU at 184 VGPRs (C = 3)
+        switch (N / V / 32) {
+            case 2: rmsnorm_bwd_hw_kernel<T, 2><<<grid, 256, lds, s>>>(dy, x, w, rstd, dx, partial, dres, M, N); break;
+            case 3: rmsnorm_bwd_hw_kernel<T, 3><<<grid, 256, lds, s>>>(dy, x, w, rstd, dx, partial, dres, M, N); break;
+            default: rmsnorm_bwd_hw_kernel<T, 4><<<grid, 256, lds, s>>>(dy, x, w, rstd, dx, partial, dres, M, N); break;
+        }
+        return grid;
     }
     const int chunks = (N / V + 63) / 64;
-    const size_t lds = (size_t)4 * N * sizeof(float);
 #define RMS_CASE(CC)                                                                                    \
     if (chunks <= CC) {                                                                                 \
         rmsnorm_bwd_kernel<T, CC><<<grid, 256, lds, s>>>(dy, x, w, rstd, dx, partial, dres, M, N);      \
-        return;                                                                                         \
+        return grid;                                                                                    \
     }
     RMS_CASE(1) RMS_CASE(2) RMS_CASE(4) RMS_CASE(8)
 #undef RMS_CASE
+    return grid;
 }
 
 void launch_add_rmsnorm_fwd(int dtype, const void* x, const void* d, const void* w, void* sum, void* y, float* rstd,
@@ -426,14 +532,14 @@ int rmsnorm_bwd_grid(int M) {
 
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
                         float* partial, void* dw, const void* dres, int M, int N, hipStream_t s) {
-    const int grid = rmsnorm_bwd_grid(M);
+    const int grid = rmsnorm_bwd_grid(M);  // the partial buffer's rows (the kernel may use fewer)
     if (dtype == DT_BF16) {
-        rms_bwd_dispatch<__bf16>((const __bf16*)dy, (const __bf16*)x, (const __bf16*)w, rstd, (__bf16*)dx, partial,
-                                 (const __bf16*)dres, grid, M, N, s);
-        colsum_kernel<__bf16><<<(N + 63) / 64, 1024, 0, s>>>(partial, (__bf16*)dw, grid, N);
+        const int g = rms_bwd_dispatch<__bf16>((const __bf16*)dy, (const __bf16*)x, (const __bf16*)w, rstd,
+                                               (__bf16*)dx, partial, (const __bf16*)dres, grid, M, N, s);
+        colsum_kernel<__bf16><<<(N + 63) / 64, 1024, 0, s>>>(partial, (__bf16*)dw, g, N);
     } else {
-        rms_bwd_dispatch<float>((const float*)dy, (const float*)x, (const float*)w, rstd, (float*)dx, partial,
-                                (const float*)dres, grid, M, N, s);
-        colsum_kernel<float><<<(N + 63) / 64, 1024, 0, s>>>(partial, (float*)dw, grid, N);
+        const int g = rms_bwd_dispatch<float>((const float*)dy, (const float*)x, (const float*)w, rstd, (float*)dx,
+                                              partial, (const float*)dres, grid, M, N, s);
+        colsum_kernel<float><<<(N + 63) / 64, 1024, 0, s>>>(partial, (float*)dw, g, N);
     }
 }

@@ -31,7 +31,10 @@ def _ref_grads(fn, inputs, dout):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(64, 768), (3, 5, 2048), (7, 512), (2048, 2048), (33, 4096)])
+# (64, 768), (4096, 768), (6, 1024) bf16 and (10, 384) fp32: the half-wave-row backward (csrc/rmsnorm.hip), the
+# second with a grid-stride loop over more rows than one round; (7, 512): odd rows, the one-wave-per-row kernel
+@pytest.mark.parametrize("shape", [(64, 768), (3, 5, 2048), (7, 512), (2048, 2048), (33, 4096), (4096, 768), (6, 1024),
+                                   (10, 384)])
 def test_rmsnorm(gpu_device, dtype, shape):
     torch.manual_seed(0)
     x = torch.randn(*shape, device=gpu_device, dtype=dtype, requires_grad=True)
@@ -44,6 +47,26 @@ def test_rmsnorm(gpu_device, dtype, shape):
     assert rel(y.cpu(), yr) < tol
     assert rel(x.grad.cpu(), gx) < tol * 2
     assert rel(w.grad.cpu(), gw) < tol * 2
+
+
+@pytest.mark.parametrize("M,N", [(4096, 768), (64, 512), (7, 768)])
+def test_rmsnorm_bwd_residual_grad(gpu_device, M, N):
+    """rmsnorm_bwd with the residual-branch gradient fused in: dx(dres) == dx + dres and dw unchanged."""
+    torch.manual_seed(2)
+    h = torch.ops.bpe_hip
+    x = torch.randn(M, N, device=gpu_device, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(N, device=gpu_device)).to(torch.bfloat16)
+    _, rstd = h.rmsnorm_fwd(x, w, 1e-5)
+    dy = torch.randn_like(x)
+    dres = torch.randn_like(x)
+    dx0, dw0 = h.rmsnorm_bwd(dy, x, w, rstd, None)
+    dx1, dw1 = h.rmsnorm_bwd(dy, x, w, rstd, dres)
+    assert torch.equal(dw0, dw1)
+    assert rel(dx1.float(), dx0.float() + dres.float()) < 1e-2
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    R.rmsnorm(xr, wr, 1e-5).backward(dy.float())
+    assert rel(dx0.float(), xr.grad) < 2e-2 and rel(dw0.float(), wr.grad) < 2e-2
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
