@@ -13,8 +13,9 @@ forward (x = xr + xd: the previous block's residual and its not-yet-added FFN ou
     gu, a = h2 @ [W1;W3]^T, silu(g)*u our ping-pong GEMM with the gate in its epilogue (csrc/gemm_pp.hip,
                                       d_model <= 1024; else hipBLASLt + the HIP gate kernel)
     g2 = a @ W2^T                     hipBLASLt; the block returns (xm, g2), added by the next norm
-    (fp8 with fp8 weight gradients: the gate writes a only as fp8 in both layouts, and its backward writes the
-    gate gradient only as e5m2 in both layouts: ops/fp8.py swiglu_fwd_cast_t / swiglu_bwd_cast_t)
+    (fp8 with fp8 weight gradients: the two norms write h1 / h2 and the gate writes a only as e4m3 in both
+    layouts, and the gate's backward writes its gradient only as e5m2 in both layouts: ops/fp8.py
+    add_rmsnorm_cast_t, swiglu_fwd_cast_t / swiglu_bwd_cast_t)
 
 backward: the mirror image, with
   * the SwiGLU backward fused into the epilogue of the dY @ W2 GEMM (our
@@ -48,7 +49,7 @@ from torch import Tensor
 
 from ..ops._ext import ops as hip
 from ..ops.attention import prerotate_default
-from ..ops.fp8 import swiglu_bwd_cast_t, swiglu_cast_ok, swiglu_fwd_cast_t
+from ..ops.fp8 import add_rmsnorm_cast_t, norm_cast_ok, swiglu_bwd_cast_t, swiglu_cast_ok, swiglu_fwd_cast_t
 from ..ops.gemm import accumulate_weight_grad
 
 
@@ -96,6 +97,8 @@ _FUSE_QKV_ROPE = True  # module flag (tests and A/B runs compare the unfused pat
 # fp8 weight-gradient path: SwiGLU forward / backward write their outputs only as fp8 in both layouts (one pass with
 # the cast, csrc/fp8.hip swiglu_cast_fp8_t) instead of bf16 plus a cast pass (module flag for tests and A/B runs)
 _FP8_SWIGLU_CAST = True
+# ... and the two RMSNorms write the QKV / W13 projections' inputs only as e4m3 in both layouts (module flag)
+_FP8_NORM_CAST = True
 
 
 def _fuse_qkv_rope(x: Tensor, w: Tensor, S: int) -> bool:
@@ -133,9 +136,16 @@ class FusedBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(D)
         w_qkv = _cat_weights([wq, wk, wv])
         w_13 = _cat_weights([w1, w3])
+        # fp8 weight gradients: the norms write h1 / h2 only as e4m3 in both layouts (they feed nothing else)
+        norm8 = (fp8 is not None and fp8[2] is not None and train and len(fp8) > 4 and bool(fp8[4])
+                 and _FP8_NORM_CAST and norm_cast_ok(xr))
         # block input x2 = xr + xd: the previous block's residual and its un-added FFN output (residual adds
         # are fused into the following RMSNorm instead of a copy-then-accumulate GEMM)
-        if xd is None:
+        h1q = h2q = None
+        if norm8:
+            x2, h1q, r1 = add_rmsnorm_cast_t(fp8[0], xr, xd, ln1, eps, fp8[1] + 0)
+            h1 = None
+        elif xd is None:
             x2 = xr
             h1, r1 = hip().rmsnorm_fwd(x2, ln1, eps)
         else:
@@ -159,7 +169,7 @@ class FusedBlockFn(torch.autograd.Function):
                     xt8s.append(xt8)
                 return y
 
-            qkv = mm(h1, w_qkv, 0)
+            qkv = mm(h1, w_qkv, 0, xq=h1q)
         pre = use_rope and prerotate_default(D)
         if fp8 is None and pre and _fuse_qkv_rope(h1, w_qkv, S):
             # RoPE on Q / K in the projection's epilogue (saved rotated for the backward)
@@ -178,11 +188,15 @@ class FusedBlockFn(torch.autograd.Function):
         o, lse = hip().fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, pre, dq_acc)
         ctx.dq_acc = dq_acc
         g1 = mm(o, wo.detach(), 1) if fp8 is not None else torch.matmul(o, wo.t())
-        xm, h2, r2 = hip().add_rmsnorm_fwd(x2, g1, ln2, eps)
+        if norm8:
+            xm, h2q, r2 = add_rmsnorm_cast_t(fp8[0], x2, g1, ln2, eps, fp8[1] + 2)
+            h2 = None
+        else:
+            xm, h2, r2 = hip().add_rmsnorm_fwd(x2, g1, ln2, eps)
         if fp8 is None and _fuse_swiglu_fwd(h2, w_13):
             gu, a = hip().gemm_swiglu_fwd(h2, w_13)  # the gate in the GEMM epilogue: no second pass over gu
         else:
-            gu = mm(h2, w_13, 2) if fp8 is not None else torch.matmul(h2, w_13.t())
+            gu = mm(h2, w_13, 2, xq=h2q) if fp8 is not None else torch.matmul(h2, w_13.t())
             a = None if xt8s is not None and _FP8_SWIGLU_CAST and swiglu_cast_ok(gu) else hip().swiglu_fwd(gu)
         if a is None:
             # fp8 weight gradients: a = silu(g) u is written only as the W2 GEMM's fp8 operand, in both layouts,

@@ -392,6 +392,96 @@ __global__ void __launch_bounds__(256) swiglu_cast_fp8_t128_kernel(const __bf16*
     if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
 
+// Residual add + RMSNorm with an fp8 output (the fp8 weight-gradient path, where the normalised activation only
+// feeds fp8 GEMMs): s = x + d (bf16, stored: the residual stream; d == nullptr: s = x, not stored), rstd stored,
+// and y = s * rstd * w -- rounded to bf16 exactly as add_rmsnorm_fwd / rmsnorm_fwd store it -- written only as
+// e4m3 [M][N] (scale, amax folded in); transpose_fp8_t128_kernel then writes [N][M].  One wave per row, C 16-byte
+// chunks per lane (N / 8 <= 64 C).  Against the norm + two-layout cast pair it drops the bf16 y write and its re-read.
+template <int C>
+__global__ void __launch_bounds__(256) add_rmsnorm_fp8_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ d,
+                                                              const __bf16* __restrict__ w, __bf16* __restrict__ sum,
+                                                              uint8_t* __restrict__ y8, float* __restrict__ rstd_out,
+                                                              int M, int N, float eps, const float* __restrict__ scale,
+                                                              unsigned* __restrict__ amax_bits) {
+    __shared__ float red[4];
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nvec = N / 8;
+    float am = 0.f;
+    if (row < M) {
+        const size_t off = (size_t)row * N;
+        float ss = 0.f;
+        Vec<__bf16> keep[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int i = c * 64 + lane;
+            if (i < nvec) {
+                Vec<__bf16> a;
+                a.load(x + off + i * 8);
+                if (d != nullptr) {
+                    Vec<__bf16> b;
+                    b.load(d + off + i * 8);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) a.v[j] = bf2f(f2bf(a.v[j] + b.v[j]));
+                    a.store(sum + off + i * 8);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ss += a.v[j] * a.v[j];
+                keep[c] = a;
+            }
+        }
+        ss = wave_sum(ss);
+        const float r = rsqrtf(ss / (float)N + eps);
+        if (lane == 0) rstd_out[row] = r;
+        const float sc = *scale;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int i = c * 64 + lane;
+            if (i < nvec) {
+                Vec<__bf16> g;
+                g.load(w + i * 8);
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    v[j] = bf2f(f2bf(keep[c].v[j] * r * g.v[j]));
+                    am = fmaxf(am, fabsf(v[j]));
+                }
+                *reinterpret_cast<uint2*>(y8 + off + i * 8) =
+                    uint2{pack4_fp8<0>(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc),
+                          pack4_fp8<0>(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc)};
+            }
+        }
+    }
+    am = block_max(am, red);
+    if (threadIdx.x == 0) atomicMax(amax_bits, __float_as_uint(am));
+}
+
+// fp8 [M][N] -> [N][M] (M, N multiples of 128) through the 128 x 128 tile helpers above
+__global__ void __launch_bounds__(256) transpose_fp8_t128_kernel(const uint8_t* __restrict__ a, uint8_t* __restrict__ at,
+                                                                 int M, int N) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[128 * T128_TS];
+    const int tid = threadIdx.x;
+    const int tiles_n = N / 128, ntiles = (M / 128) * tiles_n;
+    const int r = tid >> 1, hc = (tid & 1) * 64, kq = tid >> 3, ns = tid & 7;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int m0 = (t / tiles_n) * 128, n0 = (t % tiles_n) * 128;
+        const uint8_t* src = a + (long)(m0 + r) * N + n0 + hc;
+        unsigned q[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint4 u = *reinterpret_cast<const uint4*>(src + 16 * i);
+            q[4 * i] = u.x;
+            q[4 * i + 1] = u.y;
+            q[4 * i + 2] = u.z;
+            q[4 * i + 3] = u.w;
+        }
+        lds_barrier();  // the previous tile's transposed reads are done
+        t128_put(tile, q, r, hc);
+        lds_barrier();
+        t128_get_store(tile, kq, ns, at + (long)(n0 + 4 * kq) * M + m0 + 16 * ns, M);
+    }
+}
+
 // amax_cur [n] (float bits, zeroed here after use), hist [n][H], scale/inv [n]
 __global__ void __launch_bounds__(256) update_scales_kernel(unsigned* __restrict__ amax_cur, float* __restrict__ hist,
                                                             float* __restrict__ scale, float* __restrict__ inv_scale,
@@ -474,6 +564,22 @@ void launch_swiglu_cast_fp8_t(int mode, const void* gu, const void* dout, int M,
     else
         swiglu_cast_fp8_t_kernel<1, 1><<<grid, 256, 0, s>>>((const __bf16*)gu, (const __bf16*)dout, M, F, scale,
                                                             (uint8_t*)o8, (uint8_t*)o8t, amax_bits);
+}
+
+void launch_add_rmsnorm_cast_fp8_t(const void* x, const void* d, const void* w, void* sum, void* y8, void* y8t,
+                                   float* rstd, int M, int N, float eps, const float* scale, unsigned* amax_bits,
+                                   hipStream_t s) {
+    const int grid = (M + 3) / 4;
+    const int chunks = (N / 8 + 63) / 64;
+#define ARF(CC)                                                                                                  \
+    add_rmsnorm_fp8_kernel<CC><<<grid, 256, 0, s>>>((const __bf16*)x, (const __bf16*)d, (const __bf16*)w,        \
+                                                    (__bf16*)sum, (uint8_t*)y8, rstd, M, N, eps, scale, amax_bits)
+    if (chunks <= 1) ARF(1);
+    else if (chunks <= 2) ARF(2);
+    else ARF(4);
+#undef ARF
+    const int nt = (M / 128) * (N / 128);
+    transpose_fp8_t128_kernel<<<nt < 2048 ? nt : 2048, 256, 0, s>>>((const uint8_t*)y8, (uint8_t*)y8t, M, N);
 }
 
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,

@@ -62,7 +62,12 @@ void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8
 // SwiGLU + two-layout fp8 cast (fp8.hip): mode 0 a = silu(g) u -> a8 [M][F], a8t [F][M] (e4m3); mode 1 the gate
 // gradient from dout [M][F] -> dgu8 [M][2F], dgu8t [2F][M] (e5m2); gu = [g | u] [M][2F]; M, F multiples of 64
 void launch_swiglu_cast_fp8_t(int mode, const void* gu, const void* dout, int M, int F, const float* scale, void* o8,
-                              void* o8t, unsigned* amax_bits, hipStream_t s);  // bf16 W [N][K] -> e4m3 w8 [N][K] and w8t [K][N]
+                              void* o8t, unsigned* amax_bits, hipStream_t s);
+// residual add + RMSNorm written only as e4m3 in both layouts (fp8.hip): sum = x + d (bf16; d == nullptr: no add,
+// nothing stored), rstd, y8 [M][N] and y8t [N][M]; bf16, M and N multiples of 128, N <= 2048
+void launch_add_rmsnorm_cast_fp8_t(const void* x, const void* d, const void* w, void* sum, void* y8, void* y8t,
+                                   float* rstd, int M, int N, float eps, const float* scale, unsigned* amax_bits,
+                                   hipStream_t s);  // bf16 W [N][K] -> e4m3 w8 [N][K] and w8t [K][N]
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,
                           float margin, int fmt, hipStream_t s);
 

@@ -592,6 +592,35 @@ void swiglu_cast_fp8_t(const at::Tensor& gu, const c10::optional<at::Tensor>& do
                              reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
 }
 
+// residual add + RMSNorm with an e4m3 output in both layouts: returns (sum, rstd); sum is empty without d (the
+// caller's x is the norm input)
+std::tuple<at::Tensor, at::Tensor> add_rmsnorm_cast_fp8_t(const at::Tensor& x, const c10::optional<at::Tensor>& d,
+                                                          const at::Tensor& w, double eps, const at::Tensor& scale,
+                                                          at::Tensor y8, at::Tensor y8t, at::Tensor amax_bits) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.scalar_type() == at::kBFloat16, "add_rmsnorm_cast_fp8_t: bf16 x");
+    const int M = (int)x.size(0), N = (int)x.size(1);
+    TORCH_CHECK(M % 128 == 0 && N % 128 == 0 && N <= 2048, "add_rmsnorm_cast_fp8_t: M, N multiples of 128, N <= 2048");
+    const bool add = d.has_value() && d->defined();
+    if (add)
+        TORCH_CHECK(d->is_contiguous() && d->scalar_type() == at::kBFloat16 && d->sizes() == x.sizes() &&
+                        d->device() == x.device(), "add_rmsnorm_cast_fp8_t: d like x");
+    TORCH_CHECK(w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.numel() == N, "add_rmsnorm_cast_fp8_t: w [N]");
+    TORCH_CHECK(y8.is_contiguous() && y8t.is_contiguous() && y8.scalar_type() == at::kFloat8_e4m3fn &&
+                    y8t.scalar_type() == at::kFloat8_e4m3fn && y8.size(0) == M && y8.size(1) == N &&
+                    y8t.size(0) == N && y8t.size(1) == M, "add_rmsnorm_cast_fp8_t: e4m3 y8 [M, N] and y8t [N, M]");
+    TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1 && amax_bits.scalar_type() == at::kInt &&
+                    amax_bits.numel() == 1, "add_rmsnorm_cast_fp8_t: one fp32 scale and one int32 amax slot");
+    DevGuard g(x.device());
+    auto sum = add ? at::empty_like(x) : at::empty({0}, x.options());
+    auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+    launch_add_rmsnorm_cast_fp8_t(x.data_ptr(), add ? d->data_ptr() : nullptr, w.data_ptr(),
+                                  add ? sum.data_ptr() : nullptr, y8.data_ptr(), y8t.data_ptr(), rstd.data_ptr<float>(),
+                                  M, N, (float)eps, scale.data_ptr<float>(),
+                                  reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
+    return {sum, rstd};
+}
+
 void update_scales(at::Tensor amax_bits, at::Tensor hist, at::Tensor scale, at::Tensor inv_scale, int64_t pos,
                    double margin, int64_t fmt) {
     check_cuda(hist, "hist");
@@ -990,6 +1019,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("cast_fp8_t(Tensor w, Tensor scale, Tensor(a!) w8, Tensor(b!) w8t, Tensor(c!) amax_bits) -> ()");
     m.def("swiglu_cast_fp8_t(Tensor gu, Tensor? dout, Tensor scale, Tensor(a!) o8, Tensor(b!) o8t, "
           "Tensor(c!) amax_bits) -> ()");
+    m.def("add_rmsnorm_cast_fp8_t(Tensor x, Tensor? d, Tensor w, float eps, Tensor scale, Tensor(a!) y8, "
+          "Tensor(b!) y8t, Tensor(c!) amax_bits) -> (Tensor, Tensor)");
     m.def("update_scales(Tensor(a!) amax_bits, Tensor(b!) hist, Tensor(c!) scale, Tensor(d!) inv_scale, int pos, "
           "float margin, int fmt=0) -> ()");
     m.def("masked_sdpa(Tensor q, Tensor k, Tensor v, Tensor? mask, float scale) -> Tensor");
@@ -1036,6 +1067,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("transpose_bf16", &transpose_bf16);
     m.impl("cast_fp8_t", &cast_fp8_t);
     m.impl("swiglu_cast_fp8_t", &swiglu_cast_fp8_t);
+    m.impl("add_rmsnorm_cast_fp8_t", &add_rmsnorm_cast_fp8_t);
     m.impl("update_scales", &update_scales);
     m.impl("masked_sdpa", &masked_sdpa);
     m.impl("softmax_fwd", &softmax_fwd);

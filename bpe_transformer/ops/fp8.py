@@ -253,6 +253,25 @@ def swiglu_bwd_cast_t(state: Fp8State, da: Tensor, gu: Tensor, slot: int) -> tup
     return g8, g8t
 
 
+def norm_cast_ok(x: Tensor) -> bool:
+    """A block input the fused residual add + RMSNorm + two-layout e4m3 cast takes: bf16 [M, N] contiguous, M and N
+    multiples of 128, N <= 2048."""
+    return (x.dtype == torch.bfloat16 and x.dim() == 2 and x.is_contiguous() and x.shape[0] % 128 == 0
+            and x.shape[1] % 128 == 0 and x.shape[1] <= 2048)
+
+
+def add_rmsnorm_cast_t(state: Fp8State, x: Tensor, d: Tensor | None, w: Tensor, eps: float, slot: int):
+    """``s = x + d`` (``d`` None: ``s = x``) and ``RMSNorm(s) * w`` written only in fp8 (this state's e4m3) in both
+    layouts, slot ``slot``: returns ``(s, (y8 [M, N], y8t [N, M]), rstd)``.  One pass for the norm (no bf16 y) plus
+    an fp8 transpose, instead of ``add_rmsnorm_fwd`` and ``cast_t`` (csrc/fp8.hip add_rmsnorm_fp8_kernel)."""
+    M, N = x.shape
+    y8 = torch.empty(M, N, dtype=state.dtype, device=x.device)
+    y8t = torch.empty(N, M, dtype=state.dtype, device=x.device)
+    s, rstd = ops().add_rmsnorm_cast_fp8_t(x, None if d is None else d.contiguous(), w, eps,
+                                           state.scale[slot : slot + 1], y8, y8t, state.amax[slot : slot + 1])
+    return (x if d is None else s), (y8, y8t), rstd
+
+
 def quantize_reference(x: Tensor, scale: float, fmt: str = "e4m3") -> Tensor:
     """Oracle: saturating cast to e4m3fn / e5m2 and back (for tests)."""
     dt, _ = _FMT[fmt]

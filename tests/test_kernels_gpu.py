@@ -927,6 +927,38 @@ def test_swiglu_cast_fp8_transposed(gpu_device, M, F):
         assert abs(am - ram) <= 1e-2 * ram, (fwd, am, ram)
 
 
+@pytest.mark.parametrize("M,N,add", [(256, 256, True), (1024, 2048, True), (384, 768, False)])
+def test_add_rmsnorm_cast_fp8_transposed(gpu_device, M, N, add):
+    """Residual add + RMSNorm written only as e4m3 in both layouts (fp8.hip add_rmsnorm_fp8_kernel + the fp8
+    transpose) against add_rmsnorm_fwd / rmsnorm_fwd followed by the two-layout cast: same sum and rstd, fp8 bytes
+    equal up to rare one-ulp bf16 differences, same amax."""
+    from bpe_transformer.ops.fp8 import Fp8State, add_rmsnorm_cast_t
+    h = torch.ops.bpe_hip
+    torch.manual_seed(9)
+    x = torch.randn(M, N, device=gpu_device, dtype=torch.bfloat16)
+    d = torch.randn(M, N, device=gpu_device, dtype=torch.bfloat16) if add else None
+    w = (1 + 0.1 * torch.randn(N, device=gpu_device)).to(torch.bfloat16)
+    st = Fp8State(1, gpu_device)
+    st.scale.fill_(16.0)
+    s, (y8, y8t), rstd = add_rmsnorm_cast_t(st, x, d, w, 1e-5, 0)
+    if add:
+        s_ref, y_ref, r_ref = h.add_rmsnorm_fwd(x, d, w, 1e-5)
+        assert torch.equal(s, s_ref)
+    else:
+        y_ref, r_ref = h.rmsnorm_fwd(x, w, 1e-5)
+        assert s is x
+    assert rel(rstd, r_ref) < 1e-5
+    amax = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+    r8 = torch.empty(M, N, dtype=torch.float8_e4m3fn, device=gpu_device)
+    r8t = torch.empty(N, M, dtype=torch.float8_e4m3fn, device=gpu_device)
+    h.cast_fp8_t(y_ref, st.scale[:1], r8, r8t, amax)
+    assert torch.equal(y8t.view(torch.uint8), y8.view(torch.uint8).t().contiguous())
+    diff = (y8.view(torch.uint8) != r8.view(torch.uint8)).float().mean().item()
+    assert diff < 1e-3, diff
+    am, ram = st.amax.view(torch.float32).item(), amax.view(torch.float32).item()
+    assert abs(am - ram) <= 1e-2 * ram, (am, ram)
+
+
 def test_fp8_grads_weight_gradient(gpu_device):
     """ops.fp8.grads: one e5m2 cast of the output gradient serves dX = g W and dW = g^T X; both against the fp32
     products of the dequantised operands (the weight-gradient GEMM reduces over all tokens: M = N_out, K = T)."""

@@ -136,12 +136,14 @@ def test_fp8_close_to_bf16(gpu_device, dgrad, wgrad):
         assert e < (0.2 if dgrad else 0.15), (n, float(e))
 
 
-def test_fp8_swiglu_cast_fused_matches_two_pass(gpu_device, monkeypatch):
-    """fp8 weight-gradient path: the SwiGLU gate and its backward writing only fp8 in both layouts (one pass with the
-    cast) give the loss and gradients of the two-pass form (bf16 a / dgu, then the two-layout cast)."""
+@pytest.mark.parametrize("flag", ["_FP8_SWIGLU_CAST", "_FP8_NORM_CAST"])
+def test_fp8_swiglu_cast_fused_matches_two_pass(gpu_device, monkeypatch, flag):
+    """fp8 weight-gradient path: the SwiGLU gate and its backward (flag _FP8_SWIGLU_CAST), and the two RMSNorms
+    (_FP8_NORM_CAST), writing only fp8 in both layouts give the loss and gradients of the two-pass form (bf16
+    output, then the two-layout cast)."""
     from bpe_transformer.models import fused_block
 
-    assert fused_block._FP8_SWIGLU_CAST
+    assert getattr(fused_block, flag)
     _, a = _pair(gpu_device)
     a.enable_fp8(dgrad=True, wgrad=True)
     ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
@@ -153,7 +155,7 @@ def test_fp8_swiglu_cast_fused_matches_two_pass(gpu_device, monkeypatch):
     b = copy.deepcopy(a)
     la = a.loss(ids, tgt)
     la.backward()
-    monkeypatch.setattr(fused_block, "_FP8_SWIGLU_CAST", False)
+    monkeypatch.setattr(fused_block, flag, False)
     lb = b.loss(ids, tgt)
     lb.backward()
     assert abs(la.item() - lb.item()) < 1e-3, (la.item(), lb.item())
