@@ -6,7 +6,7 @@ forward (x = xr + xd: the previous block's residual and its not-yet-added FFN ou
 
     x, h1 = add_rmsnorm(xr, xd; ln1)  HIP (the residual add fused into the norm)
     qkv = h1 @ [Wq;Wk;Wv]^T, RoPE     our persistent ping-pong GEMM with RoPE on Q / K in its epilogue (D = 64
-                                      and 128; fp8: ops/fp8.py + the in-place rope_qk_)
+                                      and 128; fp8: the same in the hand fp8 kernel, gemm_fp8_rope)
     o = flash_attn(qkv)               HIP (csrc/flash_attn_fwd_v4.hip)
     g1 = o @ Wo^T                     hipBLASLt
     xm, h2 = add_rmsnorm(x, g1; ln2)  HIP
@@ -49,7 +49,7 @@ from torch import Tensor
 
 from ..ops._ext import ops as hip
 from ..ops.attention import prerotate_default
-from ..ops.fp8 import add_rmsnorm_cast_t, norm_cast_ok, swiglu_bwd_cast_t, swiglu_cast_ok, swiglu_fwd_cast_t
+from ..ops.fp8 import add_rmsnorm_cast_t, norm_cast_ok, rope_ok, swiglu_bwd_cast_t, swiglu_cast_ok, swiglu_fwd_cast_t
 from ..ops.gemm import accumulate_weight_grad
 
 
@@ -99,6 +99,8 @@ _FUSE_QKV_ROPE = True  # module flag (tests and A/B runs compare the unfused pat
 _FP8_SWIGLU_CAST = True
 # ... and the two RMSNorms write the QKV / W13 projections' inputs only as e4m3 in both layouts (module flag)
 _FP8_NORM_CAST = True
+# ... and the fp8 QKV projection runs on the hand fp8 kernel with RoPE in its epilogue instead of hipBLASLt + rope_qk_
+_FP8_QKV_ROPE = True
 
 
 def _fuse_qkv_rope(x: Tensor, w: Tensor, S: int) -> bool:
@@ -160,24 +162,28 @@ class FusedBlockFn(torch.autograd.Function):
             w8s = []
             xt8s = [] if wg else None
 
-            def mm(x, w, i, xq=None):
+            def mm(x, w, i, xq=None, rope=None):
                 if not keep:
-                    return st.matmul(x, w, s0 + i, s0 + 4 + i)
-                y, w8t, xt8 = st.matmul(x, w, s0 + i, s0 + 4 + i, keep_w8=True, keep_xt=wg, xq=xq)
+                    return st.matmul(x, w, s0 + i, s0 + 4 + i, rope=rope)
+                y, w8t, xt8 = st.matmul(x, w, s0 + i, s0 + 4 + i, keep_w8=True, keep_xt=wg, xq=xq, rope=rope)
                 w8s.append(w8t)
                 if wg:
                     xt8s.append(xt8)
                 return y
 
-            qkv = mm(h1, w_qkv, 0, xq=h1q)
         pre = use_rope and prerotate_default(D)
+        rope8 = False
+        if fp8 is not None:
+            xin = h1 if h1 is not None else h1q[0]
+            rope8 = pre and _FP8_QKV_ROPE and rope_ok(xin, w_qkv, S)
+            qkv = mm(h1, w_qkv, 0, xq=h1q, rope=(cos, sin, S, D, (H + Hkv) * D) if rope8 else None)
         if fp8 is None and pre and _fuse_qkv_rope(h1, w_qkv, S):
             # RoPE on Q / K in the projection's epilogue (saved rotated for the backward)
             qkv = hip().gemm_qkv_rope(h1, w_qkv, cos, sin, S, D, (H + Hkv) * D)
         else:
             if fp8 is None:
                 qkv = torch.matmul(h1, w_qkv.t())
-            if pre:  # RoPE once, in place on Q / K of the QKV activation (saved rotated for the backward)
+            if pre and not rope8:  # RoPE once, in place on Q / K of the QKV activation (saved rotated for the backward)
                 hip().rope_qk_(qkv, cos, sin, B, S, H, Hkv, D)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         # training: the forward kernel zeroes the backward's fp32 dQ accumulator in its epilogue (hidden under

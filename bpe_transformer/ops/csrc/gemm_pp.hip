@@ -998,6 +998,35 @@ void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, 
                                                   (__bf16*)C, ldc, 0.f, M, N, K / 2, 1, ep);
 }
 
+// qkv = (X8 . Wqkv8^T) * sa * sb (e4m3 x e4m3, K-major) with RoPE on output columns [0, rot_cols) in the epilogue:
+// the fp8 QKV projection and the in-place rope_qk_ pass in one kernel (the scaled product is rounded to bf16 and
+// rotated exactly as launch_gemm_fp8 + rope_qk_kernel do it)
+void launch_gemm_fp8_rope(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                          const float* sa, const float* sb, const float* cosT, const float* sinT, int S, int D,
+                          int rot_cols, hipStream_t s) {
+    Epi ep{};
+    ep.prio = prio_mode();
+    ep.sa = sa;
+    ep.sb = sb;
+    ep.cosT = cosT;
+    ep.sinT = sinT;
+    ep.S = S;
+    ep.D = D;
+    ep.rot_cols = rot_cols;
+    if (g_persist) {
+        static bool pattr = false;
+        auto* kp = &gemm_pp_persist_kernel<true, true, EPI_ROPE, 1, 1>;
+        if (!pattr) lds_attr(kp), pattr = true;
+        return launch_persist(kp, (M / BT) * (N / BT), s, (const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2,
+                              (__bf16*)C, ldc, 0.f, M, N, K / 2, ep);
+    }
+    static bool attr = false;
+    auto* k = &gemm_pp_kernel<true, true, false, 0, EPI_ROPE, 1, 1>;
+    if (!attr) lds_attr(k), attr = true;
+    k<<<(M / BT) * (N / BT), NT, LDS_BYTES, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, nullptr,
+                                                  (__bf16*)C, ldc, 0.f, M, N, K / 2, 1, ep);
+}
+
 // C = beta * C + (A8 . B8^T) * sa * sb, split over K into `splits` fp32 partials (slab [splits][M][N]) summed in a
 // fixed order by splitk_reduce: the fp8 weight-gradient GEMM (few output tiles, K = all tokens).  C bf16 or fp32.
 void launch_gemm_fp8_splitk(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,

@@ -190,5 +190,10 @@ void launch_gemm_fp8_splitk(const void* A, long lda, const void* B, long ldb, vo
 // qkv = X . Wqkv^T (bf16, both K-major) with RoPE applied to output columns [0, rot_cols) in the epilogue
 void launch_gemm_pp_rope(const void* X, long ldx, const void* W, long ldw, void* C, long ldc, int M, int N, int R,
                          const float* cosT, const float* sinT, int S, int D, int rot_cols, hipStream_t s);
+// the fp8 (e4m3 x e4m3) QKV projection with RoPE on output columns [0, rot_cols) in the epilogue (strides in bytes
+// for A / B)
+void launch_gemm_fp8_rope(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                          const float* sa, const float* sb, const float* cosT, const float* sinT, int S, int D,
+                          int rot_cols, hipStream_t s);
 // whether FaArgs::dkv_part (GQA fp32 dK / dV partials of the fused backward) must be set
 bool fa_dkv_partials_needed(int D, int rope = 0);

@@ -424,6 +424,36 @@ at::Tensor gemm_fp8(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor
     return y;
 }
 
+// qkv = (a8 @ b8^T) * sa * sb (e4m3 x e4m3) with RoPE on output columns [0, rot_cols) in the epilogue
+at::Tensor gemm_fp8_rope(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor& sa, const at::Tensor& sb,
+                         const at::Tensor& cos, const at::Tensor& sin, int64_t S, int64_t D, int64_t rot_cols) {
+    check_cuda(a8, "a8");
+    check_cuda(b8, "b8");
+    TORCH_CHECK(a8.scalar_type() == at::kFloat8_e4m3fn && b8.scalar_type() == at::kFloat8_e4m3fn,
+                "gemm_fp8_rope: e4m3 operands");
+    TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.stride(1) == 1 && b8.stride(1) == 1 && a8.size(1) == b8.size(1),
+                "gemm_fp8_rope: a8 [M, K] and b8 [N, K] row-major with a common K");
+    const int64_t M = a8.size(0), N = b8.size(0), K = a8.size(1);
+    TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0, "gemm_fp8_rope: M, N multiples of 256, K of 128");
+    TORCH_CHECK(a8.stride(0) % 16 == 0 && b8.stride(0) % 16 == 0 && (a8.stride(0) * 256) < (1L << 32),
+                "gemm_fp8_rope: 16-byte aligned rows");
+    TORCH_CHECK(sa.scalar_type() == at::kFloat && sb.scalar_type() == at::kFloat && sa.numel() >= 1 &&
+                    sb.numel() >= 1 && sa.device() == a8.device() && sb.device() == a8.device(),
+                "gemm_fp8_rope: sa / sb must be fp32 device scalars");
+    TORCH_CHECK(D % 8 == 0 && rot_cols % D == 0 && rot_cols <= N && S > 0 && M % S == 0,
+                "gemm_fp8_rope: D multiple of 8, rot_cols of D, rows a multiple of S");
+    TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+                    sin.is_contiguous() && cos.device() == a8.device() && sin.device() == a8.device() &&
+                    cos.numel() >= S * (D / 2) && sin.numel() >= S * (D / 2),
+                "gemm_fp8_rope: contiguous fp32 cos / sin tables of >= S rows on the GPU");
+    DevGuard g(a8.device());
+    auto y = at::empty({M, N}, a8.options().dtype(at::kBFloat16));
+    launch_gemm_fp8_rope(a8.data_ptr(), a8.stride(0), b8.data_ptr(), b8.stride(0), y.data_ptr(), y.stride(0), (int)M,
+                         (int)N, (int)K, sa.data_ptr<float>(), sb.data_ptr<float>(), cos.data_ptr<float>(),
+                         sin.data_ptr<float>(), (int)S, (int)D, (int)rot_cols, cur_stream());
+    return y;
+}
+
 // c = beta * c + (a8 @ b8^T) * sa * sb, split-K (`splits` fp32 partials, ordered reduce): the fp8 weight-gradient
 // GEMM, accumulating straight into the (bf16 or fp32) gradient buffer view c
 void gemm_fp8_acc(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor& sa, const at::Tensor& sb, at::Tensor c,
@@ -1012,6 +1042,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int S, int D, int rot_cols) -> Tensor");
     m.def("gemm_fp8_acc(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor(a!) c, float beta, int splits) -> ()");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb) -> Tensor");
+    m.def("gemm_fp8_rope(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor cos, Tensor sin, int S, int D, "
+          "int rot_cols) -> Tensor");
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
@@ -1063,6 +1095,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("gemm_qkv_rope", &gemm_qkv_rope);
     m.impl("gemm_fp8_acc", &gemm_fp8_acc);
     m.impl("gemm_fp8", &gemm_fp8);
+    m.impl("gemm_fp8_rope", &gemm_fp8_rope);
     m.impl("cast_fp8", &cast_fp8);
     m.impl("transpose_bf16", &transpose_bf16);
     m.impl("cast_fp8_t", &cast_fp8_t);

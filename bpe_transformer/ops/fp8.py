@@ -138,13 +138,14 @@ class Fp8State:
         return w8, w8t
 
     def matmul(self, x: Tensor | None, w: Tensor, x_slot: int, w_slot: int, keep_w8: bool = False,
-               keep_xt: bool = False, xq: tuple[Tensor, Tensor] | None = None):
+               keep_xt: bool = False, xq: tuple[Tensor, Tensor] | None = None, rope: tuple | None = None):
         """``x @ w.T`` in fp8 with bf16 output; x: [M, K] bf16, w: [N, K] bf16.  Without flags returns y.  With
         ``keep_w8`` / ``keep_xt`` returns ``(y, w8t, xt8)``: the quantised weight in the [K, N] layout the
         input-gradient GEMM needs and the quantised activation in the [K, M] layout of the weight-gradient GEMM
         (each written by the same cast pass as the forward operand; None when not asked for).  ``xq`` = (x8, xt8):
         x already quantised in both layouts by its producer in slot ``x_slot`` (``swiglu_fwd_cast_t``); x is then
-        not read."""
+        not read.  ``rope`` = (cos, sin, S, D, rot_cols): the QKV projection with RoPE on its first ``rot_cols`` output
+        columns in the hand fp8 kernel's epilogue (the caller checks :func:`rope_ok`)."""
         xt8 = None
         if xq is not None:
             x8, xt8 = xq
@@ -161,10 +162,22 @@ class Fp8State:
             w8 = self.cast(w, w_slot)
             if keep_w8:
                 w8t = w8.t().contiguous()
-        y = mm_fp8(x8, w8, self.inv_scale[x_slot], self.inv_scale[w_slot])
+        if rope is not None:
+            c, s, S, D, rot = rope
+            y = ops().gemm_fp8_rope(x8, w8, self.inv_scale[x_slot : x_slot + 1], self.inv_scale[w_slot : w_slot + 1],
+                                    c, s, S, D, rot)
+        else:
+            y = mm_fp8(x8, w8, self.inv_scale[x_slot], self.inv_scale[w_slot])
         if not keep_w8 and not keep_xt:
             return y
         return y, w8t, xt8
+
+
+def rope_ok(x: Tensor, w: Tensor, S: int) -> bool:
+    """Shapes the fp8 QKV GEMM with the RoPE epilogue takes: tokens and QKV width multiples of 256, d_model of 128,
+    whole sequences."""
+    return (x.shape[0] % 256 == 0 and w.shape[0] % 256 == 0 and x.shape[1] % 128 == 0 and x.shape[0] % S == 0
+            and _MODE != "lib")
 
 
 def _t_ok(t: Tensor) -> bool:

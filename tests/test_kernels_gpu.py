@@ -959,6 +959,26 @@ def test_add_rmsnorm_cast_fp8_transposed(gpu_device, M, N, add):
     assert abs(am - ram) <= 1e-2 * ram, (am, ram)
 
 
+@pytest.mark.parametrize("H,Hkv,D", [(8, 2, 64), (4, 2, 128)])
+def test_gemm_fp8_rope(gpu_device, H, Hkv, D):
+    """The fp8 QKV projection with RoPE in the hand kernel's epilogue equals the same kernel without it followed by
+    rope_qk_ in place (same bf16-rounded scaled products, same rotation arithmetic): bitwise."""
+    from bpe_transformer.ops import reference as R
+    h = torch.ops.bpe_hip
+    torch.manual_seed(4)
+    B, S, d = 2, 256, 256
+    N = (H + 2 * Hkv) * D
+    x8 = (torch.randn(B * S, d, device=gpu_device) * 4).to(torch.float8_e4m3fn)
+    w8 = (torch.randn(N, d, device=gpu_device) * 4).to(torch.float8_e4m3fn)
+    sa = torch.tensor([0.25], device=gpu_device)
+    sb = torch.tensor([0.125], device=gpu_device)
+    cos, sin = R.rope_tables(D, 1024, 10000.0, device=gpu_device)
+    ref = h.gemm_fp8(x8, w8, sa, sb)
+    h.rope_qk_(ref, cos, sin, B, S, H, Hkv, D)
+    out = h.gemm_fp8_rope(x8, w8, sa, sb, cos, sin, S, D, (H + Hkv) * D)
+    assert torch.equal(out, ref)
+
+
 def test_fp8_grads_weight_gradient(gpu_device):
     """ops.fp8.grads: one e5m2 cast of the output gradient serves dX = g W and dW = g^T X; both against the fp32
     products of the dequantised operands (the weight-gradient GEMM reduces over all tokens: M = N_out, K = T)."""

@@ -136,11 +136,12 @@ def test_fp8_close_to_bf16(gpu_device, dgrad, wgrad):
         assert e < (0.2 if dgrad else 0.15), (n, float(e))
 
 
-@pytest.mark.parametrize("flag", ["_FP8_SWIGLU_CAST", "_FP8_NORM_CAST"])
+@pytest.mark.parametrize("flag", ["_FP8_SWIGLU_CAST", "_FP8_NORM_CAST", "_FP8_QKV_ROPE"])
 def test_fp8_swiglu_cast_fused_matches_two_pass(gpu_device, monkeypatch, flag):
     """fp8 weight-gradient path: the SwiGLU gate and its backward (flag _FP8_SWIGLU_CAST), and the two RMSNorms
     (_FP8_NORM_CAST), writing only fp8 in both layouts give the loss and gradients of the two-pass form (bf16
-    output, then the two-layout cast)."""
+    output, then the two-layout cast); the QKV projection with RoPE in the hand fp8 kernel's epilogue
+    (_FP8_QKV_ROPE) those of the routed GEMM + rope_qk_."""
     from bpe_transformer.models import fused_block
 
     assert getattr(fused_block, flag)
