@@ -101,6 +101,8 @@ _FP8_SWIGLU_CAST = True
 _FP8_NORM_CAST = True
 # ... and the fp8 QKV projection runs on the hand fp8 kernel with RoPE in its epilogue instead of hipBLASLt + rope_qk_
 _FP8_QKV_ROPE = True
+# the RMSNorm weight gradients added into their flat gradient slots by the column-sum kernel (module flag for A/B)
+_NORM_DW_ACC = True
 
 
 def _fuse_qkv_rope(x: Tensor, w: Tensor, S: int) -> bool:
@@ -328,7 +330,9 @@ class FusedBlockFn(torch.autograd.Function):
             else:
                 dgu = hip().swiglu_bwd(da, gu)
         dh2 = proj(dgu, [w1, w3], 2, h2, gq=dgu_q)
-        dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dxm_out)
+        # with flat gradient slots the norm weights' gradients are added there by the column-sum kernel itself
+        nacc = main and _NORM_DW_ACC
+        dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dxm_out, ln2.main_grad if nacc else None)
         # ---- attention
         do = proj(dxm, [wo], 1, o)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
@@ -336,11 +340,12 @@ class FusedBlockFn(torch.autograd.Function):
                             ctx.dq_acc)
         ctx.dq_acc = None
         dh1 = proj(dqkv, [wq, wk, wv], 0, h1)
-        dx2, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm)
+        dx2, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm, ln1.main_grad if nacc else None)
         dxd = dx2 if ctx.has_xd else None
         if main:
-            ln2.main_grad.add_(dln2)
-            ln1.main_grad.add_(dln1)
+            if not nacc:
+                ln2.main_grad.add_(dln2)
+                ln1.main_grad.add_(dln1)
             _notify(ln2)
             _notify(ln1)
             return (dx2, dxd) + (None,) * 12

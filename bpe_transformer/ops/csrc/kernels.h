@@ -14,8 +14,9 @@ void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float*
 void launch_add_rmsnorm_fwd(int dtype, const void* x, const void* d, const void* w, void* sum, void* y, float* rstd,
                             int M, int N, float eps, hipStream_t s);
 int rmsnorm_bwd_grid(int M);
+// dw_mode 0: dw = the column sums (activation dtype); 1 / 2: dw += them (a bf16 / fp32 gradient slot)
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                        float* partial, void* dw, const void* dres, int M, int N, hipStream_t s);
+                        float* partial, void* dw, const void* dres, int M, int N, hipStream_t s, int dw_mode = 0);
 
 // activations.hip
 void launch_swiglu_fwd(int dtype, const void* gu, void* out, size_t M, int F, hipStream_t s);

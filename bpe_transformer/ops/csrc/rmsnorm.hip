@@ -426,8 +426,9 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_wide_kernel(const T* __restri
 
 // Column sum of the per-block partials [rows, N] -> dw [N]: 16 waves per block,
 // lane = column (coalesced 256-B rows), waves split the rows, fixed-order LDS
-// combine (deterministic).
-template <typename T>
+// combine (deterministic).  ACC: out += the sum (the parameter's flat gradient slot; bf16 or fp32), instead of a
+// fresh dw and a separate add kernel.
+template <typename T, bool ACC = false>
 __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ partial, T* __restrict__ out,
                                                       int rows, int N) {
     __shared__ float red[16][64];
@@ -444,6 +445,7 @@ __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ 
         float t = 0.f;
 #pragma unroll
         for (int i = 0; i < 16; ++i) t += red[i][lane];
+        if constexpr (ACC) t += ld1<T>(out + col);
         st1<T>(out + col, t);
     }
 }
@@ -530,16 +532,24 @@ int rmsnorm_bwd_grid(int M) {
     return g < BPE_RMS_BWD_GRID ? g : BPE_RMS_BWD_GRID;
 }
 
+// dw_mode: 0 = write dw (the activation dtype), 1 / 2 = accumulate into a bf16 / fp32 gradient slot at dw
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                        float* partial, void* dw, const void* dres, int M, int N, hipStream_t s) {
+                        float* partial, void* dw, const void* dres, int M, int N, hipStream_t s, int dw_mode) {
     const int grid = rmsnorm_bwd_grid(M);  // the partial buffer's rows (the kernel may use fewer)
-    if (dtype == DT_BF16) {
-        const int g = rms_bwd_dispatch<__bf16>((const __bf16*)dy, (const __bf16*)x, (const __bf16*)w, rstd,
-                                               (__bf16*)dx, partial, (const __bf16*)dres, grid, M, N, s);
-        colsum_kernel<__bf16><<<(N + 63) / 64, 1024, 0, s>>>(partial, (__bf16*)dw, g, N);
-    } else {
-        const int g = rms_bwd_dispatch<float>((const float*)dy, (const float*)x, (const float*)w, rstd, (float*)dx,
-                                              partial, (const float*)dres, grid, M, N, s);
-        colsum_kernel<float><<<(N + 63) / 64, 1024, 0, s>>>(partial, (float*)dw, g, N);
-    }
+    int g;
+    if (dtype == DT_BF16)
+        g = rms_bwd_dispatch<__bf16>((const __bf16*)dy, (const __bf16*)x, (const __bf16*)w, rstd, (__bf16*)dx,
+                                     partial, (const __bf16*)dres, grid, M, N, s);
+    else
+        g = rms_bwd_dispatch<float>((const float*)dy, (const float*)x, (const float*)w, rstd, (float*)dx, partial,
+                                    (const float*)dres, grid, M, N, s);
+    const int cb = (N + 63) / 64;
+    if (dw_mode == 1)
+        colsum_kernel<__bf16, true><<<cb, 1024, 0, s>>>(partial, (__bf16*)dw, g, N);
+    else if (dw_mode == 2)
+        colsum_kernel<float, true><<<cb, 1024, 0, s>>>(partial, (float*)dw, g, N);
+    else if (dtype == DT_BF16)
+        colsum_kernel<__bf16><<<cb, 1024, 0, s>>>(partial, (__bf16*)dw, g, N);
+    else
+        colsum_kernel<float><<<cb, 1024, 0, s>>>(partial, (float*)dw, g, N);
 }

@@ -78,8 +78,11 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Te
     return {y, rstd};
 }
 
+// dw_acc: add dw into this (bf16 or fp32, contiguous, N elements: a parameter's flat gradient slot) instead of
+// returning it (the second output is then empty)
 std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
-                                               const at::Tensor& rstd, const c10::optional<at::Tensor>& dres) {
+                                               const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
+                                               const c10::optional<at::Tensor>& dw_acc) {
     check_cuda(x, "x");
     auto dyc = dy.contiguous();
     const int N = (int)x.size(-1);
@@ -90,7 +93,15 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     TORCH_CHECK(dyc.scalar_type() == x.scalar_type(), "rmsnorm bwd: dtype mismatch");
     DevGuard g(x.device());
     auto dx = at::empty_like(x);
-    auto dw = at::empty_like(w);
+    const bool acc = dw_acc.has_value() && dw_acc->defined();
+    int mode = 0;
+    if (acc) {
+        TORCH_CHECK(dw_acc->is_contiguous() && dw_acc->numel() == N && dw_acc->device() == x.device() &&
+                        (dw_acc->scalar_type() == at::kBFloat16 || dw_acc->scalar_type() == at::kFloat),
+                    "rmsnorm bwd: dw_acc must be a contiguous bf16 / fp32 [N] tensor on the device");
+        mode = dw_acc->scalar_type() == at::kFloat ? 2 : 1;
+    }
+    auto dw = acc ? at::empty({0}, w.options()) : at::empty_like(w);
     const int grid = rmsnorm_bwd_grid(M);
     auto partial = at::empty({grid, N}, x.options().dtype(at::kFloat));
     const void* rp = nullptr;
@@ -101,7 +112,8 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
         rp = rc.data_ptr();
     }
     launch_rmsnorm_bwd(dt_code(x), dyc.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dx.data_ptr(),
-                       partial.data_ptr<float>(), dw.data_ptr(), rp, M, N, cur_stream());
+                       partial.data_ptr<float>(), acc ? dw_acc->data_ptr() : dw.data_ptr(), rp, M, N, cur_stream(),
+                       mode);
     return {dx, dw};
 }
 
@@ -1022,7 +1034,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("decode_attn_proj(Tensor part, Tensor w) -> Tensor");
     m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
     m.def("add_rmsnorm_fwd(Tensor x, Tensor d, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
-    m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
+    m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None, Tensor(a!)? dw_acc=None) -> "
+          "(Tensor, Tensor)");
     m.def("swiglu_fwd(Tensor gu) -> Tensor");
     m.def("swiglu_bwd(Tensor dout, Tensor gu) -> Tensor");
     m.def("act_fwd(Tensor x, int kind) -> Tensor");

@@ -67,6 +67,16 @@ def test_rmsnorm_bwd_residual_grad(gpu_device, M, N):
     wr = w.float().requires_grad_(True)
     R.rmsnorm(xr, wr, 1e-5).backward(dy.float())
     assert rel(dx0.float(), xr.grad) < 2e-2 and rel(dw0.float(), wr.grad) < 2e-2
+    # dw added straight into a gradient slot (bf16 / fp32): slot + the fp32 column sums, rounded once
+    for dt in (torch.bfloat16, torch.float32):
+        slot = torch.randn(N, device=gpu_device).to(dt)
+        before = slot.float().clone()
+        dx2, dw2 = h.rmsnorm_bwd(dy, x, w, rstd, dres, slot)
+        assert dw2.numel() == 0 and torch.equal(dx2, dx1)
+        if dt == torch.bfloat16:
+            assert rel(slot.float(), before + dw0.float()) < 1e-2
+        else:  # fp32: the column sums are added unrounded (dw0 is their bf16 rounding)
+            assert rel(slot - before, wr.grad) < 2e-2
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
