@@ -16,6 +16,7 @@ Shapes (2 layers each, so the tests stay short):
   with 4 accumulated micro-batches (fp32 gradient buffer);
 * ``llama``: d_model 2048, 32 query / 4 KV heads (GQA, the split backward's KV-head sweep), d_ff 5632 (the
   unfused SwiGLU forward past d_model 1024), batch x seq = 2 x 2048;
+* ``d128``: d_model 1024, 8 query / 2 KV heads of 128 (the split backward at D = 128), d_ff 2816, 2 x 2048;
 * ``llama`` fp8: our engine with fp8 projections (e4m3 forward, e5m2 x e4m3 input gradients) against our bf16
   engine, once through the per-shape routes and once with every fp8 GEMM forced onto the hand-written
   ``gemm_pp`` F8 kernel (``BPE_FP8_GEMM=hip``).
@@ -62,7 +63,9 @@ class Shape:
 # on and their trajectories part chaotically (matching to 6e-4 relative before the first spike), which says nothing
 # about the arithmetic.
 SHAPES = {"gpt2": Shape("gpt2shape", 4, 1024, 768, 12, 12, 2048, 1e-3),
-          "llama": Shape("llamashape", 2, 2048, 2048, 32, 4, 5632, 3e-4)}
+          "llama": Shape("llamashape", 2, 2048, 2048, 32, 4, 5632, 3e-4),
+          # head size 128 (the D = 128 split backward, RoPE in the QKV GEMM epilogue), GQA 8:2
+          "d128": Shape("headdim128", 2, 2048, 1024, 8, 2, 2816, 5e-4)}
 
 
 def _lr(it: int, c) -> float:
@@ -257,7 +260,7 @@ def _log(name, payload):
             json.dump(payload, f)
 
 
-@pytest.mark.parametrize("shape,accum", [("gpt2", 1), ("gpt2", 4), ("llama", 1)])
+@pytest.mark.parametrize("shape,accum", [("gpt2", 1), ("gpt2", 4), ("llama", 1), ("d128", 1)])
 def test_fused_engine_tracks_eager_pytorch(gpu_device, shape, accum):
     c = SHAPES[shape]
     lo, le = _run(c, accum, gpu_device)
