@@ -1,4 +1,4 @@
-"""The 4-wave persistent GEMM (gemm_w4.hip; w4 = the ring form, w4s = the 2-stage form) against the persistent ping-pong kernel (gemm_pp.hip) and hipBLASLt
+"""The 4-wave persistent GEMM (gemm_w4.hip; w4 = the ring form, w4s = the 2-stage form, w4g = the register-staged ring) against the persistent ping-pong kernel (gemm_pp.hip) and hipBLASLt
 (torch.matmul) on the one-pass GEMMs of a training step, interleaved over rounds in one process (guide §5.4 rule 24).
 
     python benchmarks/gemm_w4_bench.py [--model gpt2|llama] [--tokens 131072] [--rounds 5]
@@ -81,6 +81,7 @@ def main():
         arms = {
             "w4": w4(1),
             "w4s": w4(0),
+            "w4g": w4(2),
             "pp": lambda: h.gemm_pp(A, ak, B, bk, out, 0.0, 1),
             "lib": (lambda: torch.matmul(A, B.t(), out=out)) if bk else (lambda: torch.matmul(A, B, out=out)),
         }
@@ -105,6 +106,7 @@ def main():
             row[f"{k}_ms"] = round(m, 4)
             row[f"{k}_tflops"] = round(flops / m / 1e9, 1)
         row["w4_vs_w4s"] = round(row["w4s_ms"] / row["w4_ms"], 3)
+        row["w4g_vs_pp"] = round(row["pp_ms"] / row["w4g_ms"], 3)
         row["w4_vs_pp"] = round(row["pp_ms"] / row["w4_ms"], 3)
         row["w4_vs_lib"] = round(row["lib_ms"] / row["w4_ms"], 3)
         print(json.dumps(row), flush=True)

@@ -605,6 +605,198 @@ gemm_w4r_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict
 }
 
 }  // namespace ring
+
+// ---------------------------------------------------------------------------------------------------------
+// Register-staged ring (the "g" form): the same 4-stage ring and fragment reads, but the step data travels
+// global_load_dwordx4 -> VGPRs -> ds_write_b128 (the lane-linear image the DMA would write, so the same swizzled
+// sources and reads).  Why: in the DMA forms the computing wave pays each LDS-DMA piece's issue (~60 cycles among
+// bare MFMAs, guide; measured here: the 2-stage loop without its in-loop DMA runs 1.4-2x faster, with the DMA issued
+// but never waited for no faster than the real loop).  Step s is loaded in section s - 3 (8 loads into register
+// set S[s & 1]), written in section s - 2 into stage s % 4 (free: its previous step's fragments were read in section
+// s - 5 .. s - 6), read as F_s in section s - 1 and multiplied in section s.  The loads' waits are the compiler's
+// own counted vmcnt (plain loads).
+namespace ring {
+
+template <int EPI, bool BETA, bool AK, bool BKM>
+__device__ __forceinline__ void epilogue_g(const f32x4 (&acc)[8][8], char* stg, int wm, int wn, int l, int tid,
+                                           int i0, int j0, __bf16* C, long ldc, float beta, Set& X,
+                                           const char* __restrict__ st0, const ROff<AK>& fa_, const ROff<BKM>& fb_) {
+    asm volatile("" : "+v"(l), "+v"(tid));
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int ib = 2 * p + h;
+#pragma unroll
+            for (int jb = 0; jb < 8; ++jb) {
+                const int i = 32 * wm + 16 * h + (l & 15);
+                const int j = 128 * wn + 16 * jb + 4 * (l >> 4);
+                const f32x4 v = acc[ib][jb];
+                const u16x4 q = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+                *reinterpret_cast<u16x4*>(stg + i * 512 + (((j >> 3) ^ (i & 15)) << 4) + ((j & 7) << 1)) = q;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        bar();
+        const int c = tid & 31;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int i = 8 * q + (tid >> 5);
+            u16x8 v = *reinterpret_cast<const u16x8*>(stg + i * 512 + ((c ^ (i & 15)) << 4));
+            __bf16* cp = C + (long)(i0 + pass_row(p, i)) * ldc + j0 + c * 8;
+            if constexpr (BETA) {
+                const u16x8 o = *reinterpret_cast<const u16x8*>(cp);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + beta * bf2f(o[e]));
+            }
+            *reinterpret_cast<u16x8*>(cp) = v;
+        }
+        if (p == 3) rread<AK, BKM>(X, st0, wm, wn, fa_, fb_);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        bar();
+    }
+}
+
+template <bool KM>
+__device__ __forceinline__ void gload4(u16x8 (&r)[4], const __bf16* step0, const unsigned (&voff)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        r[j] = *reinterpret_cast<const u16x8*>(reinterpret_cast<const char*>(step0) + voff[j]);
+}
+
+__device__ __forceinline__ void gwrite4(const u16x8 (&r)[4], char* img, int w, int l) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<u16x8*>(img + (4 * w + j) * 1024 + 16 * l) = r[j];
+}
+
+struct Stg {
+    u16x8 a[4], b[4];
+};
+
+// section: MFMAs on X; reads of F_{j+1} (RD) into Y; loads of step j + 3 into `ld`; writes of `wr` (step j + 2) into
+// the stage wdst
+template <bool AK, bool BKM, bool FIRST, bool RD>
+__device__ __forceinline__ void gsection(f32x4 (&acc)[8][8], const Set& X, Set& Y, const char* __restrict__ rd_st,
+                                         char* __restrict__ wdst, Stg& ld, const Stg& wr, const __bf16* an,
+                                         const __bf16* bn, const unsigned (&oa)[4], const unsigned (&ob)[4], int w,
+                                         int wm, int wn, int l, const ROff<AK>& fa_, const ROff<BKM>& fb_) {
+    if constexpr (RD) rread<AK, BKM>(Y, rd_st, wm, wn, fa_, fb_);
+    gload4<AK>(ld.a, an, oa);
+    gload4<BKM>(ld.b, bn, ob);
+    gwrite4(wr.a, wdst, w, l);
+    gwrite4(wr.b, wdst + OP, w, l);
+    mma_set<FIRST>(acc, X);
+    constexpr int NRD = RD ? (AK ? 1 : 2) + (BKM ? 1 : 2) : 0;
+    // first half: reads, the 8 loads, MFMAs; second half: reads, the 8 writes (their loads a section old), MFMAs
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (NRD > 0) __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (NRD > 0) __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    }
+}
+
+template <bool AK, bool BKM, int EPI, bool BETA>
+__global__ void __launch_bounds__(NT, 1)
+gemm_w4g_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict__ B, long ldb,
+                __bf16* __restrict__ C, long ldc, float beta, int M, int N, int R) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w >> 1, wn = w & 1;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    const int tiles_n = N / BT;
+    const int ntiles = (M / BT) * tiles_n;
+    const int nk = R / SBK;  // >= 4, even
+
+    unsigned oa[4], ob[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = 64 * (4 * w + j) + l;
+        oa[j] = 2u * (unsigned)rsrc_off<AK>(e, (int)lda);
+        ob[j] = 2u * (unsigned)rsrc_off<BKM>(e, (int)ldb);
+    }
+    const ROff<AK> foa = roffsets<AK>(l);
+    const ROff<BKM> fob = roffsets<BKM>(l);
+    int t = wid;
+    int i0 = (t / tiles_n) * BT, j0 = (t % tiles_n) * BT;
+    // prologue: steps 0, 1 into stages 0, 1 (DMA), step 2 into register set S1 (as if loaded in section -1)
+    Stg S0, S1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        rdma4(rstep_ptr<AK>(A, lda, i0, q), oa, smem + q * STG, w);
+        rdma4(rstep_ptr<BKM>(B, ldb, j0, q), ob, smem + q * STG + OP, w);
+    }
+    gload4<AK>(S1.a, rstep_ptr<AK>(A, lda, i0, 2), oa);
+    gload4<BKM>(S1.b, rstep_ptr<BKM>(B, ldb, j0, 2), ob);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // the DMA of steps 0, 1 (older than the 8 register loads)
+    bar();
+    Set X, Y;
+    rread<AK, BKM>(X, smem, wm, wn, foa, fob);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    bar();
+    f32x4 acc[8][8];
+    int g = 0;
+    for (;;) {
+        const int tn = t + nwg;
+        const bool more = tn < ntiles;
+        const int i0n = more ? (tn / tiles_n) * BT : i0, j0n = more ? (tn % tiles_n) * BT : j0;
+        auto src = [&](int q, const __bf16*& an, const __bf16*& bn) {
+            an = rstep_ptr<AK>(A, lda, q < nk ? i0 : i0n, q < nk ? q : q - nk);
+            bn = rstep_ptr<BKM>(B, ldb, q < nk ? j0 : j0n, q < nk ? q : q - nk);
+        };
+        auto stage = [&](int j) { return smem + ((g + j) & 3) * STG; };
+        auto close = [&]() {  // the section's writes and reads retired, then the barrier
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            bar();
+        };
+        int j = 0;
+        for (; j + 2 < nk; j += 2) {
+            const __bf16 *an, *bn;
+            src(j + 3, an, bn);
+            if (j == 0)
+                gsection<AK, BKM, true, true>(acc, X, Y, stage(1), stage(2), S0, S1, an, bn, oa, ob, w, wm, wn, l, foa,
+                                              fob);
+            else
+                gsection<AK, BKM, false, true>(acc, X, Y, stage(j + 1), stage(j + 2), S0, S1, an, bn, oa, ob, w, wm,
+                                               wn, l, foa, fob);
+            close();
+            src(j + 4, an, bn);
+            gsection<AK, BKM, false, true>(acc, Y, X, stage(j + 2), stage(j + 3), S1, S0, an, bn, oa, ob, w, wm, wn,
+                                           l, foa, fob);
+            close();
+        }
+        {
+            const __bf16 *an, *bn;
+            src(j + 3, an, bn);
+            gsection<AK, BKM, false, true>(acc, X, Y, stage(j + 1), stage(j + 2), S0, S1, an, bn, oa, ob, w, wm, wn,
+                                           l, foa, fob);
+            close();
+            src(j + 4, an, bn);
+            gsection<AK, BKM, false, false>(acc, Y, X, stage(j + 2), stage(j + 3), S1, S0, an, bn, oa, ob, w, wm, wn,
+                                            l, foa, fob);
+        }
+        g += nk;
+        // the next tile's F_0 (stage g % 4, written two sections ago) is read inside the epilogue before its last
+        // barrier; S1 holds the next tile's step 2 (loaded in the last section)
+        epilogue_g<EPI, BETA, AK, BKM>(acc, smem + EOFF, wm, wn, l, tid, i0, j0, C, ldc, beta, X,
+                                       smem + (g & 3) * STG, foa, fob);
+        if (!more) break;
+        t = tn;
+        i0 = i0n;
+        j0 = j0n;
+    }
+}
+
+}  // namespace ring
 }  // namespace gw4
 }  // namespace bpe
 
@@ -676,6 +868,19 @@ static void launch_w4(const __bf16* a, long lda, const __bf16* b, long ldb, __bf
     const int ntiles = (M / BT) * (N / BT);
     const int cap = g_w4_grid_cap > 0 ? g_w4_grid_cap : num_cus_w4();
     const int grid = ntiles < cap ? ntiles : cap;
+    if (g_w4_ring == 2) {
+        static bool gattr = false;
+        if (!gattr) {
+            (void)hipFuncSetAttribute((const void*)&ring::gemm_w4g_kernel<AK, BKM, 0, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, ring::LDS);
+            (void)hipFuncSetAttribute((const void*)&ring::gemm_w4g_kernel<AK, BKM, 0, false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, ring::LDS);
+            gattr = true;
+        }
+        auto* k = beta != 0.f ? &ring::gemm_w4g_kernel<AK, BKM, 0, true> : &ring::gemm_w4g_kernel<AK, BKM, 0, false>;
+        k<<<grid, NT, ring::LDS, s>>>(a, lda, b, ldb, c, ldc, beta, M, N, R);
+        return;
+    }
     if (g_w4_ring) {
         auto* k = beta != 0.f ? &ring::gemm_w4r_kernel<AK, BKM, 0, true> : &ring::gemm_w4r_kernel<AK, BKM, 0, false>;
         k<<<grid, NT, ring::LDS, s>>>(a, lda, b, ldb, c, ldc, beta, M, N, R);

@@ -18,11 +18,13 @@ def rel(a: torch.Tensor, b: torch.Tensor) -> float:
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
 
 
-@pytest.fixture(params=[(0, 1), (1, 1), (3, 1), (0, 0), (3, 0)],
-                ids=["ring-percu", "ring-one_wg", "ring-three_wg", "2stage-percu", "2stage-three_wg"])
+@pytest.fixture(params=[(0, 1), (1, 1), (3, 1), (0, 0), (3, 0), (0, 2), (1, 2), (3, 2)],
+                ids=["ring-percu", "ring-one_wg", "ring-three_wg", "2stage-percu", "2stage-three_wg", "regring-percu",
+                     "regring-one_wg", "regring-three_wg"])
 def w4_cap(request, gpu_device):
     """(workgroup cap, form): cap 0 = one per CU (the production form), 1 = a single workgroup walks every tile, 3 =
-    tiles split unevenly over three; form 1 = the 4-stage ring of 32-deep steps, 0 = the 2-stage 64-deep form."""
+    tiles split unevenly over three; form 1 = the 4-stage ring of 32-deep steps, 0 = the 2-stage 64-deep form, 2 = the
+    ring with register-staged loads."""
     h = torch.ops.bpe_hip
     cap, ring = request.param
     prev = h.gw4_grid_config(cap)
@@ -88,7 +90,7 @@ def test_gemm_w4_bitwise_many_tiles(gpu_device):
     prev = h.gw4_grid_config(0)
     prev_ring = h.gw4_ring_config(1)
     try:
-        for cap, ring in ((0, 1), (1, 1), (0, 1), (0, 1), (0, 0), (1, 0)):
+        for cap, ring in ((0, 1), (1, 1), (0, 1), (0, 1), (0, 0), (1, 0), (0, 2), (1, 2), (0, 2)):
             h.gw4_grid_config(cap)
             h.gw4_ring_config(ring)
             c = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
