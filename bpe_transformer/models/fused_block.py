@@ -260,6 +260,12 @@ class FusedBlockFn(torch.autograd.Function):
         fp8 = ctx.meta[7]
         w8s = getattr(ctx, "w8s", None)
         xt8s = getattr(ctx, "xt8s", None)
+        if getattr(ctx, "consumed", False):
+            # the fp8 weight-gradient path frees its saved fp8 activations (and h1 / h2 / a were never kept), and the
+            # fused attention backward consumes dq_acc: a second backward through the same graph has no operands
+            raise RuntimeError("FusedBlockFn: backward ran twice through the same graph (retain_graph=True); the "
+                               "fused block frees its saved activations in its first backward")
+        ctx.consumed = xt8s is not None or getattr(ctx, "dq_acc", None) is not None
         ctx.xt8s = None
 
         def acc_dw(ps: list[Tensor], dw: Tensor) -> None:

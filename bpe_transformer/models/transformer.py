@@ -86,7 +86,8 @@ class TransformerLM(nn.Module):
     fp8_state = None
     fp8_grad_state = None
 
-    def enable_fp8(self, history: int = 16, margin: float = 1.0, dgrad: bool = True, wgrad: bool | None = None):
+    def enable_fp8(self, history: int = 16, margin: float = 1.0, dgrad: bool = True, wgrad: bool | None = None,
+                   grad_margin: float = 2.0):
         """Run the block projections in fp8 with delayed scaling: forward GEMMs e4m3 x e4m3; with ``dgrad`` the
         input-gradient GEMMs e5m2 (gradient) x e4m3 (weight) as well, and with ``wgrad`` (needs ``dgrad``) the
         weight-gradient GEMMs e5m2 (gradient^T) x e4m3 (activation^T) from the same gradient cast (None: the
@@ -94,14 +95,19 @@ class TransformerLM(nn.Module):
 
         Only the fused GPU block path quantises (``models/fused_block.py``); every block owns 8 e4m3 scale
         slots (4 activations + 4 weights) and 4 e5m2 slots (output gradients).  The training engine calls
-        ``update()`` on both states once per optimizer step.
+        ``update()`` on both states once per optimizer step.  ``margin`` / ``grad_margin``: headroom factors of
+        the e4m3 and e5m2 scales over their amax history (the gradient state uses the larger of the two).
         """
         from ..ops.fp8 import Fp8State
 
         dev = self.lm_head.weight.device
         L = len(self.layers)
         self.fp8_state = Fp8State(8 * L, dev, history=history, margin=margin)
-        self.fp8_grad_state = Fp8State(4 * L, dev, history=history, margin=margin, fmt="e5m2") if dgrad else None
+        # gradients: a 2x margin (e5m2 spans ~2^32, so the headroom costs nothing measurable); with margin 1 the
+        # Llama-shape parity run saturated its gradient casts by up to 2.9x at a loss-spike step, with 2 once by 1.5x
+        # (benchmarks/fp8_spike_probe.py, profiles/bench/fp8_spike_probe_margins_r5.log)
+        self.fp8_grad_state = (Fp8State(4 * L, dev, history=history, margin=max(margin, grad_margin), fmt="e5m2")
+                               if dgrad else None)
         for i, layer in enumerate(self.layers):
             layer.fp8 = (self.fp8_state, 8 * i, self.fp8_grad_state, 4 * i,
                          bool(dgrad and (FP8_WGRAD if wgrad is None else wgrad)))

@@ -1,8 +1,18 @@
-// FP8 (OCP e4m3fn) quantisation kernels for gfx950, delayed scaling.
+// FP8 (OCP e4m3fn / e5m2) quantisation kernels for gfx950, delayed scaling.
 //
 // The fp8 training path (BASELINE.json config "Llama-style 1.1B fp8 MFMA
-// path") runs the forward projections as fp8 x fp8 -> bf16 GEMMs on the
-// MFMA fp8 units through hipBLASLt, with per-tensor scales:
+// path") runs every block projection's GEMMs as fp8 x fp8 on the MFMA fp8
+// units, with per-tensor scales.  Which kernel runs them (ops/fp8.py):
+//   * the QKV forward: the hand-written f8f6f4 kernel (gemm_pp.hip, F8) with
+//     RoPE in its epilogue (gemm_fp8_rope);
+//   * every weight gradient dW = dY^T X (e5m2 x e4m3): the hand kernel's
+//     split-K form (gemm_fp8_acc, fp32 partials, ordered reduce into the
+//     gradient buffer);
+//   * the other forward and the input-gradient GEMMs: hipBLASLt
+//     (torch._scaled_mm) -- it leads the hand kernel by 11-17 % at the
+//     65 536-token shapes -- except the shapes routed to the hand kernel in
+//     ops/tuning/fp8_routes.json (two 16 384-token shapes).
+// The casts here produce their operands:
 //
 //   x8 = sat(x * s)            s = FMAX / (max over the amax history), FMAX = 448 (e4m3) / 57344 (e5m2)
 //   y  = (x8 / s_x) . (w8 / s_w)^T

@@ -87,16 +87,6 @@ bool gemm_pp_shape_ok(int M, int N, int R, int splits);
 void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                     float beta, int M, int N, int R, int splits, float* slab, int c_f32, hipStream_t s);
 
-// gemm_w4.hip (4-wave persistent GEMM, 256 x 256 x 64 tiles, one wave per SIMD with a 128 x 128 block; any layout,
-// bf16 C = beta * C + A B; M, N multiples of 256, R of 64 and >= 128)
-bool gemm_w4_shape_ok(int M, int N, int R);
-void launch_gemm_w4(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-                    float beta, int M, int N, int R, hipStream_t s);
-// gemm_w4: at most `cap` workgroups (tests: many tiles per workgroup); 0 = one per CU; -1 queries
-int gw4_grid_config(int cap);
-// gemm_w4: 1 = the ring form (32-deep K-steps, 4 LDS stages; default), 0 = the 2-stage form; -1 queries
-int gw4_ring_config(int mode);
-
 // fp8 x fp8 -> bf16 on the ping-pong kernel with v_mfma_scale_f32_16x16x128_f8f6f4: C = A8 B8^T * sa * sb,
 // A8 [M][K] (fmt_a 0 e4m3 / 1 e5m2), B8 [N][K] e4m3, both K-major; strides in bytes (A, B) / elements (C)
 void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,

@@ -411,31 +411,6 @@ void gemm_pp(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kma
                    c32 ? 1 : 0, cur_stream());
 }
 
-// 4-wave persistent GEMM (gemm_w4.hip): same operand convention as gemm_pp(); bf16 C only, no split-K.
-void gemm_w4(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor, at::Tensor C, double beta) {
-    check_cuda(C, "C");
-    TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
-                    C.scalar_type() == at::kBFloat16, "gemm_w4: bf16 operands and output required");
-    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
-                    C.stride(1) == 1, "gemm_w4: 2-D row-major operands required");
-    TORCH_CHECK(A.device() == C.device() && B.device() == C.device(), "gemm_w4: operands on different devices");
-    const int M = (int)C.size(0), N = (int)C.size(1);
-    const int R = (int)(a_kmajor ? A.size(1) : A.size(0));
-    TORCH_CHECK((a_kmajor ? A.size(0) : A.size(1)) == M, "gemm_w4: A / C shape mismatch");
-    TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == N && (b_kmajor ? B.size(1) : B.size(0)) == R,
-                "gemm_w4: B shape mismatch");
-    TORCH_CHECK(gemm_w4_shape_ok(M, N, R), "gemm_w4: M, N must be multiples of 256, R of 64 and >= 128");
-    TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 && C.stride(0) % 8 == 0, "gemm_w4: 16-byte row alignment");
-    TORCH_CHECK((A.stride(0) * 256) < (1L << 31) && (B.stride(0) * 256) < (1L << 31),
-                "gemm_w4: leading dimension too large for 32-bit tile offsets");
-    DevGuard g(C.device());
-    launch_gemm_w4(a_kmajor, b_kmajor, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(),
-                   C.stride(0), (float)beta, M, N, R, cur_stream());
-}
-
-int64_t gw4_grid_config_op(int64_t cap) { return gw4_grid_config((int)cap); }
-int64_t gw4_ring_config_op(int64_t mode) { return gw4_ring_config((int)mode); }
-
 // y = (a8 @ b8^T) * sa * sb in bf16: a8 [M, K] e4m3 / e5m2, b8 [N, K] e4m3 (both K-major), sa / sb device fp32
 // scalars (the per-tensor inverse scales); the hand-written fp8 MFMA ping-pong kernel (gemm_pp.hip)
 at::Tensor gemm_fp8(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor& sa, const at::Tensor& sb) {
@@ -1108,9 +1083,6 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("fa_stamps(int n) -> Tensor", &fa_stamps_op);
     m.def("gpp_stamps(int n) -> Tensor", &gpp_stamps_op);
     m.def("gpp_persist_config(int mode=-1) -> int", &gpp_persist_config_op);
-    m.def("gemm_w4(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta=0.0) -> ()");
-    m.def("gw4_grid_config(int cap=-1) -> int", &gw4_grid_config_op);
-    m.def("gw4_ring_config(int mode=-1) -> int", &gw4_ring_config_op);
     m.def("fa_fwd_config(int ver=0) -> int", &fa_fwd_config_op);
 }
 
@@ -1131,7 +1103,6 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("scale_", &scale_);
     m.impl("gemm", &gemm);
     m.impl("gemm_pp", &gemm_pp);
-    m.impl("gemm_w4", &gemm_w4);
     m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
     m.impl("gemm_swiglu_fwd", &gemm_swiglu_fwd);
     m.impl("gemm_qkv_rope", &gemm_qkv_rope);

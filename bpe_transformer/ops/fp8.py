@@ -2,14 +2,21 @@
 
 Recipe (BASELINE.json "Llama-style 1.1B fp8 MFMA path"):
   * the four projection GEMMs of every block run as fp8 x fp8 -> bf16 on the
-    MFMA fp8 units: the hand-written ping-pong kernel with
-    ``v_mfma_scale_f32_16x16x128_f8f6f4`` (``csrc/gemm_pp.hip``, F8 variants;
-    per-tensor inverse scales applied in its epilogue, read from the device)
-    for the shapes in ``ops/tuning/fp8_routes.json``, where it measured faster
-    than hipBLASLt, and hipBLASLt's ``torch._scaled_mm`` for the rest
-    (``BPE_FP8_GEMM=hip`` / ``lib`` force one path).  At the Llama-1.1B shapes
-    (``benchmarks/gemm_fp8_bench.py``, ``profiles/bench/gemm_fp8_pinned_vs_lib.log``)
-    ours runs 1.5-2.8 PF/s, the library 1.7-3.4 PF/s, bf16 1.1-1.6 PF/s;
+    MFMA fp8 units.  Which kernel serves which GEMM at the bench config
+    (Llama-1.1B, s4096 B16 = 65 536 tokens):
+      - the QKV forward: the hand-written ping-pong kernel with
+        ``v_mfma_scale_f32_16x16x128_f8f6f4`` (``csrc/gemm_pp.hip``, F8; per-tensor
+        inverse scales applied in its epilogue, read from the device) with RoPE
+        in its epilogue (``gemm_fp8_rope``, :func:`rope_ok`);
+      - every weight gradient: the hand kernel's split-K form
+        (:func:`wgrad_acc`, ``gemm_fp8_acc``), 2.29-2.64 vs the library's
+        1.65-2.09 PF/s (``profiles/bench/fp8_wgrad_r4.log``);
+      - the O / W13 / W2 forward and every input gradient: hipBLASLt's
+        ``torch._scaled_mm``, which leads the hand kernel by 11-17 % at these
+        shapes (``profiles/bench/gemm_fp8_persistent_vs_lib_r4.log``).  The route
+        table ``ops/tuning/fp8_routes.json`` sends only its listed shapes (two
+        16 384-token ones) to the hand kernel; ``BPE_FP8_GEMM=hip`` / ``lib`` force
+        one path for all of :func:`mm_fp8`;
   * activations and weights are quantised by ``csrc/fp8.hip`` with a scale
     derived from an amax history (delayed scaling, powers of two); the cast
     pass also records this step's amax, and one launch per step refreshes all
@@ -102,6 +109,9 @@ class Fp8State:
         self.inv_scale = torch.ones(n_slots, dtype=torch.float32, device=device)
         self.margin = margin
         self.pos = 0
+        # diagnostic (benchmarks/fp8_spike_probe.py): when a list, update() appends a [2, n] device tensor per step --
+        # the step's amax per slot and the scale its casts used.  amax * scale / FMAX > 1 means values saturated.
+        self.trace: list | None = None
 
     def cast(self, x: Tensor, slot: int) -> Tensor:
         out = torch.empty(x.shape, dtype=self.dtype, device=x.device)
@@ -110,6 +120,8 @@ class Fp8State:
 
     def update(self) -> None:
         """Fold this step's amaxes into the history and recompute every scale (one launch)."""
+        if self.trace is not None:
+            self.trace.append(torch.stack([self.amax.view(torch.float32).clone(), self.scale.clone()]))
         ops().update_scales(self.amax, self.hist, self.scale, self.inv_scale, self.pos, self.margin, self.fmt_code)
         self.pos += 1
 

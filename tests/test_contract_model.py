@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import math
 
+import pytest
 import torch
 
 from .adapters import (
@@ -39,6 +40,15 @@ def test_4d_scaled_dot_product_attention(numpy_snapshot, q, k, v, mask):
     q4, k4, v4 = (x.reshape(2, 2, *x.shape[1:]) for x in (q, k, v))
     m4 = mask.reshape(2, 2, *mask.shape[1:])
     numpy_snapshot.assert_match(run_scaled_dot_product_attention(q4, k4, v4, m4), atol=1e-6)
+
+
+@pytest.mark.parametrize("mdtype", [torch.int64, torch.float32, torch.uint8])
+def test_scaled_dot_product_attention_nonbool_mask(q, k, v, mask, mdtype):
+    """A 0/1 int / float mask means the same as the boolean one (nonzero = attend) on every path; the HIP kernel
+    treats it so too (``ops/attention.py``)."""
+    ref = run_scaled_dot_product_attention(q, k, v, mask)
+    got = run_scaled_dot_product_attention(q, k, v, mask.to(mdtype))
+    assert torch.equal(got, ref)
 
 
 def test_rope(numpy_snapshot, in_embeddings, d_model, theta, n_queries, pos_ids):

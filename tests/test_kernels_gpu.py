@@ -970,7 +970,7 @@ def test_add_rmsnorm_cast_fp8_transposed(gpu_device, M, N, add):
 
 
 @pytest.mark.parametrize("H,Hkv,D", [(8, 2, 64), (4, 2, 128)])
-def test_gemm_fp8_rope(gpu_device, H, Hkv, D):
+def test_gemm_fp8_rope(gpu_device, gpp_mode, H, Hkv, D):
     """The fp8 QKV projection with RoPE in the hand kernel's epilogue equals the same kernel without it followed by
     rope_qk_ in place (same bf16-rounded scaled products, same rotation arithmetic): bitwise."""
     from bpe_transformer.ops import reference as R
@@ -1077,6 +1077,50 @@ def test_gemm_fp8_exact(gpu_device, gpp_mode, M, N, K, fmt_a):
     assert torch.equal(y.cpu(), ref)
 
 
+def test_gemm_fp8_persistent_bitwise_many_tiles(gpu_device):
+    """The fp8 kernels at production tile counts (640 output tiles: every persistent workgroup walks 2-3 of them, the
+    3-workgroup form ~213), on small-integer operands whose products are exact: the one-tile, persistent and
+    3-workgroup forms of gemm_fp8 and gemm_fp8_rope, and the split-K gemm_fp8_acc (160 tiles x 4 splits), must all
+    equal the exact reference bitwise, on repeated runs -- a race in the seam prefetch or the store overlap (the
+    bf16 persistent kernel had one, docs/performance.md) shows as wrong tiles."""
+    from bpe_transformer.ops import reference as R
+    h = torch.ops.bpe_hip
+    g = torch.Generator(device="cpu").manual_seed(17)
+    M, N, K = 16384, 2560, 1024  # 64 x 10 = 640 tiles, 8 fp8 K-tiles
+    a = torch.randint(-4, 5, (M, K), generator=g).float()
+    b = torch.randint(-4, 5, (N, K), generator=g).float()
+    a8 = a.to(torch.float8_e4m3fn).to(gpu_device)
+    b8 = b.to(torch.float8_e4m3fn).to(gpu_device)
+    sa = torch.tensor([0.25], device=gpu_device)
+    sb = torch.tensor([2.0], device=gpu_device)
+    exact = (a.to(gpu_device) @ b.to(gpu_device).t()) * 0.5  # |sum| <= 16 K: exact in fp32
+    ref = exact.to(torch.bfloat16)
+    S, D, H, Hkv = 1024, 128, 12, 4  # N = (12 + 2 * 4) * 128 = 2560; RoPE on Q / K, V untouched
+    cos, sin = R.rope_tables(D, S, 10000.0, device=gpu_device)
+    ref_rope = ref.clone()
+    h.rope_qk_(ref_rope, cos, sin, M // S, S, H, Hkv, D)
+    prev = h.gpp_persist_config(0)
+    try:
+        for mode in (0, 1, 3, 1, 1):
+            h.gpp_persist_config(mode)
+            assert torch.equal(h.gemm_fp8(a8, b8, sa, sb), ref), mode
+            assert torch.equal(h.gemm_fp8_rope(a8, b8, sa, sb, cos, sin, S, D, (H + Hkv) * D), ref_rope), mode
+    finally:
+        h.gpp_persist_config(prev)
+    # split-K weight-gradient form: 16 x 10 output tiles x 4 splits over K = 16384 tokens, fp32 C, beta = 1
+    Mw, Kw = 4096, 16384
+    aw = torch.randint(-2, 3, (Mw, Kw), generator=g).float()
+    bw = torch.randint(-2, 3, (N, Kw), generator=g).float()
+    aw8 = aw.to(torch.float8_e5m2).to(gpu_device)
+    bw8 = bw.to(torch.float8_e4m3fn).to(gpu_device)
+    c0 = torch.randint(-8, 9, (Mw, N), generator=g).float().to(gpu_device)
+    refw = c0 + (aw.to(gpu_device) @ bw.to(gpu_device).t()) * 0.5  # |sum| <= 4 * 16384: exact in fp32
+    for _ in range(3):
+        c = c0.clone()
+        h.gemm_fp8_acc(aw8, bw8, sa, sb, c, 1.0, 4)
+        assert torch.equal(c, refw)
+
+
 def test_gemm_fp8_random_vs_dequantised(gpu_device, gpp_mode):
     """Random e4m3 operands at a Llama projection shape against the fp32 product of the dequantised operands."""
     torch.manual_seed(7)
@@ -1171,6 +1215,19 @@ def test_sdpa_contract_snapshots_on_gpu(gpu_device, q, k, v, mask):
     q4, k4, v4, m4 = (t.reshape(2, 2, *t.shape[1:]) for t in (qg, kg, vg, mg))
     out4 = run_scaled_dot_product_attention(q4, k4, v4, m4)
     NumpySnapshot("test_4d_scaled_dot_product_attention", False).assert_match(out4, atol=1e-6)
+
+
+def test_masked_sdpa_many_batch_heads_falls_back(gpu_device):
+    """More batch-heads than the kernel's grid.y (65535) take the oracle path instead of failing; an int mask counts
+    nonzero as attend there too."""
+    torch.manual_seed(3)
+    Q = torch.randn(65536 + 7, 2, 8, device=gpu_device)
+    K = torch.randn(65536 + 7, 3, 8, device=gpu_device)
+    V = torch.randn(65536 + 7, 3, 8, device=gpu_device)
+    m = torch.tensor([[1, 1, 0], [1, 0, 1]], device=gpu_device)
+    got = ops.scaled_dot_product_attention(Q, K, V, m)
+    ref = R.scaled_dot_product_attention(Q.float(), K.float(), V.float(), m.bool())
+    assert got.shape == ref.shape and rel(got, ref) < 1e-5
 
 
 @pytest.mark.parametrize("lead,Sq,Sk,D,Dv", [((3,), 7, 5, 16, 16), ((2, 3), 70, 130, 64, 32), ((1,), 129, 64, 128, 128),

@@ -181,6 +181,19 @@ def test_fp8_engine_reduces_loss(gpu_device):
     assert model.fp8_state.pos == 31
 
 
+def test_fp8_second_backward_raises(gpu_device):
+    """The fp8 weight-gradient path frees the block's saved fp8 activations in its backward: a second backward through
+    the same graph (retain_graph=True) raises a clear error instead of failing inside a GEMM on missing operands."""
+    torch.manual_seed(0)
+    model = TransformerLM(1000, 128, 256, 2, 4, 512, device=gpu_device, dtype=torch.bfloat16)
+    model.enable_fp8(wgrad=True)
+    x = torch.randint(0, 1000, (4, 128), device=gpu_device)
+    loss = model.loss(x, torch.roll(x, -1, 1))
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="backward ran twice"):
+        loss.backward()
+
+
 @pytest.mark.parametrize("heads", [4, 2])
 def test_forward_and_backward_are_bitwise_deterministic(gpu_device, heads):
     """Every kernel of the step is run-to-run deterministic at D = 64 and D = 128: the forward (attention, norms, CE,
