@@ -23,12 +23,13 @@ def main():
     ap.add_argument("--no-rope", action="store_true", help="plain attention (isolates the fused-RoPE cost)")
     ap.add_argument("--no-causal", action="store_true", help="full (non-causal) attention")
     ap.add_argument("--bwd-ab", action="store_true",
-                    help="interleaved same-process A/B of the backward forms (ops.fa_bwd_config): fused (atomics) "
-                         "and split")
+                    help="interleaved same-process A/B of the backward forms (ops.fa_bwd_config / fa_dq_config): "
+                         "fused (atomics), split, split with the 16-queries-per-wave dQ kernel")
     ap.add_argument("--fwd-ab", action="store_true",
                     help="interleaved same-process A/B of the D = 64 forward versions 2 (fa_fwd_kernel) and 8 "
                          "(flash_attn_fwd_v4.hip) (ops.fa_fwd_config)")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--dq-form", type=int, default=-1, help="ops.fa_dq_config form for the run (-1: the default)")
     ap.add_argument("--fwd-versions", type=int, nargs="+", default=[2, 8])
     ap.add_argument("--bwd-arms", nargs="+", default=None, help="subset of the --bwd-ab arms (names below)")
     ap.add_argument("--mode", choices=["block", "fused"], default="block",
@@ -43,6 +44,8 @@ def main():
     from bpe_transformer.ops._ext import ops as _ops
 
     hip = _ops()
+    if a.dq_form >= 0:
+        hip.fa_dq_config(a.dq_form)
     scale = 1.0 / D ** 0.5
     rope = cos is not None
     causal = not a.no_causal
@@ -87,15 +90,18 @@ def main():
         if not a.bwd_ab:
             return
     if a.bwd_ab:
-        arms = {"fused": 1, "split": 0}
+        # (backward form, dQ form): split with the 32- or 16-queries-per-wave dQ kernel (ops.fa_dq_config)
+        arms = {"fused": (1, 0), "split": (0, 0), "split_dq16": (0, 1)}
         if a.bwd_arms:
             arms = {n: arms[n] for n in a.bwd_arms}
         prev = hip.fa_bwd_config(-1)
+        prev_dq = hip.fa_dq_config(-1)
         times = {k: [] for k in arms}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for _ in range(a.rounds):
-            for name, cfg in arms.items():
+            for name, (cfg, dqf) in arms.items():
                 hip.fa_bwd_config(cfg)
+                hip.fa_dq_config(dqf)
                 bwd(o, lse)
                 ev[0].record()
                 for _ in range(a.iters):
@@ -104,6 +110,7 @@ def main():
                 torch.cuda.synchronize()
                 times[name].append(ev[0].elapsed_time(ev[1]) / a.iters)
         hip.fa_bwd_config(prev)
+        hip.fa_dq_config(prev_dq)
         for name, t in times.items():
             t = sorted(t)
             print(json.dumps({"shape": [B, S, H, Hkv, D], "arm": name, "bwd_ms_median": round(t[len(t) // 2], 4),

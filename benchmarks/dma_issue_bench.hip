@@ -30,7 +30,8 @@ constexpr int ITERS = 512;
 template <int V, int P>
 __global__ void __launch_bounds__(256, 1) probe(const char* __restrict__ src, unsigned long long span, float* out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    // w wave-uniform for the compiler too: a buffer resource built from a VGPR value compiles to a waterfall loop
+    const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     f32x4 acc[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -86,6 +86,39 @@ def same_weights(c, steps, dev, margin=1.0):
     return out
 
 
+def cross(c, steps, dev):
+    """The other half of the split: train in fp8 and, before step s, evaluate batch s on the fp8-trained weights in
+    fp8 and with fp8 switched off (bf16).  A spike that the bf16 evaluation of the same weights shows too is in the
+    weights (the fp8 trajectory), not in the fp8 forward's rounding."""
+    from bpe_transformer.ops import gemm
+
+    gemm._AUTOTUNE = False
+    gemm._route.clear()
+    ids, vocab = P._tokens()
+    model = P._ours(vocab, c, dev)
+    model.enable_fp8()
+    eng = P._engine(model, 1, c)
+    data = P._batches(ids, P.STEPS, c.B, c.S, dev)
+    out = {}
+    for it in range(max(steps) + 1):
+        if it in steps:
+            with torch.no_grad():
+                x, y = data[it]
+                saved = [layer.fp8 for layer in model.layers]
+                for layer in model.layers:
+                    layer.fp8 = None
+                lb = float(model.loss(x, y))
+                for layer, f in zip(model.layers, saved):
+                    layer.fp8 = f
+            out[it] = {"bf16_eval_of_fp8_weights": lb}
+            print(json.dumps({"cross_step": it, "bf16_eval_of_fp8_weights": round(lb, 4)}), flush=True)
+        loss = eng.train_step([data[it]], lr=P._lr(it, c))
+        if it in steps:
+            out[it]["fp8_train_loss"] = float(loss)
+            print(json.dumps({"cross_step": it, "fp8_train_loss": round(float(loss), 4)}), flush=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--margins", default="1,2")
@@ -93,9 +126,16 @@ def main():
     ap.add_argument("--bf16-wgrad", action="store_true")
     ap.add_argument("--out", default="gpurun_out/fp8_spike_probe.json")
     ap.add_argument("--same-weights", default="", help="steps (comma list): the same-weights evaluation only")
+    ap.add_argument("--cross", default="", help="steps (comma list): bf16 evaluation of the fp8-trained weights")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     c = P.SHAPES["llama"]
+    if a.cross:
+        res = cross(c, [int(x) for x in a.cross.split(",")], dev)
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f)
+        return
     if a.same_weights:
         res = same_weights(c, [int(x) for x in a.same_weights.split(",")], dev)
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

@@ -1,0 +1,266 @@
+// Flash attention backward, dQ kernel with 16 queries per wave (D = 64), gfx950 (MI355X).
+//
+// Parity target: the dQ of the split backward (flash_attn_bwd_split.hip fa_bwd_dq_kernel; reference contracts
+// K7/K10, `tests/adapters.py:92-184`); checked against autograd of the fp32 oracle and against the 32-row kernel
+// (tests/test_kernels_gpu.py).
+//
+// Why: the 32-row split dQ kernel runs at mfma_util 0.29 (profiles/attention_pmc.md): each wave's 32-key step is a
+// dependency chain (S / dP MFMAs -> exp -> dS -> dQ MFMAs) and two waves per SIMD cannot cover it.  This form
+// computes the same five products with v_mfma_f32_16x16x32_bf16 on 16 queries per wave, so a wave holds half the
+// registers (<= 128: four waves per SIMD, two 512-thread workgroups per CU) and each SIMD has twice as many
+// independent chains to interleave.  Per 32-key step and wave: S^T and dP^T as two 16-key blocks each
+// (4 + 4 MFMAs over d = 64), dQ^T += K^T dS^T over 4 d-tiles (4 MFMAs); the same VALU per score as before.
+//
+//   S^T [key][query]  = K . (cQ)^T - lse     A = K rows (ds_read_b128), B = the pinned c*Q (query on the lane)
+//   dP^T              = V . dO^T - delta     A = V rows,                B = the pinned dO
+//   dS^T = exp2(S^T) * dP^T                  accumulator rows = keys 16 kb + 4 g + i (g = lane >> 4)
+//   dQ^T [d][query]  += K^T . dS^T           A = K^T (two ds_read_b64_tr_b16), B = dS^T packed from the two
+//                                            accumulators in the permuted key order 16 (j >> 2) + 4 g + (j & 3)
+//
+// LDS image: 128-byte rows, chunk c of row r at c ^ (r & 6).  Both reads are conflict-free on it (a brute-force
+// search over per-row XORs, docs/performance.md): the 16-lane groups of the row reads cover rows 16 m + 0..15 at
+// chunks 4 ks + g, the transposed reads 4-row blocks 8 rows apart x one 32-byte column pair.  (The 32-row kernels'
+// image, fa_common.h swz<128>, leaves both 2-way conflicted for these fragments.)  K / V tiles of 128 keys are
+// DMA'd through buffer resources, one wave-instruction per wave and 64-row image.
+#include "fa_common.h"
+#include "kernels.h"
+
+namespace bpe {
+namespace fa {
+namespace dq16 {
+
+constexpr int NW = 8;            // waves per workgroup, 16 queries each
+constexpr int QB = 16 * NW;      // queries per workgroup
+constexpr int KT = 128;          // keys per K / V tile (two 64-row images)
+constexpr int TILE = 64 * 128;   // one 64-row image of 128-byte rows
+constexpr int BUF = 2 * TILE;    // one tile
+
+__device__ __forceinline__ int sw(int row, int c) { return row * 128 + ((c ^ (row & 6)) << 4); }
+// byte offset of the 8-byte granule at (row, col) (transposed reads)
+__device__ __forceinline__ int sw_tr(int row, int col) { return sw(row, col >> 3) + ((col & 7) << 1); }
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// lane offset (bytes, inside a 64-row tile of a row-major tensor of row stride ld) of the source chunk this lane's
+// DMA slot holds: wave w's one wave-instruction per image fills physical chunks 64 w + lane
+__device__ __forceinline__ unsigned dma_lane_off(long ld, int w, int l) {
+    const int e = 64 * w + l, r = e >> 3, pc = e & 7;
+    return (unsigned)((r * ld + ((pc ^ (r & 6)) << 3)) * 2);
+}
+
+__device__ __forceinline__ void dma_image(const __bf16* base, int nbytes, unsigned voff, int r0, long ld, char* img,
+                                          int w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nbytes, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + 1024 * w), 16, voff,
+                                             (unsigned)((long)r0 * ld * 2), 0, 0);
+#endif
+}
+
+template <bool CAUSAL, bool ROPE>
+__global__ void __launch_bounds__(NW * 64, 2)
+fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
+                   long ld_q, long ld_kv, const __bf16* __restrict__ O, long ld_o, const __bf16* __restrict__ dO,
+                   long ld_do, const float* __restrict__ LSE, float* __restrict__ DELTA, __bf16* __restrict__ dQ,
+                   long ld_dq, const float* __restrict__ cosT, const float* __restrict__ sinT, int B, int H, int Hkv,
+                   int S, float scale_log2, float scale, int group) {
+    constexpr int D = 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Ks = smem;            // [2][KT keys][128 B]
+    char* Vs = smem + 2 * BUF;  // [2][KT keys][128 B]
+
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, i16 = l & 15;
+    const int nqb = (S + QB - 1) / QB;
+    int rank, bh;
+    grouped_order((int)blockIdx.x, nqb, B * H, group, rank, bh);
+    const int qblk = CAUSAL ? nqb - 1 - rank : rank;  // causal: the heaviest query blocks first
+    const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+    const int q0 = qblk * QB, qw = q0 + 16 * w, q = qw + i16;
+    const bool q_ok = q < S;
+    const long qc = q_ok ? q : S - 1;
+    const long qrow = (long)b * S + qc;
+
+    // ---- prologue: every load issued before any is waited for (pinned Q / dO rows, O rows of delta, LSE, tile 0)
+    // lane: query i16, d = 32 ks + 8 g + j
+    u16x8 tqr[2], tgr[2], tor[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        const int d0 = 32 * ks + 8 * g;
+        tqr[ks] = *reinterpret_cast<const u16x8*>(Q + qrow * ld_q + (long)h * D + d0);
+        tgr[ks] = *reinterpret_cast<const u16x8*>(dO + qrow * ld_do + (long)h * D + d0);
+        tor[ks] = *reinterpret_cast<const u16x8*>(O + qrow * ld_o + (long)h * D + d0);
+    }
+    const float lse = LSE[((long)b * H + h) * S + qc];
+
+    const int kend = CAUSAL ? min(S, q0 + QB) : S;
+    const int nkt = (kend + KT - 1) / KT;
+    const __bf16* kb = K + (long)b * S * ld_kv + (long)hk * D;
+    const __bf16* vb = Vv + (long)b * S * ld_kv + (long)hk * D;
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int hbytes = head_bytes(ld_kv, S, D);
+    const unsigned voff = dma_lane_off(ld_kv, wu, l);
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+        dma_image(kb, hbytes, voff, 64 * sb, ld_kv, Ks + sb * TILE, wu);
+        dma_image(vb, hbytes, voff, 64 * sb, ld_kv, Vs + sb * TILE, wu);
+    }
+
+    // ---- pinned B operands (c folded into Q: S^T in log2 units) and delta = rowsum(dO * O)
+    bf16x8 qf[2], of[2];
+    float dsum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        float x[8];
+        unpack8(tqr[ks], x);
+        qf[ks] = __builtin_bit_cast(bf16x8, pack8(x, scale_log2));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dsum += bf2f(tgr[ks][i]) * bf2f(tor[ks][i]);
+        of[ks] = __builtin_bit_cast(bf16x8, tgr[ks]);
+    }
+    dsum += __shfl_xor(dsum, 16, 64);
+    dsum += __shfl_xor(dsum, 32, 64);
+    // row constants as the initial accumulators: S^T starts at -lse (-inf on pad rows: P = 0), dP^T at -delta
+    const float nl = (q_ok && lse < INFINITY) ? -lse : -INFINITY;
+
+    f32x4 acc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    __syncthreads();
+
+    const int trq = i16 >> 2, trc = 4 * (i16 & 3);  // transposed read: row 4 g + trq of a block, column trc
+    for (int it = 0; it < nkt; ++it) {
+        const int cur = it & 1, k0 = it * KT;
+        // current / next buffers as __restrict__ parameters: the next tile's DMA and this tile's reads are disjoint
+        // to the wait-count pass (no vmcnt(0) drain before the first transposed read; flash_attn_bwd_split.hip)
+        auto body = [&](char* __restrict__ Kc, const char* __restrict__ Vc, char* __restrict__ Kn,
+                        char* __restrict__ Vn) {
+            if (it + 1 < nkt) {  // buffer cur ^ 1 was last read in iteration it - 1, before its closing barrier
+#pragma unroll
+                for (int sb = 0; sb < 2; ++sb) {
+                    dma_image(kb, hbytes, voff, k0 + KT + 64 * sb, ld_kv, Kn + sb * TILE, wu);
+                    dma_image(vb, hbytes, voff, k0 + KT + 64 * sb, ld_kv, Vn + sb * TILE, wu);
+                }
+            }
+            if (CAUSAL && k0 > qw + 15) return;
+#pragma unroll
+            for (int kq = 0; kq < KT / 32; ++kq) {
+                if (CAUSAL && k0 + 32 * kq > qw + 15) break;  // the step is past every query of the wave
+                const bool need_mask = (CAUSAL && k0 + 32 * kq + 31 > qw) || (k0 + 32 * kq + 32 > S);
+                char* Kh = Kc + (kq >> 1) * TILE;
+                const char* Vh = Vc + (kq >> 1) * TILE;
+                const int kr = 32 * (kq & 1);
+                bf16x8 fk[2][2], fv[2][2];
+#pragma unroll
+                for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks) {
+                        const int off = sw(kr + 16 * kb2 + i16, 4 * ks + g);
+                        fk[kb2][ks] = lds_row16(Kh, off);
+                        fv[kb2][ks] = lds_row16(Vh, off);
+                    }
+                f32x4 sp[2], dp[2];
+#pragma unroll
+                for (int kb2 = 0; kb2 < 2; ++kb2) {
+                    sp[kb2] = f32x4{nl, nl, nl, nl};
+                    dp[kb2] = f32x4{-dsum, -dsum, -dsum, -dsum};
+                }
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int kb2 = 0; kb2 < 2; ++kb2) {
+                        sp[kb2] = mfma16(fk[kb2][ks], qf[ks], sp[kb2]);
+                        dp[kb2] = mfma16(fv[kb2][ks], of[ks], dp[kb2]);
+                    }
+                bf16x8 tk[4];
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt)
+                    tk[mt] = lds_tr_pair(Kh, sw_tr(kr + 4 * g + trq, 16 * mt + trc),
+                                         sw_tr(kr + 16 + 4 * g + trq, 16 * mt + trc));
+                // P^T = exp2(S^T), dS^T = P^T dP^T; key = k0 + 32 kq + 16 kb + 4 g + r, query = q
+                if (need_mask) {
+                    const int klim = (CAUSAL ? min(q, S - 1) : S - 1) - k0 - 32 * kq - 4 * g;
+#pragma unroll
+                    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float p = fast_exp2(sp[kb2][r]);
+                            dp[kb2][r] = (16 * kb2 + r <= klim) ? p * dp[kb2][r] : 0.f;
+                        }
+                } else {
+#pragma unroll
+                    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) dp[kb2][r] = fast_exp2(sp[kb2][r]) * dp[kb2][r];
+                }
+                bf16x8 db;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) db[j] = (__bf16)dp[j >> 2][j & 3];
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16(tk[mt], db, acc[mt]);
+            }
+        };
+        body(Ks + cur * BUF, Vs + cur * BUF, Ks + (cur ^ 1) * BUF, Vs + (cur ^ 1) * BUF);
+        if (it + 1 < nkt) __syncthreads();  // (none after the last tile: a wave done with the diagonal leaves early)
+    }
+
+    // ---- epilogue: delta for the dK/dV kernel; dQ = scale * R(-pos) dQ^T (lane: query i16, d = 16 mt + 4 g + i)
+    if (q_ok && g == 0) DELTA[((long)b * H + h) * S + q] = dsum;
+    if (!q_ok) return;
+    __bf16* dqp = dQ + ((long)b * S + q) * ld_dq + (long)h * D;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+        const int d0 = 16 * mt + 4 * g;
+        float x[4] = {acc[mt][0] * scale, acc[mt][1] * scale, acc[mt][2] * scale, acc[mt][3] * scale};
+        if (ROPE) {
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+                const float c = cosT[(long)q * (D / 2) + d0 / 2 + pr];
+                const float sn = sinT[(long)q * (D / 2) + d0 / 2 + pr];
+                const float a = x[2 * pr], bb = x[2 * pr + 1];
+                x[2 * pr] = a * c + bb * sn;
+                x[2 * pr + 1] = -a * sn + bb * c;
+            }
+        }
+        *reinterpret_cast<u16x4*>(dqp + d0) = u16x4{f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+    }
+}
+
+}  // namespace dq16
+}  // namespace fa
+}  // namespace bpe
+
+using namespace bpe;
+using namespace bpe::fa;
+
+// dQ form of the split backward at D = 64 without in-kernel RoPE: 0 = 32 queries per wave (fa_bwd_dq_kernel),
+// 1 = 16 queries per wave (this file); switched at run time (tests compare the two)
+static int g_dq_form = 0;
+
+int fa_dq_config(int form) {
+    const int prev = g_dq_form;
+    if (form >= 0) g_dq_form = form ? 1 : 0;
+    return prev;
+}
+
+// launches the 16-row dQ kernel when selected and applicable (D = 64, rope 0 / 2); false otherwise
+bool launch_fa_bwd_dq16(const FaArgs& a, hipStream_t s) {
+    if (g_dq_form != 1 || a.D != 64 || a.rope == 1) return false;
+    const int nblk = (a.S + dq16::QB - 1) / dq16::QB;
+    const int lds = 4 * dq16::BUF;
+    auto go = [&](auto kern) {
+        kern<<<nblk * a.B * a.H, dq16::NW * 64, lds, s>>>(a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do,
+                                                          a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin, a.B, a.H,
+                                                          a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
+    };
+    if (a.causal) {
+        if (a.rope == 2) go(dq16::fa_bwd_dq16_kernel<true, true>);
+        else go(dq16::fa_bwd_dq16_kernel<true, false>);
+    } else {
+        if (a.rope == 2) go(dq16::fa_bwd_dq16_kernel<false, true>);
+        else go(dq16::fa_bwd_dq16_kernel<false, false>);
+    }
+    return true;
+}

@@ -657,9 +657,11 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
     constexpr int NSUB = (RIN || D == 128) ? 1 : 2;  // 64-row images per LDS buffer (128-row tiles with LDS-DMA)
     constexpr int TILE = split::Geo<D>::TILE;
     const int nblk = (a.S + 32 * split::NW - 1) / (32 * split::NW);
-    split::fa_bwd_dq_kernel<D, C, R, RIN><<<nblk * a.B * a.H, split::NW * 64, 4 * TILE * NSUB, s>>>(
-        a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do, a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin,
-        a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
+    // the 16-queries-per-wave dQ kernel when selected (fa_dq_config; D = 64 without in-kernel RoPE)
+    if (!launch_fa_bwd_dq16(a, s))
+        split::fa_bwd_dq_kernel<D, C, R, RIN><<<nblk * a.B * a.H, split::NW * 64, 4 * TILE * NSUB, s>>>(
+            a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do, a.lse, a.delta, a.dq, a.ld_dq, a.cos,
+            a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
     // Q / dO buffers + the -lse / -delta rows
     const int lds = 4 * TILE * NSUB + 16 * 64 * NSUB;
     split::fa_bwd_dkv_kernel<D, C, R, RIN><<<nblk * a.B * a.Hkv, split::NW * 64, lds, s>>>(

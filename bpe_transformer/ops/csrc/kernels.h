@@ -177,6 +177,11 @@ void launch_fa_bwd(const FaArgs& a, hipStream_t s);
 bool fa_bwd_split_active(int D, int rope = 0);
 // backward form 0 split / 1 fused; negative = unchanged; returns the form in force before the call
 int fa_bwd_config(int mode);
+// flash_attn_bwd_dq16.hip: the split backward's dQ kernel with 16 queries per wave (D = 64, rope 0 / 2) when
+// fa_dq_config(1) selected it; false when not applicable / not selected.  fa_dq_config: 0 = 32 queries per wave,
+// 1 = 16; negative = unchanged; returns the form in force before the call
+bool launch_fa_bwd_dq16(const FaArgs& a, hipStream_t s);
+int fa_dq_config(int form);
 // per-workgroup s_memtime stamps of the last split-backward launch (BPE_FA_STAMPS builds only; false otherwise)
 bool fa_read_stamps(long long* host, int n);
 // per-workgroup s_memtime stamps of the last gemm_pp launch (BPE_GPP_STAMPS builds only; false otherwise)

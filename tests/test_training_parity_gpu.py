@@ -281,7 +281,8 @@ def test_fp8_engine_tracks_bf16_engine(gpu_device, monkeypatch, route, wgrad):
     the Llama shape: the final loss within 2 %, the 10-step running mean within 3 % throughout with bf16 weight
     gradients and within 4 % with fp8 ones (single steps of the early transient differ by more: the two precisions
     take different paths through the same loss landscape; the e5m2 rounding of the gradient in dW widens the
-    transient -- measured 1.4 % vs 3.1 % at its peak, step 24 -- while the final loss stays within 0.6 %).
+    transient -- measured 1.5 % vs 3.0 % at its peak -- while the final loss stays within 1.01 %, e5m2 margin 2;
+    single-step gaps of up to 27 % are the two trajectories' weights: test_fp8_forward_matches_bf16_on_same_weights).
     ``route``: the per-shape route table, or every fp8 GEMM on the hand-written gemm_pp F8 kernel (asserted: the
     hand kernel served every fp8 GEMM of the run -- forward, input and weight gradients at this 4096-token shape)."""
     from bpe_transformer.ops import fp8
@@ -311,3 +312,41 @@ def test_fp8_engine_tracks_bf16_engine(gpu_device, monkeypatch, route, wgrad):
     assert lb[-1] < lb[0] - 2.0
     assert max(rel_mean) < (0.04 if wgrad else 0.03), (max(rel_mean), rel_mean.index(max(rel_mean)))
     assert rel[-1] < 0.02, rel[-1]
+
+
+def _same_weights_losses(c: Shape, steps, gpu_device, margin: float = 1.0) -> dict:
+    """Train the bf16 engine and, before step s in ``steps``, evaluate batch s on the SAME weights in bf16 and in fp8
+    (scales calibrated on the 16 preceding batches, what the delayed recipe holds at that step)."""
+    ids, vocab = _tokens()
+    model = _ours(vocab, c, gpu_device)
+    eng = _engine(model, 1, c)
+    data = _batches(ids, STEPS, c.B, c.S, gpu_device)
+    out = {}
+    for it in range(max(steps) + 1):
+        if it in steps:
+            with torch.no_grad():
+                x, y = data[it]
+                lb = float(model.loss(x, y))
+                model.enable_fp8(margin=margin)
+                for jt in range(max(0, it - 16), it):
+                    model.loss(*data[jt])
+                    for st in model.fp8_states():
+                        st.update()
+                l8 = float(model.loss(x, y))
+                for layer in model.layers:
+                    layer.fp8 = None
+                model.fp8_state = model.fp8_grad_state = None
+            out[it] = (lb, l8)
+        eng.train_step([data[it]], lr=_lr(it, c))
+    return out
+
+
+def test_fp8_forward_matches_bf16_on_same_weights(gpu_device):
+    """Per-step bound on the fp8 forward itself: at the steps where the fp8 run's loss departs most from the bf16
+    run's (18, 25, 73: up to 27 %, benchmarks/fp8_spike_probe.py), the fp8 forward on the bf16 run's own weights is
+    within 1 % of the bf16 forward.  The transient gaps of test_fp8_engine_tracks_bf16_engine are therefore the two
+    trajectories' weights, not the rounding of one fp8 step (profiles/parity/fp8_spike_probe_r5.json)."""
+    res = _same_weights_losses(SHAPES["llama"], [18, 25, 73], gpu_device)
+    _log("parity_llamashape_L2_fp8_same_weights.json", {str(k): {"bf16": v[0], "fp8": v[1]} for k, v in res.items()})
+    for it, (lb, l8) in res.items():
+        assert math.isfinite(l8) and abs(l8 - lb) / lb < 0.01, (it, lb, l8)
