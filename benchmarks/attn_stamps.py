@@ -2,7 +2,7 @@
 
 Needs the stamps variant build (``python -m bpe_transformer.ops.build --variant stamps -D BPE_FA_STAMPS``) and runs
 with ``BPE_HIP_VARIANT=stamps``.  For each kernel (dQ, dK/dV) and each tile count it prints the mean workgroup
-duration, its prologue (entry -> first barrier) and the per-tile loop time, in shader cycles.
+duration, its prologue (entry -> first barrier) and the time per full tile and the last (diagonal) tile, in shader cycles.
 usage: BPE_HIP_VARIANT=stamps python benchmarks/attn_stamps.py [--batch B] [--seq S] [--heads H] [--kv-heads Hkv]
 """
 import argparse
@@ -22,8 +22,10 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--heads", type=int, default=12)
     ap.add_argument("--kv-heads", type=int, default=None)
+    ap.add_argument("--dq-form", type=int, default=0, help="ops.fa_dq_config: 0 = 32 queries per wave, 1 = 16")
     a = ap.parse_args()
     h = ops()
+    h.fa_dq_config(a.dq_form)
     B, S, H, D = a.batch, a.seq, a.heads, 64
     Hkv = a.kv_heads or H
     torch.manual_seed(0)
@@ -42,13 +44,18 @@ def main():
     nblk = (S + 127) // 128
     for name, base, n in (("dQ", 0, nblk * B * H), ("dK/dV", 32768, nblk * B * Hkv)):
         r = st[base : base + n]
-        dur, pro, loop, nt = r[:, 3] - r[:, 0], r[:, 1] - r[:, 0], r[:, 3] - r[:, 1], r[:, 5]
-        print(f"{name} B={B} S={S} H={H} Hkv={Hkv}: {n} workgroups, mean {dur.mean():.0f} cycles, prologue "
-              f"{pro.mean():.0f} ({pro.sum() / dur.sum() * 100:.1f} %)")
+        # slot 2 = start of the last (diagonal) tile; the epilogue is not stamped (entry .. slot 3)
+        dur, pro, nt = r[:, 3] - r[:, 0], r[:, 1] - r[:, 0], r[:, 5]
+        diag, body = r[:, 3] - r[:, 2], r[:, 2] - r[:, 1]
+        print(f"{name} B={B} S={S} H={H} Hkv={Hkv} dq_form={a.dq_form}: {n} workgroups, mean {dur.mean():.0f} cycles: "
+              f"prologue {pro.mean():.0f} ({pro.sum() / dur.sum() * 100:.1f} %), full tiles {body.mean():.0f} "
+              f"({body.sum() / dur.sum() * 100:.1f} %), last (diagonal) tile {diag.mean():.0f} "
+              f"({diag.sum() / dur.sum() * 100:.1f} %)")
         for t in sorted(set(nt.tolist())):
             m = nt == t
+            full = (body[m] / (t - 1)).mean() if t > 1 else float("nan")
             print(f"  tiles {int(t):3d}: n {int(m.sum()):5d}  workgroup {dur[m].mean():8.0f}  prologue {pro[m].mean():6.0f}"
-                  f"  loop/tile {(loop[m] / t).mean():6.0f}")
+                  f"  full tile {full:6.0f}  last tile {diag[m].mean():6.0f}")
 
 
 if __name__ == "__main__":

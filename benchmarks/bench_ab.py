@@ -3,7 +3,9 @@
     python benchmarks/bench_ab.py --set bpe_transformer.models.fused_block._FUSE_QKV_ROPE=0 -- --steps 20
 
 Each ``--set module.attr=value`` imports the module and sets the attribute (ints / floats / True / False parsed,
-anything else kept as a string) before bench.py runs in this process; everything after ``--`` goes to bench.py.
+anything else kept as a string) before bench.py runs in this process; each ``--op name=int`` calls the HIP
+library's run-time switch ``torch.ops.bpe_hip.<name>(int)`` (e.g. ``--op fa_dq_config=1``); everything after
+``--`` goes to bench.py.
 """
 import importlib
 import os
@@ -32,8 +34,18 @@ def main():
     sys.path.insert(0, root)
     it = iter(argv)
     for a in it:
+        if a == "--op":
+            name, value = next(it).split("=", 1)
+            import torch
+
+            from bpe_transformer import ops
+
+            ops.load()
+            prev = getattr(torch.ops.bpe_hip, name)(int(value))
+            print(f"[bench_ab] {name}({value}) (was {prev})", file=sys.stderr)
+            continue
         if a != "--set":
-            sys.exit(f"unknown argument {a!r} (use --set module.attr=value ... -- bench args)")
+            sys.exit(f"unknown argument {a!r} (use --set module.attr=value / --op name=int ... -- bench args)")
         spec = next(it)
         target, value = spec.split("=", 1)
         mod, attr = target.rsplit(".", 1)

@@ -62,10 +62,26 @@ def _digest(paths: list[Path], extra: list[str]) -> str:
     return h.hexdigest()
 
 
-def source_digest(csrc: Path = CSRC, defines: list[str] | None = None) -> str:
+def source_digest(csrc: Path = CSRC, defines: list[str] | None = None, flags: list[str] | None = None) -> str:
     """sha256 over every kernel source, header and the binding unit plus the arch and flags: the library stamp."""
     files = sorted(csrc.glob("*.h")) + sorted(csrc.glob("*.hip")) + [csrc / "torch_bindings.cpp"]
-    return _digest(files, [ARCH, *COMMON_FLAGS, *[f"-D{d}" for d in (defines or [])]])
+    return _digest(files, [ARCH, *COMMON_FLAGS, *[f"-D{d}" for d in (defines or [])], *(flags or [])])
+
+
+def file_flags(src: Path) -> list[str]:
+    """Per-file compiler flags: a ``// build-flags: ...`` line among the first 40 lines of the source (part of the
+    source, so covered by its digest).  The attention and GEMM kernels use it for ``-fno-slp-vectorize``: packed f32
+    VALU (``v_pk_mul_f32`` / ``v_pk_fma_f32``) issued beside MFMAs costs more than the two scalar instructions it
+    replaces (MI355X_MICROARCH, price of one filler beside MFMAs)."""
+    for line in src.read_text().splitlines()[:40]:
+        if line.startswith("// build-flags:"):
+            out = []
+            for tok in line.split(":", 1)[1].split():  # flags up to the first word that is not one (a remark)
+                if not tok.startswith("-"):
+                    break
+                out.append(tok)
+            return out
+    return []
 
 
 def stamp_path(lib: Path) -> Path:
@@ -108,11 +124,12 @@ def lib_path(variant: str | None = None) -> Path:
 
 
 def build(verbose: bool = False, jobs: int | None = None, force: bool = False, variant: str | None = None,
-          defines: list[str] | None = None, src_dir: Path | None = None) -> Path:
+          defines: list[str] | None = None, src_dir: Path | None = None, flags: list[str] | None = None) -> Path:
     """Build the library; ``variant`` + ``defines`` build an A/B copy (``_bpe_hip_<variant>.so``, own object
     directory) compiled with extra ``-D`` flags, selected at run time with ``BPE_HIP_VARIANT=<variant>``.
     ``src_dir``: compile another copy of ``csrc`` (e.g. an older revision, ``tools/ab_build.sh``) into the
-    variant, for same-process / same-box A/B runs."""
+    variant, for same-process / same-box A/B runs.  ``flags``: extra compiler flags after every file's own (a
+    variant's ``-fslp-vectorize`` undoes the per-file ``-fno-slp-vectorize``, for instance)."""
     csrc = Path(src_dir) if src_dir else CSRC
     build_dir = BUILD if not variant else BUILD.parent / f"hip_{variant}"
     lib = lib_path(variant)
@@ -127,7 +144,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False, v
     for src in hip_srcs:
         obj = build_dir / (src.stem + ".o")
         objs.append(obj)
-        cmd = [HIPCC, *common, "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, *common, *file_flags(src), *(flags or []), "-c", str(src), "-o", str(obj)]
         key = _digest([src, *headers], cmd)
         if force or _needs_build(obj, key):
             jobs_list.append((cmd, obj, key))
@@ -153,7 +170,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False, v
         n = jobs or min(8, os.cpu_count() or 4)
         with cf.ThreadPoolExecutor(n) as ex:
             list(ex.map(compile_one, jobs_list))
-    digest = source_digest(csrc, defines)
+    digest = source_digest(csrc, defines, flags)
     if force or jobs_list or not lib.exists() or read_stamp(lib) != digest:  # (read_stamp checks the lib bytes)
         stamp_path(lib).unlink(missing_ok=True)
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(lib), *map(str, objs)]
@@ -162,7 +179,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False, v
         link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip"]
         _run(link, verbose)
         stamp_path(lib).write_text(json.dumps({"digest": digest, "lib_sha256": lib_sha(lib), "arch": ARCH,
-                                               "defines": defines or [], "src": str(csrc)}) + "\n")
+                                               "defines": defines or [], "flags": flags or [], "src": str(csrc)}) + "\n")
     return lib
 
 
@@ -173,11 +190,15 @@ def main() -> None:
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--variant", default=None, help="build an A/B copy _bpe_hip_<variant>.so")
     ap.add_argument("-D", dest="defines", action="append", default=[], help="extra preprocessor define")
+    ap.add_argument("--flag", dest="flags", action="append", default=[],
+                    help="extra compiler flag for every source (variants only), e.g. --flag=-fslp-vectorize")
     ap.add_argument("--src", default=None, help="csrc directory to compile instead of the in-tree one (--variant)")
     a = ap.parse_args()
     if a.src and not a.variant:
         ap.error("--src needs --variant (never overwrite the in-tree library with other sources)")
-    print(build(verbose=a.verbose, jobs=a.jobs, force=a.force, variant=a.variant, defines=a.defines,
+    if a.flags and not a.variant:
+        ap.error("--flag needs --variant (the in-tree library takes its flags from the sources)")
+    print(build(verbose=a.verbose, jobs=a.jobs, force=a.force, variant=a.variant, defines=a.defines, flags=a.flags,
                 src_dir=a.src))
 
 

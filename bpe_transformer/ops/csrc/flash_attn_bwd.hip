@@ -1,4 +1,5 @@
 // Flash attention backward with fused RoPE, gfx950 (MI355X).
+// build-flags: -fno-slp-vectorize   (no packed f32 VALU beside the MFMAs: ops/build.py file_flags)
 //
 // Parity target: the gradient of reference contracts K7/K10
 // (`tests/adapters.py:92-184`); checked against autograd of the fp32 oracle.

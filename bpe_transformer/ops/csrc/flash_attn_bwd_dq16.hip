@@ -1,4 +1,5 @@
 // Flash attention backward, dQ kernel with 16 queries per wave (D = 64), gfx950 (MI355X).
+// build-flags: -fno-slp-vectorize   (no packed f32 VALU beside the MFMAs: ops/build.py file_flags)
 //
 // Parity target: the dQ of the split backward (flash_attn_bwd_split.hip fa_bwd_dq_kernel; reference contracts
 // K7/K10, `tests/adapters.py:92-184`); checked against autograd of the fp32 oracle and against the 32-row kernel
@@ -39,6 +40,20 @@ __device__ __forceinline__ int sw(int row, int c) { return row * 128 + ((c ^ (ro
 // byte offset of the 8-byte granule at (row, col) (transposed reads)
 __device__ __forceinline__ int sw_tr(int row, int col) { return sw(row, col >> 3) + ((col & 7) << 1); }
 
+// Per-workgroup s_memtime stamps (BPE_FA_STAMPS variant builds; read through fa_read_stamps, rows 0.. when this
+// kernel is selected), taken by the LAST wave (the one with the most steps on the diagonal tile): slot 0 entry, 1
+// after the prologue barrier, 2 at the start of the last tile, 3 after the tile loop, 5 the tile count
+#ifdef BPE_FA_STAMPS
+__device__ long long g_stamps16[32768 * 8];
+#define DQ16_STAMP(i, v)                                                                             \
+    if (threadIdx.x == (NW - 1) * 64) {                                                              \
+        g_stamps16[(long)(blockIdx.x & 32767) * 8 + (i)] = __builtin_amdgcn_s_memtime();            \
+        if ((i) == 3) g_stamps16[(long)(blockIdx.x & 32767) * 8 + 5] = (v);                        \
+    }
+#else
+#define DQ16_STAMP(i, v)
+#endif
+
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -72,6 +87,7 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
     char* Vs = smem + 2 * BUF;  // [2][KT keys][128 B]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, i16 = l & 15;
+    DQ16_STAMP(0, 0);
     const int nqb = (S + QB - 1) / QB;
     int rank, bh;
     grouped_order((int)blockIdx.x, nqb, B * H, group, rank, bh);
@@ -129,10 +145,12 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
     for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     __syncthreads();
+    DQ16_STAMP(1, 0);
 
     const int trq = i16 >> 2, trc = 4 * (i16 & 3);  // transposed read: row 4 g + trq of a block, column trc
     for (int it = 0; it < nkt; ++it) {
         const int cur = it & 1, k0 = it * KT;
+        if (it + 1 == nkt) DQ16_STAMP(2, 0);
         // current / next buffers as __restrict__ parameters: the next tile's DMA and this tile's reads are disjoint
         // to the wait-count pass (no vmcnt(0) drain before the first transposed read; flash_attn_bwd_split.hip)
         auto body = [&](char* __restrict__ Kc, const char* __restrict__ Vc, char* __restrict__ Kn,
@@ -206,6 +224,7 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
         if (it + 1 < nkt) __syncthreads();  // (none after the last tile: a wave done with the diagonal leaves early)
     }
 
+    DQ16_STAMP(3, nkt);
     // ---- epilogue: delta for the dK/dV kernel; dQ = scale * R(-pos) dQ^T (lane: query i16, d = 16 mt + 4 g + i)
     if (q_ok && g == 0) DELTA[((long)b * H + h) * S + q] = dsum;
     if (!q_ok) return;
@@ -243,6 +262,22 @@ int fa_dq_config(int form) {
     const int prev = g_dq_form;
     if (form >= 0) g_dq_form = form ? 1 : 0;
     return prev;
+}
+
+// copy the 16-row dQ kernel's stamps of the last launch into rows [0, 32768) (BPE_FA_STAMPS builds; false
+// otherwise or when the kernel is not selected)
+bool fa_read_stamps_dq16(long long* host, int n) {
+#ifdef BPE_FA_STAMPS
+    if (g_dq_form != 1) return false;
+    (void)hipDeviceSynchronize();
+    const int rows = n < 32768 ? n : 32768;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(dq16::g_stamps16), (size_t)rows * 8 * sizeof(long long), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess;
+#else
+    (void)host;
+    (void)n;
+    return false;
+#endif
 }
 
 // launches the 16-row dQ kernel when selected and applicable (D = 64, rope 0 / 2); false otherwise

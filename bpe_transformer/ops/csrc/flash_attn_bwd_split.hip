@@ -1,4 +1,5 @@
 // Flash attention backward, split form (D = 64 and D = 128), gfx950 (MI355X).
+// build-flags: -fno-slp-vectorize   (no packed f32 VALU beside the MFMAs: ops/build.py file_flags)
 //
 // Parity target: the gradient of reference contracts K7/K10 (`tests/adapters.py:92-184`); checked against
 // autograd of the fp32 oracle (tests/test_kernels_gpu.py).
@@ -56,7 +57,7 @@ struct Geo {
 };
 
 // Per-workgroup s_memtime stamps (a diagnostic variant build: ops.build --variant stamps -D BPE_FA_STAMPS): slot 0
-// entry, 1 after the prologue barrier, 3 after the tile loop, 5 the tile count; rows 0.. the dQ kernel's workgroups,
+// entry, 1 after the prologue barrier, 2 at the start of the last tile, 3 after the tile loop, 5 the tile count; rows 0.. the dQ kernel's workgroups,
 // rows 32768.. the dK/dV kernel's; read with ops.fa_stamps().  The normal build compiles them out.
 #ifdef BPE_FA_STAMPS
 __device__ long long g_stamps[65536 * 8];
@@ -207,6 +208,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);  // tr-read column inside a 32-wide d tile
     for (int it = 0; it < nkt; ++it) {
         const int cur = it & 1, k0 = it * KT;
+        if (it + 1 == nkt) FA_STAMP(0, 2, 0);
         // the current and next buffers as __restrict__ parameters (see fa_bwd_dkv_kernel): no DMA drain mid-tile
         auto body = [&](char* __restrict__ Kc, const char* __restrict__ Vc, char* __restrict__ Kn,
                         char* __restrict__ Vn) {
@@ -507,6 +509,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     const unsigned span = (unsigned)(S - klim);  // valid query q: (unsigned)(q - klim) < span
     for (int it = 0; it < nsteps; ++it) {
         const int cur = it & 1, m0 = m0_of(it);
+        if (it + 1 == nsteps) FA_STAMP(32768, 2, 0);
         // One iteration with the current and the next buffers as __restrict__ parameters: the DMA into the next
         // buffer and the fragment reads of the current one are then provably disjoint to the wait-count pass
         // (without it hipcc drains the DMA, vmcnt(0), before the first transposed read of every half-tile).
@@ -677,8 +680,10 @@ bool fa_dkv_partials_needed(int D, int rope) { return !fa_bwd_split_active(D, ro
 bool fa_read_stamps(long long* host, int n) {
 #ifdef BPE_FA_STAMPS
     (void)hipDeviceSynchronize();
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(split::g_stamps), (size_t)n * 8 * sizeof(long long), 0,
-                               hipMemcpyDeviceToHost) == hipSuccess;
+    const bool ok = hipMemcpyFromSymbol(host, HIP_SYMBOL(split::g_stamps), (size_t)n * 8 * sizeof(long long), 0,
+                                        hipMemcpyDeviceToHost) == hipSuccess;
+    fa_read_stamps_dq16(host, n);  // rows 0.. from the 16-row dQ kernel when it ran
+    return ok;
 #else
     (void)host;
     (void)n;

@@ -1,4 +1,5 @@
 // Flash attention forward with fused interleaved RoPE, gfx950 (MI355X).
+// build-flags: -fno-slp-vectorize   (no packed f32 VALU beside the MFMAs: ops/build.py file_flags)
 //
 // Parity targets: reference contracts K7/K9/K10 (`tests/adapters.py:92-184`):
 // softmax(Q K^T / sqrt(d) [causal]) V with RoPE on Q and K (interleaved

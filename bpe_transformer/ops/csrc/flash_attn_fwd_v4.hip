@@ -1,4 +1,5 @@
 // Flash attention forward v4 (D = 64, Q / K pre-rotated or no RoPE), gfx950 (MI355X).
+// build-flags: -fno-slp-vectorize   (no packed f32 VALU beside the MFMAs: ops/build.py file_flags)
 //
 // Parity target: reference contracts K7/K9/K10 (`tests/adapters.py:92-184`), as fa_fwd_kernel.
 //

@@ -1,4 +1,5 @@
 // bf16 MFMA GEMM with split-K for gfx950, used for the weight-gradient products.
+// build-flags: -fno-slp-vectorize   (no packed f32 VALU beside the MFMAs: ops/build.py file_flags)
 //
 //   C[Mo, No] = beta * C + sum_r A(i, r) * B(r, j)         (fp32 accumulation)
 //

@@ -1,4 +1,5 @@
 // 8-wave ping-pong bf16 MFMA GEMM for gfx950 (all three GEMMs of a linear layer).
+// build-flags: -fno-slp-vectorize   (no packed f32 VALU beside the MFMAs: ops/build.py file_flags)
 //
 //   C[M, N] = beta * C + sum_r A(i, r) B(r, j)        (fp32 accumulation, bf16 or fp32-slab output)
 //

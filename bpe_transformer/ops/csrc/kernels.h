@@ -181,6 +181,7 @@ int fa_bwd_config(int mode);
 // fa_dq_config(1) selected it; false when not applicable / not selected.  fa_dq_config: 0 = 32 queries per wave,
 // 1 = 16; negative = unchanged; returns the form in force before the call
 bool launch_fa_bwd_dq16(const FaArgs& a, hipStream_t s);
+bool fa_read_stamps_dq16(long long* host, int n);
 int fa_dq_config(int form);
 // per-workgroup s_memtime stamps of the last split-backward launch (BPE_FA_STAMPS builds only; false otherwise)
 bool fa_read_stamps(long long* host, int n);

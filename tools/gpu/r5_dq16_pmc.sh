@@ -15,3 +15,8 @@ for F in 0 1; do
 done
 find $OUT -name "*.csv" -size +20M -delete
 cat $OUT/summary_f0.txt $OUT/summary_f1.txt
+for F in 0 1; do
+  BPE_HIP_VARIANT=stamps timeout -k 10 120 python3 benchmarks/attn_stamps.py --dq-form $F > gpurun_out/attn_stamps_f$F.log 2>&1 || exit $?
+  BPE_HIP_VARIANT=stamps timeout -k 10 120 python3 benchmarks/attn_stamps.py --dq-form $F --batch 32 --seq 2048 --heads 32 --kv-heads 4 > gpurun_out/attn_stamps_llama_f$F.log 2>&1 || exit $?
+done
+cat gpurun_out/attn_stamps_f*.log
