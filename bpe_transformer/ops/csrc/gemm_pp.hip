@@ -55,6 +55,11 @@ constexpr int NT = 512, BT = 256, BK = 64;
 constexpr int OPB = 32768;          // one operand image per stage
 constexpr int STAGE = 2 * OPB;      // 64 KiB
 constexpr int LDS_BYTES = 2 * STAGE;  // 128 KiB
+#ifdef BPE_GPP_PHASE_STAMPS
+constexpr int LDS_LAUNCH = LDS_BYTES + 8 * 64 * 8;  // + the phase stamps of 8 waves
+#else
+constexpr int LDS_LAUNCH = LDS_BYTES;
+#endif
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
@@ -165,6 +170,30 @@ __device__ __forceinline__ void bar() {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
 }
+
+// Per-wave phase stamps (a diagnostic variant build: ops.build --variant pstamps -D BPE_GPP_PHASE_STAMPS; read by
+// benchmarks/gemm_phase_stamps.py): every wave records s_memtime at four events of each phase of K-tiles
+// PST_KT0 .. PST_KT0 + PST_NKT - 1 of the one-tile kernel's spread schedule -- 0 section start (before its
+// fragment reads), 1 after its wait (reads / DMA retired), 2 after the barrier (MFMA section start), 3 after the
+// MFMA issue (before the closing barrier) -- into LDS above the two stages (no VMEM traffic, so the kernel's
+// vmcnt accounting is untouched), copied to g_gpp_phase at the end for workgroups 0 .. 1023.
+#ifdef BPE_GPP_PHASE_STAMPS
+constexpr int PST_KT0 = 2, PST_NKT = 4, PST_VALS = PST_NKT * 4 * 4;  // per wave
+__device__ long long g_gpp_phase[1024 * 8 * PST_VALS];
+__device__ __forceinline__ void pst(int kt, int p, int e) {
+    extern __shared__ __attribute__((aligned(16))) char pst_smem[];
+    if (kt >= PST_KT0 && kt < PST_KT0 + PST_NKT) {
+        const long long t = __builtin_amdgcn_s_memtime();
+        const int w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0)
+            *reinterpret_cast<long long*>(pst_smem + 2 * 2 * 32768 +
+                                          ((w * PST_NKT + kt - PST_KT0) * 16 + 4 * p + e) * 8) = t;
+    }
+}
+#define PST(p, e) pst(kt_idx, p, e)
+#else
+#define PST(p, e)
+#endif
 
 template <bool AK, bool BKM, bool SUB = false>
 __device__ __forceinline__ void load_a(Frags& f, char* img, int g, int m, int l) {
@@ -352,7 +381,8 @@ __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2
 template <bool AK, bool BKM, int DIAG, bool SPLIT = false, int F8 = 0>
 __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
                                              const __bf16* an, const __bf16* bn, const SpreadOff& so, int g, int wl,
-                                             int l, f32x4 (&acc)[8][4], bool first = false) {
+                                             int l, f32x4 (&acc)[8][4], bool first = false, int kt_idx = -1) {
+    (void)kt_idx;  // phase stamps builds only
     Frags f;
     char* Ac = cur;
     char* Bc = cur + OPB;
@@ -363,6 +393,8 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     // so it waits vmcnt(6) and leaves the piece pair issued two load sections ago in flight one section longer
     auto phase = [&](const __bf16* t0, const int (&off)[2], char* img, int lb, int m, int n, bool last_nodma_wait2,
                      bool relax = false) {
+        const int ph = 2 * m + (m ? 1 - n : n);  // (m0,n0) 0, (m0,n1) 1, (m1,n1) 2, (m1,n0) 3
+        (void)ph;
         if (dma) {
             if constexpr (SPLIT) dma_one(t0, off[0], img, lb);
             else dma_pair(t0, off, img, lb);
@@ -378,7 +410,9 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
         } else {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         }
+        PST(ph, 1);
         bar();
+        PST(ph, 2);
         if constexpr (SPLIT) {
             mma_half<F8>(acc, f, m, n, 0);
             if (dma) {
@@ -390,19 +424,24 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
         } else {
             mma_quadrant<F8>(acc, f, m, n);
         }
+        PST(ph, 3);
         bar();
     };
     // phase 0: (m0, n0)
+    PST(0, 0);
     load_a<AK, BKM, true>(f, Ac, g, 0, l);
     load_b<AK, BKM, true>(f, Bc, wl, 0, l);
     phase(an, so.a0, nxt, so.la0, 0, 0, true);
     // phase 1: (m0, n1)
+    PST(1, 0);
     load_b<AK, BKM, true>(f, Bc, wl, 1, l);
     phase(bn, so.b0, nxt + OPB, so.lb0, 0, 1, false);
     // phase 2: (m1, n1)
+    PST(2, 0);
     load_a<AK, BKM, true>(f, Ac, g, 1, l);
     phase(bn, so.b1, nxt + OPB, so.lb1, 1, 1, false, true);
     // phase 3: (m1, n0)
+    PST(3, 0);
     load_b<AK, BKM, true>(f, Bc, wl, 0, l);
     phase(an, so.a1, nxt, so.la1, 1, 0, false);
 }
@@ -678,7 +717,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
             char* nxt = smem + ((kt + 1) & 1) * STAGE;
             const long k1 = (long)(kb + kt + 1) * BK;
             ktile_spread<AK, BKM, DIAG, SPREAD == 2, F8>(cur, nxt, kt + 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
-                                                         tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc);
+                                                         tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc, false, kt);
         }
     } else {
         int oa[4], ob[4];
@@ -738,6 +777,11 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
         epilogue_bf16<EPI, F8, 1>(acc, smem, g, wl, l, tid, i0, j0, jb, C, ldc, beta, ep, st_on, false, blockIdx.x);
         GPP_STAMP(4);
     }
+#ifdef BPE_GPP_PHASE_STAMPS
+    if (blockIdx.x < 1024 && l < PST_VALS)  // each wave its own values (LDS above the stages; written by itself)
+        g_gpp_phase[((long)blockIdx.x * 8 + w) * PST_VALS + l] =
+            *reinterpret_cast<const long long*>(smem + LDS_BYTES + (w * PST_VALS + l) * 8);
+#endif
 }
 
 
@@ -889,12 +933,12 @@ static void launch_persist(K* k, int ntiles, hipStream_t s, Args... args) {
     static_assert(sizeof...(Args) > 0, "");
     const int cap = g_persist >= 2 ? g_persist : num_cus();  // mode >= 2: a test hook, at most `mode` workgroups
     const int grid = ntiles < cap ? ntiles : cap;
-    k<<<grid, NT, LDS_BYTES, s>>>(args...);
+    k<<<grid, NT, LDS_LAUNCH, s>>>(args...);
 }
 
 template <typename K>
 static void lds_attr(K* k) {  // > 64 KiB dynamic LDS must be opted into once per instantiation
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_LAUNCH);
 }
 
 // dgu = swiglu_bwd(dY . W2, gu): A = dY [M][R] (K-major), B = W2 [R][F] (MN-major)
@@ -903,7 +947,7 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
     static bool attr = false;
     auto* k = &gemm_pp_kernel<true, false, false, 0, EPI_SWIGLU_BWD, 1>;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_LAUNCH);
         attr = true;
     }
     const int grid = (M / BT) * (F / BT);
@@ -916,7 +960,7 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
         return launch_persist(kp, grid, s, (const __bf16*)dY, ldy, (const __bf16*)W2, ldw, (__bf16*)nullptr, 0L, 0.f,
                               M, F, R, ep);
     }
-    k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)dY, ldy, (const __bf16*)W2, ldw, nullptr, nullptr, 0, 0.f, M, F, R,
+    k<<<grid, NT, LDS_LAUNCH, s>>>((const __bf16*)dY, ldy, (const __bf16*)W2, ldw, nullptr, nullptr, 0, 0.f, M, F, R,
                                   1, ep);
 }
 
@@ -926,7 +970,7 @@ void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ld
     static bool attr = false;
     auto* k = &gemm_pp_kernel<true, true, false, 0, EPI_SWIGLU_FWD, 1>;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_LAUNCH);
         attr = true;
     }
     const int grid = (M / BT) * (F / (BT / 2));
@@ -939,7 +983,7 @@ void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ld
         return launch_persist(kp, grid, s, (const __bf16*)X, ldx, (const __bf16*)W13, ldw, (__bf16*)nullptr, 0L, 0.f,
                               M, 2 * F, R, ep);
     }
-    k<<<grid, NT, LDS_BYTES, s>>>((const __bf16*)X, ldx, (const __bf16*)W13, ldw, nullptr, nullptr, 0, 0.f, M, 2 * F,
+    k<<<grid, NT, LDS_LAUNCH, s>>>((const __bf16*)X, ldx, (const __bf16*)W13, ldw, nullptr, nullptr, 0, 0.f, M, 2 * F,
                                   R, 1, ep);
 }
 
@@ -964,7 +1008,7 @@ void launch_gemm_pp_rope(const void* X, long ldx, const void* W, long ldw, void*
     static bool attr = false;
     auto* k = &gemm_pp_kernel<true, true, false, 0, EPI_ROPE, 1>;
     if (!attr) lds_attr(k), attr = true;
-    k<<<ntiles, NT, LDS_BYTES, s>>>((const __bf16*)X, ldx, (const __bf16*)W, ldw, nullptr, (__bf16*)C, ldc, 0.f, M,
+    k<<<ntiles, NT, LDS_LAUNCH, s>>>((const __bf16*)X, ldx, (const __bf16*)W, ldw, nullptr, (__bf16*)C, ldc, 0.f, M,
                                     N, R, 1, ep);
 }
 
@@ -978,7 +1022,7 @@ void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, 
     auto* k = fmt_a == 1 ? k2 : k1;
     bool& attr = fmt_a == 1 ? attr2 : attr1;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_LAUNCH);
         attr = true;
     }
     Epi ep{};
@@ -995,7 +1039,7 @@ void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, 
         return launch_persist(kp, (M / BT) * (N / BT), s, (const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2,
                               (__bf16*)C, ldc, 0.f, M, N, K / 2, ep);
     }
-    k<<<(M / BT) * (N / BT), NT, LDS_BYTES, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, nullptr,
+    k<<<(M / BT) * (N / BT), NT, LDS_LAUNCH, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, nullptr,
                                                   (__bf16*)C, ldc, 0.f, M, N, K / 2, 1, ep);
 }
 
@@ -1024,7 +1068,7 @@ void launch_gemm_fp8_rope(const void* A, long lda, const void* B, long ldb, void
     static bool attr = false;
     auto* k = &gemm_pp_kernel<true, true, false, 0, EPI_ROPE, 1, 1>;
     if (!attr) lds_attr(k), attr = true;
-    k<<<(M / BT) * (N / BT), NT, LDS_BYTES, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, nullptr,
+    k<<<(M / BT) * (N / BT), NT, LDS_LAUNCH, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, nullptr,
                                                   (__bf16*)C, ldc, 0.f, M, N, K / 2, 1, ep);
 }
 
@@ -1043,7 +1087,7 @@ void launch_gemm_fp8_splitk(const void* A, long lda, const void* B, long ldb, vo
     ep.prio = prio_mode();
     ep.sa = sa;
     ep.sb = sb;
-    k<<<(M / BT) * (N / BT) * splits, NT, LDS_BYTES, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, slab,
+    k<<<(M / BT) * (N / BT) * splits, NT, LDS_LAUNCH, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, slab,
                                                            nullptr, 0, 0.f, M, N, K / 2, splits, ep);
     splitk_reduce(slab, C, ldc, beta, M, N, splits, c_f32, s);
 }
@@ -1059,7 +1103,7 @@ static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, fl
     static bool attr = false;  // > 64 KiB dynamic LDS must be opted into once per instantiation
     auto* k = &gemm_pp_kernel<AK, BKM, SLAB, DIAG, EPI_NONE, SPREAD>;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_LAUNCH);
         attr = true;
     }
     const int grid = (M / BT) * (N / BT) * splits;
@@ -1073,7 +1117,7 @@ static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, fl
             return launch_persist(kp, grid, s, a, lda, b, ldb, c, ldc, beta, M, N, R, ep);
         }
     }
-    k<<<grid, NT, LDS_BYTES, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, ep);
+    k<<<grid, NT, LDS_LAUNCH, s>>>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, ep);
 }
 
 template <bool AK, bool BKM, bool SLAB, int DIAG>
@@ -1114,6 +1158,19 @@ void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const v
 }
 
 // copy the last gemm_pp launch's stamps out (BPE_GPP_STAMPS builds; false otherwise)
+// phase stamps of the last one-tile launch: n workgroups x 8 waves x PST_VALS (BPE_GPP_PHASE_STAMPS builds)
+bool gpp_read_phase_stamps(long long* host, int n) {
+#ifdef BPE_GPP_PHASE_STAMPS
+    (void)hipDeviceSynchronize();
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(bpe::gpp::g_gpp_phase), (size_t)n * 8 * PST_VALS * sizeof(long long),
+                               0, hipMemcpyDeviceToHost) == hipSuccess;
+#else
+    (void)host;
+    (void)n;
+    return false;
+#endif
+}
+
 bool gpp_read_stamps(long long* host, int n) {
 #ifdef BPE_GPP_STAMPS
     (void)hipDeviceSynchronize();

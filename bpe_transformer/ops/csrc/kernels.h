@@ -187,6 +187,8 @@ int fa_dq_config(int form);
 bool fa_read_stamps(long long* host, int n);
 // per-workgroup s_memtime stamps of the last gemm_pp launch (BPE_GPP_STAMPS builds only; false otherwise)
 bool gpp_read_stamps(long long* host, int n);
+// per-wave phase stamps of the last one-tile gemm_pp launch (BPE_GPP_PHASE_STAMPS builds only; false otherwise)
+bool gpp_read_phase_stamps(long long* host, int n);
 // gemm_pp: 1 = persistent kernel for the one-pass bf16 / fp8 GEMMs, 0 = one tile per workgroup; -1 queries.
 // Returns the previous mode.
 int gpp_persist_config(int mode);

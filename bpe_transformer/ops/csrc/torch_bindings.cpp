@@ -772,6 +772,14 @@ at::Tensor fa_stamps_op(int64_t n) {
     return t;
 }
 // the same for the last gemm_pp kernel (a BPE_GPP_STAMPS variant build)
+// phase stamps (BPE_GPP_PHASE_STAMPS builds): [n workgroups][8 waves][4 K-tiles][4 phases][4 events]
+at::Tensor gpp_phase_stamps_op(int64_t n) {
+    auto t = at::empty({n, 8, 4, 4, 4}, at::TensorOptions().dtype(at::kLong));
+    if (!gpp_read_phase_stamps(reinterpret_cast<long long*>(t.data_ptr<int64_t>()), (int)n))
+        return at::empty({0, 8, 4, 4, 4}, t.options());
+    return t;
+}
+
 at::Tensor gpp_stamps_op(int64_t n) {
     auto t = at::empty({n, 8}, at::TensorOptions().dtype(at::kLong));
     if (!gpp_read_stamps(reinterpret_cast<long long*>(t.data_ptr<int64_t>()), (int)n)) return at::empty({0, 8}, t.options());
@@ -1084,6 +1092,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("fa_dq_config(int form=-1) -> int", &fa_dq_config_op);
     m.def("fa_stamps(int n) -> Tensor", &fa_stamps_op);
     m.def("gpp_stamps(int n) -> Tensor", &gpp_stamps_op);
+    m.def("gpp_phase_stamps(int n) -> Tensor", &gpp_phase_stamps_op);
     m.def("gpp_persist_config(int mode=-1) -> int", &gpp_persist_config_op);
     m.def("fa_fwd_config(int ver=0) -> int", &fa_fwd_config_op);
 }

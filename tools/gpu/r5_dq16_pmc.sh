@@ -20,3 +20,5 @@ for F in 0 1; do
   BPE_HIP_VARIANT=stamps timeout -k 10 120 python3 benchmarks/attn_stamps.py --dq-form $F --batch 32 --seq 2048 --heads 32 --kv-heads 4 > gpurun_out/attn_stamps_llama_f$F.log 2>&1 || exit $?
 done
 cat gpurun_out/attn_stamps_f*.log
+BPE_HIP_VARIANT=pstamps timeout -k 10 180 python3 benchmarks/gemm_phase_stamps.py > gpurun_out/gemm_phase_stamps.log 2>&1 || exit $?
+cat gpurun_out/gemm_phase_stamps.log
