@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--heads", type=int, default=12)
     ap.add_argument("--kv-heads", type=int, default=None)
-    ap.add_argument("--dq-form", type=int, default=0, help="ops.fa_dq_config: 0 = 32 queries per wave, 1 = 16")
+    ap.add_argument("--dq-form", type=int, default=0, help="ops.fa_dq_config: 0 = 32 queries per wave, 1 = 16 (8 waves), 2 = 16 (4 waves)")
     a = ap.parse_args()
     h = ops()
     h.fa_dq_config(a.dq_form)
@@ -42,7 +42,8 @@ def main():
     if st.numel() == 0:
         sys.exit("not a BPE_FA_STAMPS build: set BPE_HIP_VARIANT=stamps (ops.build --variant stamps -D BPE_FA_STAMPS)")
     nblk = (S + 127) // 128
-    for name, base, n in (("dQ", 0, nblk * B * H), ("dK/dV", 32768, nblk * B * Hkv)):
+    qb = 64 if a.dq_form == 2 else 128  # queries per dQ workgroup
+    for name, base, n in (("dQ", 0, min(32768, (S + qb - 1) // qb * B * H)), ("dK/dV", 32768, nblk * B * Hkv)):
         r = st[base : base + n]
         # slot 2 = start of the last (diagonal) tile; the epilogue is not stamped (entry .. slot 3)
         dur, pro, nt = r[:, 3] - r[:, 0], r[:, 1] - r[:, 0], r[:, 5]

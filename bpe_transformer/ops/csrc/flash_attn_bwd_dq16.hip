@@ -26,15 +26,17 @@
 #include "fa_common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace bpe {
 namespace fa {
 namespace dq16 {
 
-constexpr int NW = 8;            // waves per workgroup, 16 queries each
-constexpr int QB = 16 * NW;      // queries per workgroup
-constexpr int KT = 128;          // keys per K / V tile (two 64-row images)
+// Two geometries, both at four waves per SIMD: (NW, KT) = (8, 128) -- 128 queries per workgroup, 128-key tiles, two
+// workgroups per CU (64 KiB of LDS each) -- and (4, 64) -- 64 queries, 64-key tiles, four workgroups per CU (32 KiB):
+// while one workgroup waits in its prologue (a third of a workgroup's time at S = 1024, the stamps build) three others
+// hold the SIMDs instead of one.
 constexpr int TILE = 64 * 128;   // one 64-row image of 128-byte rows
-constexpr int BUF = 2 * TILE;    // one tile
 
 __device__ __forceinline__ int sw(int row, int c) { return row * 128 + ((c ^ (row & 6)) << 4); }
 // byte offset of the 8-byte granule at (row, col) (transposed reads)
@@ -59,29 +61,36 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 }
 
 // lane offset (bytes, inside a 64-row tile of a row-major tensor of row stride ld) of the source chunk this lane's
-// DMA slot holds: wave w's one wave-instruction per image fills physical chunks 64 w + lane
-__device__ __forceinline__ unsigned dma_lane_off(long ld, int w, int l) {
-    const int e = 64 * w + l, r = e >> 3, pc = e & 7;
-    return (unsigned)((r * ld + ((pc ^ (r & 6)) << 3)) * 2);
+// DMA slot holds: wave-instruction i of wave w (CPW per wave and image) fills physical chunks 64 (CPW w + i) + lane
+template <int CPW>
+__device__ __forceinline__ void dma_lane_off(long ld, int w, int l, unsigned (&v)[CPW]) {
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+        const int e = 64 * (CPW * w + i) + l, r = e >> 3, pc = e & 7;
+        v[i] = (unsigned)((r * ld + ((pc ^ (r & 6)) << 3)) * 2);
+    }
 }
 
-__device__ __forceinline__ void dma_image(const __bf16* base, int nbytes, unsigned voff, int r0, long ld, char* img,
-                                          int w) {
+template <int CPW>
+__device__ __forceinline__ void dma_image(const __bf16* base, int nbytes, const unsigned (&voff)[CPW], int r0, long ld,
+                                          char* img, int w) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nbytes, 0x00020000);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + 1024 * w), 16, voff,
-                                             (unsigned)((long)r0 * ld * 2), 0, 0);
+#pragma unroll
+    for (int i = 0; i < CPW; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + 1024 * (CPW * w + i)), 16, voff[i],
+                                                 (unsigned)((long)r0 * ld * 2), 0, 0);
 #endif
 }
 
-template <bool CAUSAL, bool ROPE>
-__global__ void __launch_bounds__(NW * 64, 2)
+template <int NW, int KT, bool CAUSAL, bool ROPE>
+__global__ void __launch_bounds__(NW * 64, 16 / NW)
 fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ Vv,
                    long ld_q, long ld_kv, const __bf16* __restrict__ O, long ld_o, const __bf16* __restrict__ dO,
                    long ld_do, const float* __restrict__ LSE, float* __restrict__ DELTA, __bf16* __restrict__ dQ,
                    long ld_dq, const float* __restrict__ cosT, const float* __restrict__ sinT, int B, int H, int Hkv,
                    int S, float scale_log2, float scale, int group) {
-    constexpr int D = 64;
+    constexpr int D = 64, QB = 16 * NW, NSUB = KT / 64, BUF = NSUB * TILE, CPW = 512 / (NW * 64);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* Ks = smem;            // [2][KT keys][128 B]
     char* Vs = smem + 2 * BUF;  // [2][KT keys][128 B]
@@ -116,9 +125,10 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
     const __bf16* vb = Vv + (long)b * S * ld_kv + (long)hk * D;
     const int wu = __builtin_amdgcn_readfirstlane(w);
     const int hbytes = head_bytes(ld_kv, S, D);
-    const unsigned voff = dma_lane_off(ld_kv, wu, l);
+    unsigned voff[CPW];
+    dma_lane_off<CPW>(ld_kv, wu, l, voff);
 #pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
+    for (int sb = 0; sb < NSUB; ++sb) {
         dma_image(kb, hbytes, voff, 64 * sb, ld_kv, Ks + sb * TILE, wu);
         dma_image(vb, hbytes, voff, 64 * sb, ld_kv, Vs + sb * TILE, wu);
     }
@@ -157,7 +167,7 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
                         char* __restrict__ Vn) {
             if (it + 1 < nkt) {  // buffer cur ^ 1 was last read in iteration it - 1, before its closing barrier
 #pragma unroll
-                for (int sb = 0; sb < 2; ++sb) {
+                for (int sb = 0; sb < NSUB; ++sb) {
                     dma_image(kb, hbytes, voff, k0 + KT + 64 * sb, ld_kv, Kn + sb * TILE, wu);
                     dma_image(vb, hbytes, voff, k0 + KT + 64 * sb, ld_kv, Vn + sb * TILE, wu);
                 }
@@ -255,12 +265,13 @@ using namespace bpe;
 using namespace bpe::fa;
 
 // dQ form of the split backward at D = 64 without in-kernel RoPE: 0 = 32 queries per wave (fa_bwd_dq_kernel),
-// 1 = 16 queries per wave (this file); switched at run time (tests compare the two)
+// 1 = 16 queries per wave, 8 waves, 128-key tiles, 2 = 16 queries per wave, 4 waves, 64-key tiles (this file);
+// switched at run time (tests compare them)
 static int g_dq_form = 0;
 
 int fa_dq_config(int form) {
     const int prev = g_dq_form;
-    if (form >= 0) g_dq_form = form ? 1 : 0;
+    if (form >= 0) g_dq_form = form > 2 ? 2 : form;
     return prev;
 }
 
@@ -268,7 +279,7 @@ int fa_dq_config(int form) {
 // otherwise or when the kernel is not selected)
 bool fa_read_stamps_dq16(long long* host, int n) {
 #ifdef BPE_FA_STAMPS
-    if (g_dq_form != 1) return false;
+    if (g_dq_form == 0) return false;
     (void)hipDeviceSynchronize();
     const int rows = n < 32768 ? n : 32768;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(dq16::g_stamps16), (size_t)rows * 8 * sizeof(long long), 0,
@@ -282,20 +293,25 @@ bool fa_read_stamps_dq16(long long* host, int n) {
 
 // launches the 16-row dQ kernel when selected and applicable (D = 64, rope 0 / 2); false otherwise
 bool launch_fa_bwd_dq16(const FaArgs& a, hipStream_t s) {
-    if (g_dq_form != 1 || a.D != 64 || a.rope == 1) return false;
-    const int nblk = (a.S + dq16::QB - 1) / dq16::QB;
-    const int lds = 4 * dq16::BUF;
-    auto go = [&](auto kern) {
-        kern<<<nblk * a.B * a.H, dq16::NW * 64, lds, s>>>(a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do,
-                                                          a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin, a.B, a.H,
-                                                          a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
+    if (g_dq_form == 0 || a.D != 64 || a.rope == 1) return false;
+    auto run = [&](auto nw, auto kt) {
+        constexpr int NW = decltype(nw)::value, KT = decltype(kt)::value;
+        const int nblk = (a.S + 16 * NW - 1) / (16 * NW);
+        const int lds = 2 * 2 * (KT / 64) * dq16::TILE;  // K and V, two buffers
+        auto go = [&](auto kern) {
+            kern<<<nblk * a.B * a.H, NW * 64, lds, s>>>(a.q, a.k, a.v, a.ld_q, a.ld_kv, a.o, a.ld_o, a.dout, a.ld_do,
+                                                        a.lse, a.delta, a.dq, a.ld_dq, a.cos, a.sin, a.B, a.H, a.Hkv,
+                                                        a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
+        };
+        if (a.causal) {
+            if (a.rope == 2) go(dq16::fa_bwd_dq16_kernel<NW, KT, true, true>);
+            else go(dq16::fa_bwd_dq16_kernel<NW, KT, true, false>);
+        } else {
+            if (a.rope == 2) go(dq16::fa_bwd_dq16_kernel<NW, KT, false, true>);
+            else go(dq16::fa_bwd_dq16_kernel<NW, KT, false, false>);
+        }
     };
-    if (a.causal) {
-        if (a.rope == 2) go(dq16::fa_bwd_dq16_kernel<true, true>);
-        else go(dq16::fa_bwd_dq16_kernel<true, false>);
-    } else {
-        if (a.rope == 2) go(dq16::fa_bwd_dq16_kernel<false, true>);
-        else go(dq16::fa_bwd_dq16_kernel<false, false>);
-    }
+    if (g_dq_form == 1) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 128>{});
+    else run(std::integral_constant<int, 4>{}, std::integral_constant<int, 64>{});
     return true;
 }

@@ -752,9 +752,10 @@ def _split_vs_fused(gpu_device, S, H, Hkv, D, rope, causal):
 @pytest.mark.parametrize("H,Hkv", [(4, 4), (8, 2)])
 @pytest.mark.parametrize("pre", [True, False])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_bwd_dq16_vs_dq32_and_oracle(gpu_device, S, H, Hkv, pre, causal):
+@pytest.mark.parametrize("form", [1, 2], ids=["nw8_kt128", "nw4_kt64"])
+def test_flash_bwd_dq16_vs_dq32_and_oracle(gpu_device, S, H, Hkv, pre, causal, form):
     """The split backward's dQ kernel with 16 queries per wave (flash_attn_bwd_dq16.hip: 16x16x32 MFMAs, 4 waves per
-    SIMD, its own LDS swizzle) against the 32-query kernel and the fp32 oracle's autograd: dQ within the oracle
+    SIMD, its own LDS swizzle; form 1: 8 waves and 128-key tiles, form 2: 4 waves and 64-key tiles) against the 32-query kernel and the fp32 oracle's autograd: dQ within the oracle
     bound and no worse than the 32-row kernel's error; dV bitwise equal (no delta in it); dK within fp32 rounding
     of delta's summation order; bitwise repeatable.  S 136 and 1000 cover partial query blocks and key tiles."""
     h = torch.ops.bpe_hip
@@ -769,7 +770,7 @@ def test_flash_bwd_dq16_vs_dq32_and_oracle(gpu_device, S, H, Hkv, pre, causal):
     scale = D ** -0.5
     o, lse = h.fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, causal, pre, scale, pre)
     do = torch.randn_like(o)
-    prev = h.fa_dq_config(1)
+    prev = h.fa_dq_config(form)
     try:
         g16 = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, pre, scale, pre)
         again = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, pre, scale, pre)
