@@ -52,6 +52,10 @@ def main():
               f"prologue {pro.mean():.0f} ({pro.sum() / dur.sum() * 100:.1f} %), full tiles {body.mean():.0f} "
               f"({body.sum() / dur.sum() * 100:.1f} %), last (diagonal) tile {diag.mean():.0f} "
               f"({diag.sum() / dur.sum() * 100:.1f} %)")
+        if name == "dQ" and a.dq_form > 0:  # slots 6 (loads issued) and 4 (the wave's row loads arrived)
+            iss, rows = r[:, 6] - r[:, 0], r[:, 4] - r[:, 0]
+            print(f"  prologue split (last wave): loads issued at {iss.mean():.0f}, its rows arrived at {rows.mean():.0f}, "
+                  f"barrier (tile-0 DMA, all waves) passed at {pro.mean():.0f} cycles after entry")
         for t in sorted(set(nt.tolist())):
             m = nt == t
             full = (body[m] / (t - 1)).mean() if t > 1 else float("nan")

@@ -43,8 +43,9 @@ __device__ __forceinline__ int sw(int row, int c) { return row * 128 + ((c ^ (ro
 __device__ __forceinline__ int sw_tr(int row, int col) { return sw(row, col >> 3) + ((col & 7) << 1); }
 
 // Per-workgroup s_memtime stamps (BPE_FA_STAMPS variant builds; read through fa_read_stamps, rows 0.. when this
-// kernel is selected), taken by the LAST wave (the one with the most steps on the diagonal tile): slot 0 entry, 1
-// after the prologue barrier, 2 at the start of the last tile, 3 after the tile loop, 5 the tile count
+// kernel is selected), taken by the LAST wave (the one with the most steps on the diagonal tile): slot 0 entry, 6
+// every prologue load issued, 4 its row loads arrived, 1 after the prologue barrier, 2 at the start of the last
+// tile, 3 after the tile loop, 5 the tile count
 #ifdef BPE_FA_STAMPS
 __device__ long long g_stamps16[32768 * 8];
 #define DQ16_STAMP(i, v)                                                                             \
@@ -132,6 +133,7 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
         dma_image(kb, hbytes, voff, 64 * sb, ld_kv, Ks + sb * TILE, wu);
         dma_image(vb, hbytes, voff, 64 * sb, ld_kv, Vs + sb * TILE, wu);
     }
+    DQ16_STAMP(6, 0);  // every prologue load issued
 
     // ---- pinned B operands (c folded into Q: S^T in log2 units) and delta = rowsum(dO * O)
     bf16x8 qf[2], of[2];
@@ -147,6 +149,7 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
     }
     dsum += __shfl_xor(dsum, 16, 64);
     dsum += __shfl_xor(dsum, 32, 64);
+    DQ16_STAMP(4, 0);  // the wave's own row loads have arrived (its DMA and the other waves' may not have)
     // row constants as the initial accumulators: S^T starts at -lse (-inf on pad rows: P = 0), dP^T at -delta
     const float nl = (q_ok && lse < INFINITY) ? -lse : -INFINITY;
 
@@ -266,8 +269,11 @@ using namespace bpe::fa;
 
 // dQ form of the split backward at D = 64 without in-kernel RoPE: 0 = 32 queries per wave (fa_bwd_dq_kernel),
 // 1 = 16 queries per wave, 8 waves, 128-key tiles, 2 = 16 queries per wave, 4 waves, 64-key tiles (this file);
-// switched at run time (tests compare them)
-static int g_dq_form = 0;
+// switched at run time (tests compare them).  Default 1: backward -1.1 % at GPT-2 B 128 and -1.0 % at Llama s2048
+// B 32 GQA op-level, +0.25 % end to end, both rounds of an alternating A/B on one box
+// (profiles/bench/ab_attn_dq_forms_r5.log, ab_e2e_r5.log); form 2 measured no gain (four workgroups per CU do not
+// shorten the prologue, profiles/attention_stamps_r5.md).
+static int g_dq_form = 1;
 
 int fa_dq_config(int form) {
     const int prev = g_dq_form;
