@@ -170,6 +170,22 @@ __device__ __forceinline__ void dma_tile64_buf(const __bf16* base, int nbytes, c
 #endif
 }
 
+// Prologue priority.  A workgroup that starts while its CU's other waves run their MFMA loops is the youngest there,
+// and VALU issue goes by priority, then age (MI355X_MICROARCH, two waves per SIMD, item 2): its prologue -- ~200 VALU
+// of index math (integer divisions by the grid's shape) and address set-up before the first load can issue --
+// got the leftover slots.  Stamps (profiles/attention_stamps_r5.md): the 16-row dQ kernel's last wave issued its
+// prologue loads ~6.4 k cycles after entry, its rows arrived 1.6 k later.  The prologue runs at s_setprio 3 and the
+// loop at 0 (BPE_FA_PRIO=0 builds the old form for A/B).
+#ifndef BPE_FA_PRIO
+#define BPE_FA_PRIO 1
+#endif
+__device__ __forceinline__ void prologue_prio_begin() {
+    if (BPE_FA_PRIO) __builtin_amdgcn_s_setprio(3);
+}
+__device__ __forceinline__ void prologue_prio_end() {
+    if (BPE_FA_PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
 // Launch order of the (block, batch*head) work items: heads are taken in groups of `group` (batch, head) pairs
 // and, inside a group, the `nblk` blocks of every pair run heaviest first (index 0 = heaviest).  All blocks of a
 // pair thus run close together in time, so the K / V (forward) or Q / dO (backward) rows they share are re-read

@@ -97,6 +97,7 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
     char* Vs = smem + 2 * BUF;  // [2][KT keys][128 B]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, i16 = l & 15;
+    prologue_prio_begin();
     DQ16_STAMP(0, 0);
     const int nqb = (S + QB - 1) / QB;
     int rank, bh;
@@ -158,6 +159,7 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
     for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     __syncthreads();
+    prologue_prio_end();
     DQ16_STAMP(1, 0);
 
     const int trq = i16 >> 2, trc = 4 * (i16 & 3);  // transposed read: row 4 g + trq of a block, column trc

@@ -92,6 +92,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     char* Vs = smem + 2 * BUF;  // [2][KT keys][RB]
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    prologue_prio_begin();
     FA_STAMP(0, 0, 0);
     const int nqb = (S + QB - 1) / QB;
     int rank, bh;
@@ -202,6 +203,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
 
     if constexpr (!DM) write_tile(0, 0);
     __syncthreads();
+    prologue_prio_end();
     FA_STAMP(0, 1, 0);
 
     const int trow = 4 * hh + ((l & 15) >> 2);          // tr-read row inside a 16-key step
@@ -375,6 +377,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     float* dltS = lseS + 2 * QT;                                // [2][QT]  -delta
 
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
+    prologue_prio_begin();
     FA_STAMP(32768, 0, 0);
     const int nkb = (S + KB - 1) / KB;
     // One workgroup per (batch, KV head, key block) sweeps the G = H / Hkv query heads of its group one after the
@@ -502,6 +505,7 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
 
     if (nqt > 0) write_tile(0, 0);
     __syncthreads();
+    prologue_prio_end();
     FA_STAMP(32768, 1, 0);
     const int trow = 4 * hh + ((l & 15) >> 2);
     const int tcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);

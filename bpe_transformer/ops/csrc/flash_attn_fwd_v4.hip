@@ -38,6 +38,7 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* Ks = smem;             // [2][64][128 B]
     char* Vs = smem + 2 * TILE;  // [2][64][128 B]
+    prologue_prio_begin();  // (fa_common.h)
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l31 = l & 31, hh = l >> 5;
     const int nqb = (S + 127) / 128;
     int qrank, bh;
@@ -91,6 +92,7 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         qf[ks] = __builtin_bit_cast(bf16x8, pack8(x, scale_log2));
     }
     __syncthreads();
+    prologue_prio_end();
     for (int t = 0; t < ntiles; ++t) {
         const int cur = t & 1, n0 = t * 64;
         if (t + 1 < ntiles) {  // buffer cur ^ 1 was last read in tile t - 1, before its closing barrier

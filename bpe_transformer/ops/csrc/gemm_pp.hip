@@ -241,6 +241,24 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const Frags& f,
     if constexpr (F8 != 0) pin_quadrant(acc, m, n, 0, 4);
 }
 
+// i-blocks [ib0, ib1) of quadrant (m, n)
+template <int F8 = 0>
+__device__ __forceinline__ void mma_range(f32x4 (&acc)[8][4], const Frags& f, int m, int n, int ib0, int ib1) {
+#pragma unroll
+    for (int ib = ib0; ib < ib1; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+            if constexpr (F8 != 0) {
+                acc[4 * m + ib][2 * n + jb] = mfma_f8<F8>(f.b[jb], f.a[ib], acc[4 * m + ib][2 * n + jb]);
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+                    acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
+            }
+        }
+    if constexpr (F8 != 0) pin_quadrant(acc, m, n, ib0, ib1);
+}
+
 // Half of a quadrant (i-blocks 2h, 2h+1): the MFMA section can then issue one DMA piece between its halves.
 template <int F8 = 0>
 __device__ __forceinline__ void mma_half(f32x4 (&acc)[8][4], const Frags& f, int m, int n, int h) {
@@ -273,12 +291,12 @@ __device__ __forceinline__ void mma_half(f32x4 (&acc)[8][4], const Frags& f, int
 // sched_group_barriers keep the reads between the MFMAs (without them the scheduler may hoist all eight ahead of
 // the section, 32 more live registers).
 template <bool AK, int F8 = 0>
-__device__ __forceinline__ void mma_half_pre(f32x4 (&acc)[8][4], Frags& f, int m, int n, int h, char* nxtA, int g,
-                                             int l) {
+__device__ __forceinline__ void mma_range_pre(f32x4 (&acc)[8][4], Frags& f, int m, int n, int ib0, int ib1,
+                                              char* nxtA, int g, int l) {
     constexpr int NMF = F8 != 0 ? 2 : 4;   // MFMAs per i-block
     constexpr int NRD = AK ? 2 : 4;        // LDS read instructions per i-block (2 fragments; MN-major: tr pairs)
 #pragma unroll
-    for (int ib = 2 * h; ib < 2 * h + 2; ++ib) {
+    for (int ib = ib0; ib < ib1; ++ib) {
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
             if constexpr (F8 != 0) {
@@ -296,6 +314,17 @@ __device__ __forceinline__ void mma_half_pre(f32x4 (&acc)[8][4], Frags& f, int m
         __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
     }
 }
+
+// EARLYBAR: the barrier that ends a group's MFMA section is issued before the section's last i-block (4 bf16 / 2
+// fp8 MFMAs, ~64 cycles of the pipe).  At every barrier one group ends its MFMAs and the other its loads; with the
+// barrier after the last MFMA issue the matrix pipe drains while the barrier resolves and the partner's first MFMA
+// issues (~90 cycles per interval, the phase stamps' hand-off).  Issued early, the partner's first MFMAs queue
+// behind these.  Legal: the barrier orders LDS accesses between the groups, and an MFMA section touches no LDS
+// (PREA's reads of the next K-tile's image after it read bytes that were retired before phase 3's first barrier and
+// are next overwritten two K-tiles later).
+#ifndef BPE_GPP_EARLYBAR  // build define: i-blocks issued after the closing barrier (0 = the barrier after them all)
+#define BPE_GPP_EARLYBAR 1
+#endif
 
 // One K-tile: four (load section, barrier, MFMA section, barrier) phases.  `cur` is read, `nxt` is the DMA
 // target (the __restrict__ parameters let the wait-count pass see that the fragment reads do not alias the
@@ -457,24 +486,26 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
         bar();
         PST(ph, 2);
         const bool pre = PRE && m == 1 && n == 0;  // phase 3 (m, n are compile-time after inlining)
+        constexpr int EB = BPE_GPP_EARLYBAR;       // i-blocks after the closing barrier
+        auto mm = [&](int ib0, int ib1) {
+            if (ib0 >= ib1) return;
+            if (pre) mma_range_pre<AK, F8>(acc, f, m, n, ib0, ib1, nxt, g, l);
+            else mma_range<F8>(acc, f, m, n, ib0, ib1);
+        };
         if constexpr (SPLIT) {
-            if (pre) mma_half_pre<AK, F8>(acc, f, m, n, 0, nxt, g, l);
-            else mma_half<F8>(acc, f, m, n, 0);
+            mm(0, 2);
             if (dma) {
                 __builtin_amdgcn_sched_barrier(0);
                 dma_one(t0, off[1], img, lb + 64);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            if (pre) mma_half_pre<AK, F8>(acc, f, m, n, 1, nxt, g, l);
-            else mma_half<F8>(acc, f, m, n, 1);
-        } else if (pre) {
-            mma_half_pre<AK, F8>(acc, f, m, n, 0, nxt, g, l);
-            mma_half_pre<AK, F8>(acc, f, m, n, 1, nxt, g, l);
+            mm(2, 4 - EB);
         } else {
-            mma_quadrant<F8>(acc, f, m, n);
+            mm(0, 4 - EB);
         }
         PST(ph, 3);
         bar();
+        mm(4 - EB, 4);
     };
     // phase 0: (m0, n0)
     PST(0, 0);
