@@ -259,23 +259,6 @@ __device__ __forceinline__ void mma_range(f32x4 (&acc)[8][4], const Frags& f, in
     if constexpr (F8 != 0) pin_quadrant(acc, m, n, ib0, ib1);
 }
 
-// Half of a quadrant (i-blocks 2h, 2h+1): the MFMA section can then issue one DMA piece between its halves.
-template <int F8 = 0>
-__device__ __forceinline__ void mma_half(f32x4 (&acc)[8][4], const Frags& f, int m, int n, int h) {
-#pragma unroll
-    for (int ib = 2 * h; ib < 2 * h + 2; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            if constexpr (F8 != 0) {
-                acc[4 * m + ib][2 * n + jb] = mfma_f8<F8>(f.b[jb], f.a[ib], acc[4 * m + ib][2 * n + jb]);
-            } else {
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks)
-                    acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
-            }
-        }
-    if constexpr (F8 != 0) pin_quadrant(acc, m, n, 2 * h, 2 * h + 2);
-}
 
 // PREA: the next K-tile's phase-0 A fragments (the m0 half) are read during phase 3's MFMA section, each i-block
 // into the registers its last MFMA just read, so phase 0's load section reads only its B half (4 ds_read instead of
@@ -315,16 +298,9 @@ __device__ __forceinline__ void mma_range_pre(f32x4 (&acc)[8][4], Frags& f, int 
     }
 }
 
-// EARLYBAR: the barrier that ends a group's MFMA section is issued before the section's last i-block (4 bf16 / 2
-// fp8 MFMAs, ~64 cycles of the pipe).  At every barrier one group ends its MFMAs and the other its loads; with the
-// barrier after the last MFMA issue the matrix pipe drains while the barrier resolves and the partner's first MFMA
-// issues (~90 cycles per interval, the phase stamps' hand-off).  Issued early, the partner's first MFMAs queue
-// behind these.  Legal: the barrier orders LDS accesses between the groups, and an MFMA section touches no LDS
-// (PREA's reads of the next K-tile's image after it read bytes that were retired before phase 3's first barrier and
-// are next overwritten two K-tiles later).
-#ifndef BPE_GPP_EARLYBAR  // build define: i-blocks issued after the closing barrier (0 = the barrier after them all)
-#define BPE_GPP_EARLYBAR 1
-#endif
+// (Measured and dropped, round 5: issuing the barrier that ends a group's MFMA section before its last i-block, so
+// the partner's first MFMAs would queue behind it -- GPT-2 GEMMs 6-10 % slower op-level, -1.3 % end to end,
+// profiles/bench/ab_r5_earlybar_prio.log.)
 
 // One K-tile: four (load section, barrier, MFMA section, barrier) phases.  `cur` is read, `nxt` is the DMA
 // target (the __restrict__ parameters let the wait-count pass see that the fragment reads do not alias the
@@ -486,9 +462,7 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
         bar();
         PST(ph, 2);
         const bool pre = PRE && m == 1 && n == 0;  // phase 3 (m, n are compile-time after inlining)
-        constexpr int EB = BPE_GPP_EARLYBAR;       // i-blocks after the closing barrier
         auto mm = [&](int ib0, int ib1) {
-            if (ib0 >= ib1) return;
             if (pre) mma_range_pre<AK, F8>(acc, f, m, n, ib0, ib1, nxt, g, l);
             else mma_range<F8>(acc, f, m, n, ib0, ib1);
         };
@@ -499,13 +473,12 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
                 dma_one(t0, off[1], img, lb + 64);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            mm(2, 4 - EB);
+            mm(2, 4);
         } else {
-            mm(0, 4 - EB);
+            mm(0, 4);
         }
         PST(ph, 3);
         bar();
-        mm(4 - EB, 4);
     };
     // phase 0: (m0, n0)
     PST(0, 0);
