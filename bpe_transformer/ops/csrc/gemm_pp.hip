@@ -47,7 +47,6 @@
 #include "kernels.h"
 
 #include <cstdlib>
-#include <type_traits>
 
 namespace bpe {
 namespace gpp {
@@ -241,45 +240,11 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const Frags& f,
     if constexpr (F8 != 0) pin_quadrant(acc, m, n, 0, 4);
 }
 
-// i-blocks [ib0, ib1) of quadrant (m, n)
+// Half of a quadrant (i-blocks 2h, 2h+1): the MFMA section can then issue one DMA piece between its halves.
 template <int F8 = 0>
-__device__ __forceinline__ void mma_range(f32x4 (&acc)[8][4], const Frags& f, int m, int n, int ib0, int ib1) {
+__device__ __forceinline__ void mma_half(f32x4 (&acc)[8][4], const Frags& f, int m, int n, int h) {
 #pragma unroll
-    for (int ib = ib0; ib < ib1; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            if constexpr (F8 != 0) {
-                acc[4 * m + ib][2 * n + jb] = mfma_f8<F8>(f.b[jb], f.a[ib], acc[4 * m + ib][2 * n + jb]);
-            } else {
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks)
-                    acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
-            }
-        }
-    if constexpr (F8 != 0) pin_quadrant(acc, m, n, ib0, ib1);
-}
-
-
-// PREA: the next K-tile's phase-0 A fragments (the m0 half) are read during phase 3's MFMA section, each i-block
-// into the registers its last MFMA just read, so phase 0's load section reads only its B half (4 ds_read instead of
-// 12).  Measured with the phase stamps (benchmarks/gemm_phase_stamps.py, profiles/bench/gemm_phase_stamps_r5.log):
-// phase 0's load section was 1.6-2.4x the others and its loaders reached the barrier ~300 cycles after the
-// partner's last MFMA, at every phase-0 barrier; at phases 1-3 the MFMA side was the later one.
-#ifndef BPE_GPP_PREA  // build define: 0 = phase 0 reads both halves (A / B variant builds)
-#define BPE_GPP_PREA 1
-#endif
-
-// The MFMAs of i-blocks 2h, 2h+1 of quadrant (m, n), each followed by the reads of the NEXT K-tile's A fragments of
-// that i-block of the m0 half (image nxtA) into the registers the i-block's MFMAs just consumed.  The
-// sched_group_barriers keep the reads between the MFMAs (without them the scheduler may hoist all eight ahead of
-// the section, 32 more live registers).
-template <bool AK, int F8 = 0>
-__device__ __forceinline__ void mma_range_pre(f32x4 (&acc)[8][4], Frags& f, int m, int n, int ib0, int ib1,
-                                              char* nxtA, int g, int l) {
-    constexpr int NMF = F8 != 0 ? 2 : 4;   // MFMAs per i-block
-    constexpr int NRD = AK ? 2 : 4;        // LDS read instructions per i-block (2 fragments; MN-major: tr pairs)
-#pragma unroll
-    for (int ib = ib0; ib < ib1; ++ib) {
+    for (int ib = 2 * h; ib < 2 * h + 2; ++ib)
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
             if constexpr (F8 != 0) {
@@ -290,17 +255,14 @@ __device__ __forceinline__ void mma_range_pre(f32x4 (&acc)[8][4], Frags& f, int 
                     acc[4 * m + ib][2 * n + jb] = mfma16(f.b[jb][ks], f.a[ib][ks], acc[4 * m + ib][2 * n + jb]);
             }
         }
-        if constexpr (F8 != 0) pin_quadrant(acc, m, n, ib, ib + 1);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) f.a[ib][ks] = frag<AK, true>(nxtA, 8 * g + ib, ks, l);
-        __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
-    }
+    if constexpr (F8 != 0) pin_quadrant(acc, m, n, 2 * h, 2 * h + 2);
 }
 
-// (Measured and dropped, round 5: issuing the barrier that ends a group's MFMA section before its last i-block, so
-// the partner's first MFMAs would queue behind it -- GPT-2 GEMMs 6-10 % slower op-level, -1.3 % end to end,
-// profiles/bench/ab_r5_earlybar_prio.log.)
+// (Measured and dropped, round 5 (docs/performance.md, ping-pong phase stamps): reading the next K-tile's phase-0 A
+// fragments inside phase 3's MFMA section, so phase 0 reads only its B half -- the loaders' lateness at phase 0
+// halved in the stamps build, but GPT-2 GEMMs moved -1 to +1 % and the Llama SwiGLU / fp8 GEMMs lost 0.7-1.4 %,
+// profiles/bench/ab_r5_prea_fused.log; and issuing the barrier that ends an MFMA section before its last i-block --
+// 6-10 % slower, profiles/bench/ab_r5_earlybar_prio.log.)
 
 // One K-tile: four (load section, barrier, MFMA section, barrier) phases.  `cur` is read, `nxt` is the DMA
 // target (the __restrict__ parameters let the wait-count pass see that the fragment reads do not alias the
@@ -422,16 +384,12 @@ __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2
 // pieces of that image, so they wait for LDS only; phases 2-3 retire the first pieces of K-tile 1 (read before any
 // wait of K-tile 1) as always.  In the persistent kernel this lets the previous tile's epilogue stores, which
 // share the vmcnt counter with the DMA, drain during the first two phases instead of before them.
-// HAVE_A0: the previous K-tile's phase 3 read this K-tile's m0 A fragments (PREA; the callers peel K-tile 0, so
-// this is a compile-time fact and no fragment register lives across a tile's epilogue).  With PREA every K-tile's
-// phase 3 reads the next K-tile's (its image is in nxt, retired by phase 3's wait + barrier: this group's own DMA
-// pieces) -- on the last K-tile of a tile stale or next-tile bytes that nothing uses (no branch in the section).
-template <bool AK, bool BKM, int DIAG, bool SPLIT = false, int F8 = 0, bool HAVE_A0 = false>
+template <bool AK, bool BKM, int DIAG, bool SPLIT = false, int F8 = 0>
 __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __restrict__ nxt, bool dma,
                                              const __bf16* an, const __bf16* bn, const SpreadOff& so, int g, int wl,
-                                             int l, f32x4 (&acc)[8][4], Frags& f, bool first, int kt_idx = -1) {
+                                             int l, f32x4 (&acc)[8][4], bool first = false, int kt_idx = -1) {
     (void)kt_idx;  // phase stamps builds only
-    constexpr bool PRE = BPE_GPP_PREA != 0;
+    Frags f;
     char* Ac = cur;
     char* Bc = cur + OPB;
     if (DIAG == 1) dma = false;
@@ -461,28 +419,23 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
         PST(ph, 1);
         bar();
         PST(ph, 2);
-        const bool pre = PRE && m == 1 && n == 0;  // phase 3 (m, n are compile-time after inlining)
-        auto mm = [&](int ib0, int ib1) {
-            if (pre) mma_range_pre<AK, F8>(acc, f, m, n, ib0, ib1, nxt, g, l);
-            else mma_range<F8>(acc, f, m, n, ib0, ib1);
-        };
         if constexpr (SPLIT) {
-            mm(0, 2);
+            mma_half<F8>(acc, f, m, n, 0);
             if (dma) {
                 __builtin_amdgcn_sched_barrier(0);
                 dma_one(t0, off[1], img, lb + 64);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            mm(2, 4);
+            mma_half<F8>(acc, f, m, n, 1);
         } else {
-            mm(0, 4);
+            mma_quadrant<F8>(acc, f, m, n);
         }
         PST(ph, 3);
         bar();
     };
     // phase 0: (m0, n0)
     PST(0, 0);
-    if (!(PRE && HAVE_A0)) load_a<AK, BKM, true>(f, Ac, g, 0, l);
+    load_a<AK, BKM, true>(f, Ac, g, 0, l);
     load_b<AK, BKM, true>(f, Bc, wl, 0, l);
     phase(an, so.a0, nxt, so.la0, 0, 0, true);
     // phase 1: (m0, n1)
@@ -765,20 +718,12 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
         }
         GPP_STAMP(1);
         if (g == 1) bar();  // the stagger
-        Frags fr;
-        {  // K-tile 0 peeled (its A fragments are read in its own phase 0)
-            const long k1 = (long)(kb + 1) * BK;
-            ktile_spread<AK, BKM, DIAG, SPREAD == 2, F8, false>(smem, smem + STAGE, 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
-                                                                tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc, fr,
-                                                                false, 0);
-        }
-        for (int kt = 1; kt < nk; ++kt) {
+        for (int kt = 0; kt < nk; ++kt) {
             char* cur = smem + (kt & 1) * STAGE;
             char* nxt = smem + ((kt + 1) & 1) * STAGE;
             const long k1 = (long)(kb + kt + 1) * BK;
-            ktile_spread<AK, BKM, DIAG, SPREAD == 2, F8, true>(cur, nxt, kt + 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
-                                                               tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc, fr,
-                                                               false, kt);
+            ktile_spread<AK, BKM, DIAG, SPREAD == 2, F8>(cur, nxt, kt + 1 < nk, tile_ptr<AK>(A, lda, i0, k1),
+                                                         tile_ptr<BKM>(B, ldb, jb, k1), so, g, wl, l, acc, false, kt);
         }
     } else {
         int oa[4], ob[4];
@@ -904,7 +849,6 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
     }
     int st = 0;  // the stage holding the current K-tile
     f32x4 acc[8][4];
-    Frags fr;
 #ifdef BPE_GPP_STAMPS
     unsigned xcc_id, hw_id;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
@@ -929,21 +873,16 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
             for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (g == 1) bar();  // the stagger
         GPP_STAMP_T(t, 1);
-        // K-tile kt: (kt == 0: peeled, reads its own A fragments; the prefetch of the last K-tile reads the next
-        // tile's K-tile 0, which that tile's peeled K-tile 0 re-reads: no fragment register lives across the epilogue)
-        auto step = [&](int kt, auto have_a0) {
+        for (int kt = 0; kt < nk; ++kt) {
             char* cur = smem + st * STAGE;
             char* nxt = smem + (st ^ 1) * STAGE;
             const bool last = kt + 1 == nk;
             // the next K-tile of this tile, or K-tile 0 of the next tile
             const __bf16* an = last ? tile_ptr<AK>(A, lda, i0n, 0) : tile_ptr<AK>(A, lda, i0, (long)(kt + 1) * BK);
             const __bf16* bn = last ? tile_ptr<BKM>(B, ldb, jbn, 0) : tile_ptr<BKM>(B, ldb, jb, (long)(kt + 1) * BK);
-            ktile_spread<AK, BKM, 0, SPREAD == 2, F8, decltype(have_a0)::value>(cur, nxt, !last || more, an, bn, so, g,
-                                                                                wl, l, acc, fr, kt == 0);
+            ktile_spread<AK, BKM, 0, SPREAD == 2, F8>(cur, nxt, !last || more, an, bn, so, g, wl, l, acc, kt == 0);
             st ^= 1;
-        };
-        step(0, std::false_type{});
-        for (int kt = 1; kt < nk; ++kt) step(kt, std::true_type{});
+        }
         GPP_STAMP_T(t, 2);
         if (g == 0) bar();
         // the next tile's K-tile 0 (stage st) retired; the stage just read (st ^ 1) is free for the staging
