@@ -91,21 +91,18 @@ def main():
             return
     if a.bwd_ab:
         # (backward form, dQ form): split with the 32- or 16-queries-per-wave dQ kernel (ops.fa_dq_config)
-        # (backward form, dQ form, dK/dV form)
-        arms = {"fused": (1, 0, 0), "split": (0, 0, 0), "split_dq16": (0, 1, 0), "split_dq16_nw4": (0, 2, 0),
-                "split_dq16_dkv16": (0, 1, 1)}
+        # (backward form, dQ form)
+        arms = {"fused": (1, 0), "split": (0, 0), "split_dq16": (0, 1), "split_dq16_nw4": (0, 2)}
         if a.bwd_arms:
             arms = {n: arms[n] for n in a.bwd_arms}
         prev = hip.fa_bwd_config(-1)
         prev_dq = hip.fa_dq_config(-1)
-        prev_dkv = hip.fa_dkv_config(-1)
         times = {k: [] for k in arms}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for _ in range(a.rounds):
-            for name, (cfg, dqf, dkvf) in arms.items():
+            for name, (cfg, dqf) in arms.items():
                 hip.fa_bwd_config(cfg)
                 hip.fa_dq_config(dqf)
-                hip.fa_dkv_config(dkvf)
                 bwd(o, lse)
                 ev[0].record()
                 for _ in range(a.iters):
@@ -115,7 +112,6 @@ def main():
                 times[name].append(ev[0].elapsed_time(ev[1]) / a.iters)
         hip.fa_bwd_config(prev)
         hip.fa_dq_config(prev_dq)
-        hip.fa_dkv_config(prev_dkv)
         for name, t in times.items():
             t = sorted(t)
             print(json.dumps({"shape": [B, S, H, Hkv, D], "arm": name, "bwd_ms_median": round(t[len(t) // 2], 4),

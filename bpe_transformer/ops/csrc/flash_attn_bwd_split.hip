@@ -671,7 +671,6 @@ static void split_launch(const FaArgs& a, hipStream_t s) {
             a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.H));
     // Q / dO buffers + the -lse / -delta rows
     const int lds = 4 * TILE * NSUB + 16 * 64 * NSUB;
-    if (!launch_fa_bwd_dkv16(a, s))  // the 16-keys-per-wave kernel when selected (fa_dkv_config)
     split::fa_bwd_dkv_kernel<D, C, R, RIN><<<nblk * a.B * a.Hkv, split::NW * 64, lds, s>>>(
         a.q, a.k, a.v, a.ld_q, a.ld_kv, a.dout, a.ld_do, a.lse, a.delta, a.dk, a.dv, a.ld_dkv, a.cos,
         a.sin, a.B, a.H, a.Hkv, a.S, a.scale * LOG2E, a.scale, fa_group(a.B * a.Hkv));

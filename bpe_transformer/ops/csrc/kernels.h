@@ -182,11 +182,6 @@ int fa_bwd_config(int mode);
 // 1 = 16; negative = unchanged; returns the form in force before the call
 bool launch_fa_bwd_dq16(const FaArgs& a, hipStream_t s);
 bool fa_read_stamps_dq16(long long* host, int n);
-// flash_attn_bwd_dkv16.hip: the split backward's dK/dV kernel with 16 keys per wave (D = 64, rope 0 / 2) when
-// fa_dkv_config(1) selected it; false otherwise.  fa_dkv_config: 0 = 32 keys per wave, 1 = 16; negative = unchanged;
-// returns the form in force before the call
-bool launch_fa_bwd_dkv16(const FaArgs& a, hipStream_t s);
-int fa_dkv_config(int form);
 int fa_dq_config(int form);
 // per-workgroup s_memtime stamps of the last split-backward launch (BPE_FA_STAMPS builds only; false otherwise)
 bool fa_read_stamps(long long* host, int n);

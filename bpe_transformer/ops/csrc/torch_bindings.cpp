@@ -764,7 +764,6 @@ bool fa_bwd_needs_dq_acc(int64_t D) { return !fa_bwd_split_active((int)D, 2); }
 int64_t fa_fwd_config_op(int64_t ver) { return fa_fwd_config((int)ver); }
 int64_t fa_bwd_config_op(int64_t mode) { return fa_bwd_config((int)mode); }
 int64_t fa_dq_config_op(int64_t form) { return fa_dq_config((int)form); }
-int64_t fa_dkv_config_op(int64_t form) { return fa_dkv_config((int)form); }
 int64_t gpp_persist_config_op(int64_t mode) { return gpp_persist_config((int)mode); }
 // [n, 8] int64 stamps of the last split-backward kernel (a BPE_FA_STAMPS variant build), or an empty tensor
 at::Tensor fa_stamps_op(int64_t n) {
@@ -1091,7 +1090,6 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("fa_bwd_needs_dq_acc(int D) -> bool", &fa_bwd_needs_dq_acc);  // no tensors: a catch-all kernel
     m.def("fa_bwd_config(int mode=-1) -> int", &fa_bwd_config_op);
     m.def("fa_dq_config(int form=-1) -> int", &fa_dq_config_op);
-    m.def("fa_dkv_config(int form=-1) -> int", &fa_dkv_config_op);
     m.def("fa_stamps(int n) -> Tensor", &fa_stamps_op);
     m.def("gpp_stamps(int n) -> Tensor", &gpp_stamps_op);
     m.def("gpp_phase_stamps(int n) -> Tensor", &gpp_phase_stamps_op);

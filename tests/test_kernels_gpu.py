@@ -792,48 +792,6 @@ def test_flash_bwd_dq16_vs_dq32_and_oracle(gpu_device, S, H, Hkv, pre, causal, f
     assert e16 < 3e-2 and e16 < 1.2 * e32 + 2e-3, (e16, e32)
 
 
-@pytest.mark.parametrize("S", [1024, 200, 64, 1000, 136])
-@pytest.mark.parametrize("H,Hkv", [(4, 4), (8, 2), (32, 4)])
-@pytest.mark.parametrize("pre", [True, False])
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_bwd_dkv16_vs_dkv32_and_oracle(gpu_device, S, H, Hkv, pre, causal):
-    """The split backward's dK/dV kernel with 16 keys per wave (flash_attn_bwd_dkv16.hip: 16x16x32 MFMAs, 4 waves per
-    SIMD, the c ^ (r & 6) image, GQA head sweep) against the 32-key kernel and the fp32 oracle's autograd: dK and dV
-    within the oracle bound and no worse than the 32-key kernel's error, dQ bitwise equal (same dQ kernel, same
-    delta), bitwise repeatable.  S 136 / 1000 / 200 cover partial key blocks and query tiles."""
-    h = torch.ops.bpe_hip
-    B, D = 2, 64
-    torch.manual_seed(19)
-    qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device=gpu_device, dtype=torch.bfloat16)
-    cos, sin = R.rope_tables(D, S + 5, 10000.0, device=gpu_device)
-    x = qkv.clone()
-    if pre:
-        h.rope_qk_(x, cos, sin, B, S, H, Hkv, D)
-    q, k, v = x[:, : H * D], x[:, H * D : (H + Hkv) * D], x[:, (H + Hkv) * D :]
-    scale = D ** -0.5
-    o, lse = h.fa_fwd(q, k, v, cos, sin, B, S, H, Hkv, D, causal, pre, scale, pre)
-    do = torch.randn_like(o)
-    prev = h.fa_dkv_config(1)
-    try:
-        g16 = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, pre, scale, pre)
-        again = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, pre, scale, pre)
-        h.fa_dkv_config(0)
-        g32 = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, pre, scale, pre)
-    finally:
-        h.fa_dkv_config(prev)
-    assert torch.equal(g16, again), "dkv16 backward is not deterministic"
-    HD, KD = H * D, Hkv * D
-    assert torch.equal(g16[:, :HD], g32[:, :HD]), "dQ differs between the dK/dV forms"
-    qr = qkv.float().cpu().requires_grad_(True)
-    orf = ops.attention_qkv_reference(qr, B, S, H, Hkv, D, cos.cpu() if pre else None, sin.cpu() if pre else None,
-                                      causal)
-    orf.backward(do.float().cpu())
-    for name, sl in (("dk", slice(HD, HD + KD)), ("dv", slice(HD + KD, HD + 2 * KD))):
-        e16 = rel(g16[:, sl].float().cpu(), qr.grad[:, sl])
-        e32 = rel(g32[:, sl].float().cpu(), qr.grad[:, sl])
-        assert e16 < 3e-2 and e16 < 1.2 * e32 + 2e-3, (name, e16, e32)
-
-
 @pytest.mark.parametrize("S,H,Hkv", [(1024, 8, 2), (200, 32, 4), (1000, 4, 1)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_bwd_gqa_head_sweep(gpu_device, S, H, Hkv, causal):
