@@ -45,6 +45,27 @@ def main():
             m = statistics.median(t[k])
             print(json.dumps({"shape": [T, N], "op": k, "us": round(m * 1e3, 1),
                               "TBps": round(T * N * bpe / m / 1e9, 2)}), flush=True)
+    # the SwiGLU + two-layout casts at Llama width (gu = [g | u], F = 5632): forward reads gu and writes a8 / a8t
+    # (2F + 2F bytes per token... 4F + 2F), backward also reads dA and writes both layouts of [dg | du]
+    T, F = 65536, 5632
+    gu = torch.randn(T, 2 * F, device="cuda", dtype=torch.bfloat16)
+    da = torch.randn(T, F, device="cuda", dtype=torch.bfloat16)
+    s = torch.ones(1, device="cuda")
+    am = torch.zeros(1, dtype=torch.int32, device="cuda")
+    a8 = torch.empty(T, F, dtype=torch.float8_e4m3fn, device="cuda")
+    a8t = torch.empty(F, T, dtype=torch.float8_e4m3fn, device="cuda")
+    g8 = torch.empty(T, 2 * F, dtype=torch.float8_e5m2, device="cuda")
+    g8t = torch.empty(2 * F, T, dtype=torch.float8_e5m2, device="cuda")
+    arms = {"swiglu_cast_fwd": (lambda: h.swiglu_cast_fp8_t(gu, None, s, a8, a8t, am), T * F * (4 + 2)),
+            "swiglu_cast_bwd": (lambda: h.swiglu_cast_fp8_t(gu, da, s, g8, g8t, am), T * F * (4 + 2 + 4))}
+    t = {k: [] for k in arms}
+    for _ in range(3):
+        for k, (fn, _) in arms.items():
+            t[k].append(timeit(fn))
+    for k, (_, nbytes) in arms.items():
+        m = statistics.median(t[k])
+        print(json.dumps({"shape": [T, F], "op": k, "us": round(m * 1e3, 1), "TBps": round(nbytes / m / 1e9, 2)}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -146,6 +146,26 @@ __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const __bf16* __restric
 // 4 kq .. 4 kq + 3 (kq = t >> 3) over tile rows 16 ns .. 16 ns + 15 (ns = t & 7): the 8 ns of one kq are adjacent
 // lanes, so one store instruction of a wave writes 8 whole 128-byte output rows.  LDS word column c of tile row n
 // sits at c ^ sw(n), so the column reads of a 32-lane half (4 kq x 8 ns) hit 32 distinct banks.
+// Streaming access for the 128 x 128 casts: every byte they read is read once (the activation or gradient being
+// quantised) and every byte they write is consumed by a later GEMM from HBM (0.4-1.5 GB per tensor, past the 256 MB
+// Infinity Cache), so loads and stores carry the non-temporal hint (common.h ld_stream / st_stream; the softmax-CE
+// kernel measured 5.1 -> 5.5 TB/s with it).  BPE_FP8_NT=0 builds the plain form (A/B).
+#ifndef BPE_FP8_NT
+#define BPE_FP8_NT 1
+#endif
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u16x8 ld8(const __bf16* p) {
+    const u16x8* q = reinterpret_cast<const u16x8*>(p);
+    if constexpr (BPE_FP8_NT != 0) return __builtin_nontemporal_load(q);
+    else return *q;
+}
+__device__ __forceinline__ void st16(uint8_t* p, unsigned a, unsigned b, unsigned c, unsigned d) {
+    u32x4v* q = reinterpret_cast<u32x4v*>(p);
+    const u32x4v v = {a, b, c, d};
+    if constexpr (BPE_FP8_NT != 0) __builtin_nontemporal_store(v, q);
+    else *q = v;
+}
+
 constexpr int T128_TS = 132;  // LDS row stride (bytes): 33 words
 __device__ __forceinline__ int t128_sw(int n) { return ((n >> 4) & 7) << 2; }
 
@@ -175,7 +195,7 @@ __device__ __forceinline__ void t128_get_store(const uint8_t* tile, int kq, int 
         o[3][g] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) *reinterpret_cast<uint4*>(dst + e * ld) = uint4{o[e][0], o[e][1], o[e][2], o[e][3]};
+    for (int e = 0; e < 4; ++e) st16(dst + e * ld, o[e][0], o[e][1], o[e][2], o[e][3]);
 }
 
 // raw barrier behind lgkmcnt(0) only: LDS hand-off without waiting for outstanding global loads / stores
@@ -210,7 +230,7 @@ __global__ void __launch_bounds__(256) cast_fp8_t128_kernel(const __bf16* __rest
         const int n0 = (tt / tiles_k) * 128, k0 = (tt % tiles_k) * 128;
         const __bf16* src = w + (long)(n0 + r) * K + k0 + hc;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const u16x8*>(src + 8 * i);
+        for (int i = 0; i < 8; ++i) a[i] = ld8(src + 8 * i);
     };
     if (blockIdx.x < ntiles) load(blockIdx.x);
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -231,7 +251,7 @@ __global__ void __launch_bounds__(256) cast_fp8_t128_kernel(const __bf16* __rest
         uint8_t* dst = w8 + (long)(n0 + r) * K + k0 + hc;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<uint4*>(dst + 16 * i) = uint4{q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]};
+            st16(dst + 16 * i, q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
         lds_barrier();  // the previous tile's transposed reads are done
         t128_put(tile, q, r, hc);
         lds_barrier();
@@ -349,13 +369,13 @@ __global__ void __launch_bounds__(256) swiglu_cast_fp8_t128_kernel(const __bf16*
         u16x8 g[8], u[8], d[MODE == 1 ? 8 : 1];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            g[i] = *reinterpret_cast<const u16x8*>(row + 8 * i);
-            u[i] = *reinterpret_cast<const u16x8*>(row + F + 8 * i);
+            g[i] = ld8(row + 8 * i);
+            u[i] = ld8(row + F + 8 * i);
         }
         if constexpr (MODE == 1) {
             const __bf16* dr = dout + (long)(m0 + r) * F + f0 + hc;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) d[i] = *reinterpret_cast<const u16x8*>(dr + 8 * i);
+            for (int i = 0; i < 8; ++i) d[i] = ld8(dr + 8 * i);
         }
         unsigned q[NO][16];
 #pragma unroll
@@ -387,8 +407,7 @@ __global__ void __launch_bounds__(256) swiglu_cast_fp8_t128_kernel(const __bf16*
             uint8_t* dst = o8 + (long)(m0 + r) * W + (long)o * F + f0 + hc;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                *reinterpret_cast<uint4*>(dst + 16 * i) =
-                    uint4{q[o][4 * i], q[o][4 * i + 1], q[o][4 * i + 2], q[o][4 * i + 3]};
+                st16(dst + 16 * i, q[o][4 * i], q[o][4 * i + 1], q[o][4 * i + 2], q[o][4 * i + 3]);
         }
         lds_barrier();  // the previous tile's transposed reads are done
 #pragma unroll
