@@ -7,10 +7,14 @@
 //
 // Why: the 32-row split dQ kernel runs at mfma_util 0.29 (profiles/attention_pmc.md): each wave's 32-key step is a
 // dependency chain (S / dP MFMAs -> exp -> dS -> dQ MFMAs) and two waves per SIMD cannot cover it.  This form
-// computes the same five products with v_mfma_f32_16x16x32_bf16 on 16 queries per wave, so a wave holds half the
+// computes the same products with v_mfma_f32_16x16x32_bf16 on 16 queries per wave, so a wave holds half the
 // registers (<= 128: four waves per SIMD, two 512-thread workgroups per CU) and each SIMD has twice as many
 // independent chains to interleave.  Per 32-key step and wave: S^T and dP^T as two 16-key blocks each
 // (4 + 4 MFMAs over d = 64), dQ^T += K^T dS^T over 4 d-tiles (4 MFMAs); the same VALU per score as before.
+// Measured: backward -1.1 % (GPT-2 B 128) / -1.0 % (Llama s2048 GQA), mfma_util 0.298 vs 0.288 -- the default.  The
+// gain is small because a 16x16x32 MFMA holds the SIMD's vector issue for half its cycles (8 of 16, against 8 of 32
+// for 32x32x16), so the extra waves buy latency cover but lose VALU issue slots; the same form of the dK/dV kernel,
+// with more MFMA work per score, measured 1-2.5 % slower and was dropped (docs/performance.md).
 //
 //   S^T [key][query]  = K . (cQ)^T - lse     A = K rows (ds_read_b128), B = the pinned c*Q (query on the lane)
 //   dP^T              = V . dO^T - delta     A = V rows,                B = the pinned dO
@@ -18,11 +22,11 @@
 //   dQ^T [d][query]  += K^T . dS^T           A = K^T (two ds_read_b64_tr_b16), B = dS^T packed from the two
 //                                            accumulators in the permuted key order 16 (j >> 2) + 4 g + (j & 3)
 //
-// LDS image: 128-byte rows, chunk c of row r at c ^ (r & 6).  Both reads are conflict-free on it (a brute-force
-// search over per-row XORs, docs/performance.md): the 16-lane groups of the row reads cover rows 16 m + 0..15 at
-// chunks 4 ks + g, the transposed reads 4-row blocks 8 rows apart x one 32-byte column pair.  (The 32-row kernels'
-// image, fa_common.h swz<128>, leaves both 2-way conflicted for these fragments.)  K / V tiles of 128 keys are
-// DMA'd through buffer resources, one wave-instruction per wave and 64-row image.
+// LDS image: 128-byte rows, chunk c of row r at c ^ (r & 6).  Both fragment reads are conflict-free on it (found by
+// a search over per-row chunk XORs; SQ_LDS_BANK_CONFLICT 0, profiles/pmc/attn_dq16_pmc_r5.txt): the ds_read_b128 row
+// reads (rows 16 m + lane & 15, chunk 4 ks + lane >> 4) and the ds_read_b64_tr_b16 reads (4-row blocks 16 rows apart,
+// one 32-byte column pair).  The 32-row kernels' image (fa_common.h swz<128>) leaves both 2-way conflicted for these
+// fragments.  K / V tiles are DMA'd through buffer resources, CPW wave-instructions per wave and 64-row image.
 #include "fa_common.h"
 #include "kernels.h"
 
@@ -33,9 +37,9 @@ namespace fa {
 namespace dq16 {
 
 // Two geometries, both at four waves per SIMD: (NW, KT) = (8, 128) -- 128 queries per workgroup, 128-key tiles, two
-// workgroups per CU (64 KiB of LDS each) -- and (4, 64) -- 64 queries, 64-key tiles, four workgroups per CU (32 KiB):
-// while one workgroup waits in its prologue (a third of a workgroup's time at S = 1024, the stamps build) three others
-// hold the SIMDs instead of one.
+// workgroups per CU (64 KiB of LDS each), the default -- and (4, 64) -- 64 queries, 64-key tiles, four workgroups per
+// CU (32 KiB), meant to cover the ~30 % prologue with three other workgroups; it measured no faster (GPT-2) and 0.7-1.6 %
+// slower (Llama), the prologue staying at ~8.8 k cycles (profiles/attention_stamps_r5.md).
 constexpr int TILE = 64 * 128;   // one 64-row image of 128-byte rows
 
 __device__ __forceinline__ int sw(int row, int c) { return row * 128 + ((c ^ (row & 6)) << 4); }

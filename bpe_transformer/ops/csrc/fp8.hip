@@ -146,24 +146,14 @@ __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const __bf16* __restric
 // 4 kq .. 4 kq + 3 (kq = t >> 3) over tile rows 16 ns .. 16 ns + 15 (ns = t & 7): the 8 ns of one kq are adjacent
 // lanes, so one store instruction of a wave writes 8 whole 128-byte output rows.  LDS word column c of tile row n
 // sits at c ^ sw(n), so the column reads of a 32-lane half (4 kq x 8 ns) hit 32 distinct banks.
-// Streaming access for the 128 x 128 casts: every byte they read is read once (the activation or gradient being
-// quantised) and every byte they write is consumed by a later GEMM from HBM (0.4-1.5 GB per tensor, past the 256 MB
-// Infinity Cache), so loads and stores carry the non-temporal hint (common.h ld_stream / st_stream; the softmax-CE
-// kernel measured 5.1 -> 5.5 TB/s with it).  BPE_FP8_NT=0 builds the plain form (A/B).
-#ifndef BPE_FP8_NT
-#define BPE_FP8_NT 1
-#endif
-typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u16x8 ld8(const __bf16* p) {
-    const u16x8* q = reinterpret_cast<const u16x8*>(p);
-    if constexpr (BPE_FP8_NT != 0) return __builtin_nontemporal_load(q);
-    else return *q;
-}
+// Plain (temporal) loads and stores in the 128 x 128 casts.  Measured and dropped, round 5: the non-temporal hint
+// (common.h ld_stream / st_stream, which took the softmax-CE kernel from 5.1 to 5.5 TB/s) halved these kernels -- the
+// two-layout cast 4.5 -> 2.5 TB/s, the SwiGLU casts 4.0-4.2 -> 1.8-1.9 TB/s, the fp8 Llama step 192.0 k -> 166.6 k
+// tok/s (profiles/bench/ab_fp8_cast_nt_r5.log): their transposed stores write 16-byte pieces of many lines per
+// instruction, which non-temporal stores do not combine.
+__device__ __forceinline__ u16x8 ld8(const __bf16* p) { return *reinterpret_cast<const u16x8*>(p); }
 __device__ __forceinline__ void st16(uint8_t* p, unsigned a, unsigned b, unsigned c, unsigned d) {
-    u32x4v* q = reinterpret_cast<u32x4v*>(p);
-    const u32x4v v = {a, b, c, d};
-    if constexpr (BPE_FP8_NT != 0) __builtin_nontemporal_store(v, q);
-    else *q = v;
+    *reinterpret_cast<uint4*>(p) = uint4{a, b, c, d};
 }
 
 constexpr int T128_TS = 132;  // LDS row stride (bytes): 33 words
