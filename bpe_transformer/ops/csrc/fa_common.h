@@ -186,6 +186,15 @@ __device__ __forceinline__ void prologue_prio_end() {
     if (BPE_FA_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
+// Keep a value computed where it stands: an empty asm use (no instruction).  A kernel's pinned operands (the lane's
+// Q rows, LSE) are read only inside the tile loop, so without it hipcc sinks their loads and conversion past the
+// prologue barrier into the loop preheader: a second memory round trip after the barrier, in front of the first
+// tile (round-5 ISA: the dq16 kernel's Q rows and LSE, the 32-row dQ kernel's Q rows, the forward's Q rows).
+template <typename T>
+__device__ __forceinline__ void keep(const T& x) {
+    asm volatile("" ::"v"(x));
+}
+
 // Launch order of the (block, batch*head) work items: heads are taken in groups of `group` (batch, head) pairs
 // and, inside a group, the `nblk` blocks of every pair run heaviest first (index 0 = heaviest).  All blocks of a
 // pair thus run close together in time, so the K / V (forward) or Q / dO (backward) rows they share are re-read

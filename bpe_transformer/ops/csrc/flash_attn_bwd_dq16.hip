@@ -162,6 +162,13 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // the Q rows / LSE converted here, not after the barrier (fa_common.h keep)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        keep(qf[ks]);
+        keep(of[ks]);
+    }
+    keep(nl);
     __syncthreads();
     prologue_prio_end();
     DQ16_STAMP(1, 0);

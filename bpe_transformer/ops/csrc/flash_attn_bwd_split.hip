@@ -202,6 +202,13 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
 
     if constexpr (!DM) write_tile(0, 0);
+    // the Q rows / LSE converted here, not after the barrier (fa_common.h keep)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        keep(qf[ks]);
+        keep(of[ks]);
+    }
+    keep(nl);
     __syncthreads();
     prologue_prio_end();
     FA_STAMP(0, 1, 0);

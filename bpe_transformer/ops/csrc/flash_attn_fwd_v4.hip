@@ -90,6 +90,7 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         float x[8];
         unpack8(qr[ks], x);
         qf[ks] = __builtin_bit_cast(bf16x8, pack8(x, scale_log2));
+        keep(qf[ks]);  // converted here, not after the barrier (fa_common.h keep)
     }
     __syncthreads();
     prologue_prio_end();
