@@ -195,6 +195,17 @@ __device__ __forceinline__ void keep(const T& x) {
     asm volatile("" ::"v"(x));
 }
 
+// n / d for 0 <= n < 2^21, 1 <= d < 2^21: a float reciprocal (v_rcp_f32, 1 ulp) and one correction step -- exact,
+// since n * (1 / d) is then within 1/2 of n / d.  The kernels' prologue divisions (work-item decomposition by the
+// grid's shape) otherwise compile to the full 32-bit sequence, ~15 dependent VALU each, on the path to the first
+// load of a workgroup whose waves are the youngest on their SIMDs.
+__device__ __forceinline__ int sdiv(int n, int d) {
+    int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+    const int r = n - q * d;
+    q += (r >= d) - (r < 0);
+    return q;
+}
+
 // Launch order of the (block, batch*head) work items: heads are taken in groups of `group` (batch, head) pairs
 // and, inside a group, the `nblk` blocks of every pair run heaviest first (index 0 = heaviest).  All blocks of a
 // pair thus run close together in time, so the K / V (forward) or Q / dO (backward) rows they share are re-read
@@ -204,10 +215,10 @@ __device__ __forceinline__ void keep(const T& x) {
 // correctness).  Returns the block rank (0 = heaviest) and the pair index.
 __device__ __forceinline__ void grouped_order(int bid, int nblk, int BH, int group, int& rank, int& bh) {
     const int per = nblk * group;
-    const int g = bid / per;
+    const int g = sdiv(bid, per);
     const int r = bid - g * per;
     const int gs = min(group, BH - g * group);  // the last group may be short
-    rank = r / gs;
+    rank = sdiv(r, gs);
     bh = g * group + (r - rank * gs);
 }
 

@@ -107,7 +107,7 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
     int rank, bh;
     grouped_order((int)blockIdx.x, nqb, B * H, group, rank, bh);
     const int qblk = CAUSAL ? nqb - 1 - rank : rank;  // causal: the heaviest query blocks first
-    const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+    const int b = sdiv(bh, H), h = bh - b * H, hk = sdiv(h, sdiv(H, Hkv));
     const int q0 = qblk * QB, qw = q0 + 16 * w, q = qw + i16;
     const bool q_ok = q < S;
     const long qc = q_ok ? q : S - 1;
