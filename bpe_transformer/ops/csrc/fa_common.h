@@ -186,25 +186,10 @@ __device__ __forceinline__ void prologue_prio_end() {
     if (BPE_FA_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
-// Keep a value computed where it stands: an empty asm use (no instruction).  A kernel's pinned operands (the lane's
-// Q rows, LSE) are read only inside the tile loop, so without it hipcc sinks their loads and conversion past the
-// prologue barrier into the loop preheader: a second memory round trip after the barrier, in front of the first
-// tile (round-5 ISA: the dq16 kernel's Q rows and LSE, the 32-row dQ kernel's Q rows, the forward's Q rows).
-template <typename T>
-__device__ __forceinline__ void keep(const T& x) {
-    asm volatile("" ::"v"(x));
-}
-
-// n / d for 0 <= n < 2^21, 1 <= d < 2^21: a float reciprocal (v_rcp_f32, 1 ulp) and one correction step -- exact,
-// since n * (1 / d) is then within 1/2 of n / d.  The kernels' prologue divisions (work-item decomposition by the
-// grid's shape) otherwise compile to the full 32-bit sequence, ~15 dependent VALU each, on the path to the first
-// load of a workgroup whose waves are the youngest on their SIMDs.
-__device__ __forceinline__ int sdiv(int n, int d) {
-    int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
-    const int r = n - q * d;
-    q += (r >= d) - (r < 0);
-    return q;
-}
+// (Measured and dropped, round 5: pinning the prologue's Q rows / LSE before the barrier with an empty asm use --
+// hipcc otherwise sinks those loads into the loop preheader, after the barrier -- together with float-reciprocal
+// divisions for the work-item decomposition.  The dQ prologue shortened 8.1 k -> 7.5 k cycles, but the forward ran
+// 1.5-3.7 % and the backward 0.3-1.2 % slower, end to end -0.15 % (profiles/bench/ab_attn_keep_sdiv_r5.log).)
 
 // Launch order of the (block, batch*head) work items: heads are taken in groups of `group` (batch, head) pairs
 // and, inside a group, the `nblk` blocks of every pair run heaviest first (index 0 = heaviest).  All blocks of a
@@ -215,10 +200,10 @@ __device__ __forceinline__ int sdiv(int n, int d) {
 // correctness).  Returns the block rank (0 = heaviest) and the pair index.
 __device__ __forceinline__ void grouped_order(int bid, int nblk, int BH, int group, int& rank, int& bh) {
     const int per = nblk * group;
-    const int g = sdiv(bid, per);
+    const int g = bid / per;
     const int r = bid - g * per;
     const int gs = min(group, BH - g * group);  // the last group may be short
-    rank = sdiv(r, gs);
+    rank = r / gs;
     bh = g * group + (r - rank * gs);
 }
 

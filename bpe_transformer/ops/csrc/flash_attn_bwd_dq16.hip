@@ -107,7 +107,7 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
     int rank, bh;
     grouped_order((int)blockIdx.x, nqb, B * H, group, rank, bh);
     const int qblk = CAUSAL ? nqb - 1 - rank : rank;  // causal: the heaviest query blocks first
-    const int b = sdiv(bh, H), h = bh - b * H, hk = sdiv(h, sdiv(H, Hkv));
+    const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
     const int q0 = qblk * QB, qw = q0 + 16 * w, q = qw + i16;
     const bool q_ok = q < S;
     const long qc = q_ok ? q : S - 1;
@@ -162,13 +162,6 @@ fa_bwd_dq16_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, c
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // the Q rows / LSE converted here, not after the barrier (fa_common.h keep)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-        keep(qf[ks]);
-        keep(of[ks]);
-    }
-    keep(nl);
     __syncthreads();
     prologue_prio_end();
     DQ16_STAMP(1, 0);

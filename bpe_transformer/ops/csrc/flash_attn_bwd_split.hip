@@ -98,7 +98,7 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     int rank, bh;
     grouped_order((int)blockIdx.x, nqb, B * H, group, rank, bh);
     const int qblk = CAUSAL ? nqb - 1 - rank : rank;  // causal: the last (heaviest) query blocks first
-    const int b = sdiv(bh, H), h = bh - b * H, hk = sdiv(h, sdiv(H, Hkv));
+    const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
     const int q0 = qblk * QB, qw = q0 + 32 * w, q = qw + l31;
     const bool q_ok = q < S;
     const long qc = q_ok ? q : S - 1;
@@ -202,13 +202,6 @@ fa_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
 
     if constexpr (!DM) write_tile(0, 0);
-    // the Q rows / LSE converted here, not after the barrier (fa_common.h keep)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-        keep(qf[ks]);
-        keep(of[ks]);
-    }
-    keep(nl);
     __syncthreads();
     prologue_prio_end();
     FA_STAMP(0, 1, 0);
@@ -389,12 +382,12 @@ fa_bwd_dkv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, co
     const int nkb = (S + KB - 1) / KB;
     // One workgroup per (batch, KV head, key block) sweeps the G = H / Hkv query heads of its group one after the
     // other, summing their dK / dV in the accumulators: no fp32 partials, no reduce kernel (GQA).
-    const int G = sdiv(H, Hkv), GL = G;
+    const int G = H / Hkv, GL = G;
     int kblk, bh;  // causal: key block 0 (the most query tiles) first
     grouped_order((int)blockIdx.x, nkb, B * Hkv, group, kblk, bh);
-    const int b = sdiv(bh, Hkv);
-    const int hk = bh - b * Hkv;
-    const int h = hk * G;  // first query head
+    const int b = bh / Hkv;
+    const int h = (bh % Hkv) * G;  // first query head
+    const int hk = h / G;
     const int kb0 = kblk * KB, kw0 = kb0 + 32 * w, key = kw0 + l31;
     const bool key_ok = key < S;
     const long kpos = key_ok ? key : S - 1;

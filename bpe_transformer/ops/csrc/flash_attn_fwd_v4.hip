@@ -44,7 +44,7 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
     int qrank, bh;
     grouped_order((int)blockIdx.x, nqb, B * H, group, qrank, bh);
     const int qb = nqb - 1 - qrank;  // heaviest (last) query blocks first
-    const int b = sdiv(bh, H), h = bh - b * H, hk = sdiv(h, sdiv(H, Hkv));
+    const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
     const int q0 = qb * 128, qw0 = q0 + 32 * w, qrow = qw0 + l31;
 
     // prologue: the Q rows and K / V tile 0 are all requested before any is waited for (one memory round trip)
@@ -90,7 +90,6 @@ fa_fwd_v4_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K, con
         float x[8];
         unpack8(qr[ks], x);
         qf[ks] = __builtin_bit_cast(bf16x8, pack8(x, scale_log2));
-        keep(qf[ks]);  // converted here, not after the barrier (fa_common.h keep)
     }
     __syncthreads();
     prologue_prio_end();
