@@ -92,7 +92,7 @@ def main():
     if a.bwd_ab:
         # (backward form, dQ form): split with the 32- or 16-queries-per-wave dQ kernel (ops.fa_dq_config)
         # (backward form, dQ form)
-        arms = {"fused": (1, 0), "split": (0, 0), "split_dq16": (0, 1), "split_dq16_nw4": (0, 2)}
+        arms = {"fused": (1, 0), "split": (0, 0), "split_dq16": (0, 1), "split_dq16_nw4": (0, 2), "split_auto": (0, 3)}
         if a.bwd_arms:
             arms = {n: arms[n] for n in a.bwd_arms}
         prev = hip.fa_bwd_config(-1)

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--heads", type=int, default=12)
     ap.add_argument("--kv-heads", type=int, default=None)
-    ap.add_argument("--dq-form", type=int, default=0, help="ops.fa_dq_config: 0 = 32 queries per wave, 1 = 16 (8 waves), 2 = 16 (4 waves)")
+    ap.add_argument("--dq-form", type=int, default=0, help="ops.fa_dq_config: 0 = 32 queries per wave, 1 = 16 (8 waves), 2 = 16 (4 waves), 3 = auto")
     a = ap.parse_args()
     h = ops()
     h.fa_dq_config(a.dq_form)
@@ -52,7 +52,7 @@ def main():
               f"prologue {pro.mean():.0f} ({pro.sum() / dur.sum() * 100:.1f} %), full tiles {body.mean():.0f} "
               f"({body.sum() / dur.sum() * 100:.1f} %), last (diagonal) tile {diag.mean():.0f} "
               f"({diag.sum() / dur.sum() * 100:.1f} %)")
-        if name == "dQ" and a.dq_form > 0:  # slots 6 (loads issued) and 4 (the wave's row loads arrived)
+        if name == "dQ" and a.dq_form in (1, 2):  # slots 6 (loads issued) and 4 (the wave's row loads arrived)
             iss, rows = r[:, 6] - r[:, 0], r[:, 4] - r[:, 0]
             print(f"  prologue split (last wave): loads issued at {iss.mean():.0f}, its rows arrived at {rows.mean():.0f}, "
                   f"barrier (tile-0 DMA, all waves) passed at {pro.mean():.0f} cycles after entry")

@@ -274,16 +274,18 @@ using namespace bpe;
 using namespace bpe::fa;
 
 // dQ form of the split backward at D = 64 without in-kernel RoPE: 0 = 32 queries per wave (fa_bwd_dq_kernel),
-// 1 = 16 queries per wave, 8 waves, 128-key tiles, 2 = 16 queries per wave, 4 waves, 64-key tiles (this file);
-// switched at run time (tests compare them).  Default 1: backward -1.1 % at GPT-2 B 128 and -1.0 % at Llama s2048
-// B 32 GQA op-level, +0.25 % end to end, both rounds of an alternating A/B on one box
-// (profiles/bench/ab_attn_dq_forms_r5.log, ab_e2e_r5.log); form 2 measured no gain (four workgroups per CU do not
+// 1 = 16 queries per wave, 8 waves, 128-key tiles, 2 = 16 queries per wave, 4 waves, 64-key tiles (this file),
+// 3 = form 1 up to S = 2048 and form 0 above (the default); switched at run time (tests compare them).  Form 1 against
+// form 0, op-level, interleaved: backward -1.9 % (S 1024, GPT-2 B 128), -0.3 % (S 2048, Llama GQA B 32), +0.1 %
+// (S 4096), +0.5 % (S 8192) (profiles/bench/ab_attn_dq_forms_r5.log, ab_attn_dq_vs_seq_r5.log): the gain is in the
+// per-workgroup fixed cost, which long sequences amortise.  Form 2 measured no gain (four workgroups per CU do not
 // shorten the prologue, profiles/attention_stamps_r5.md).
-static int g_dq_form = 1;
+static int g_dq_form = 3;
+static bool g_dq16_ran = false;  // the last backward launched this file's kernel (stamps)
 
 int fa_dq_config(int form) {
     const int prev = g_dq_form;
-    if (form >= 0) g_dq_form = form > 2 ? 2 : form;
+    if (form >= 0) g_dq_form = form > 3 ? 3 : form;
     return prev;
 }
 
@@ -291,7 +293,7 @@ int fa_dq_config(int form) {
 // otherwise or when the kernel is not selected)
 bool fa_read_stamps_dq16(long long* host, int n) {
 #ifdef BPE_FA_STAMPS
-    if (g_dq_form == 0) return false;
+    if (!g_dq16_ran) return false;
     (void)hipDeviceSynchronize();
     const int rows = n < 32768 ? n : 32768;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(dq16::g_stamps16), (size_t)rows * 8 * sizeof(long long), 0,
@@ -305,7 +307,9 @@ bool fa_read_stamps_dq16(long long* host, int n) {
 
 // launches the 16-row dQ kernel when selected and applicable (D = 64, rope 0 / 2); false otherwise
 bool launch_fa_bwd_dq16(const FaArgs& a, hipStream_t s) {
-    if (g_dq_form == 0 || a.D != 64 || a.rope == 1) return false;
+    const int form = g_dq_form == 3 ? (a.S <= 2048 ? 1 : 0) : g_dq_form;
+    g_dq16_ran = form != 0 && a.D == 64 && a.rope != 1;
+    if (!g_dq16_ran) return false;
     auto run = [&](auto nw, auto kt) {
         constexpr int NW = decltype(nw)::value, KT = decltype(kt)::value;
         const int nblk = (a.S + 16 * NW - 1) / (16 * NW);
@@ -323,7 +327,7 @@ bool launch_fa_bwd_dq16(const FaArgs& a, hipStream_t s) {
             else go(dq16::fa_bwd_dq16_kernel<NW, KT, false, false>);
         }
     };
-    if (g_dq_form == 1) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 128>{});
+    if (form == 1) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 128>{});
     else run(std::integral_constant<int, 4>{}, std::integral_constant<int, 64>{});
     return true;
 }

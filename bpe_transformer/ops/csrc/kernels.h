@@ -178,8 +178,8 @@ bool fa_bwd_split_active(int D, int rope = 0);
 // backward form 0 split / 1 fused; negative = unchanged; returns the form in force before the call
 int fa_bwd_config(int mode);
 // flash_attn_bwd_dq16.hip: the split backward's dQ kernel with 16 queries per wave (D = 64, rope 0 / 2) when
-// fa_dq_config(1) selected it; false when not applicable / not selected.  fa_dq_config: 0 = 32 queries per wave,
-// 1 = 16; negative = unchanged; returns the form in force before the call
+// fa_dq_config selected it; false when not applicable / not selected.  fa_dq_config: 0 = 32 queries per wave, 1 = 16
+// (8 waves), 2 = 16 (4 waves), 3 = 1 up to S = 2048 else 0 (default); negative = unchanged; returns the previous form
 bool launch_fa_bwd_dq16(const FaArgs& a, hipStream_t s);
 bool fa_read_stamps_dq16(long long* host, int n);
 int fa_dq_config(int form);

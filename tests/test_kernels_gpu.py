@@ -778,7 +778,7 @@ def test_flash_bwd_dq16_vs_dq32_and_oracle(gpu_device, S, H, Hkv, pre, causal, f
         g32 = h.fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, causal, pre, scale, pre)
     finally:
         h.fa_dq_config(prev)
-    assert prev == 1, "the default dQ form is the 16-row kernel (8 waves, 128-key tiles)"
+    assert prev == 3, "the default dQ form: the 16-row kernel (8 waves) up to S = 2048, the 32-row one above"
     assert torch.equal(g16, again), "dq16 backward is not deterministic"
     HD, KD = H * D, Hkv * D
     assert torch.equal(g16[:, HD + KD :], g32[:, HD + KD :]), "dV differs between the dQ forms"
