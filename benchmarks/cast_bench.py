@@ -58,6 +58,16 @@ def main():
     g8t = torch.empty(2 * F, T, dtype=torch.float8_e5m2, device="cuda")
     arms = {"swiglu_cast_fwd": (lambda: h.swiglu_cast_fp8_t(gu, None, s, a8, a8t, am), T * F * (4 + 2)),
             "swiglu_cast_bwd": (lambda: h.swiglu_cast_fp8_t(gu, da, s, g8, g8t, am), T * F * (4 + 2 + 4))}
+    # residual add + RMSNorm with the e4m3 output, then its fp8 transpose (add_rmsnorm_cast_fp8_t), at d 2048
+    N = 2048
+    xx = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    dd = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    ww = torch.rand(N, device="cuda", dtype=torch.bfloat16) + 0.5
+    y8 = torch.empty(T, N, dtype=torch.float8_e4m3fn, device="cuda")
+    y8t = torch.empty(N, T, dtype=torch.float8_e4m3fn, device="cuda")
+    # bytes: x, d read; sum written; y8 written, re-read and written transposed
+    arms["add_rmsnorm_cast_t"] = (lambda: h.add_rmsnorm_cast_fp8_t(xx, dd, ww, 1e-5, s, y8, y8t, am),
+                                  T * N * (2 + 2 + 2 + 1 + 1 + 1))
     t = {k: [] for k in arms}
     for _ in range(3):
         for k, (fn, _) in arms.items():

@@ -141,11 +141,18 @@ __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const __bf16* __restric
     if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
 
-// 128 x 128 fp8 tile transpose through LDS (the two-layout casts below).  Row-major phase: thread t holds the 64
-// bytes of tile row t >> 1, columns 64 (t & 1) .., as 16 words q.  Transposed phase: thread t emits output rows
-// 4 kq .. 4 kq + 3 (kq = t >> 3) over tile rows 16 ns .. 16 ns + 15 (ns = t & 7): the 8 ns of one kq are adjacent
-// lanes, so one store instruction of a wave writes 8 whole 128-byte output rows.  LDS word column c of tile row n
-// sits at c ^ sw(n), so the column reads of a 32-lane half (4 kq x 8 ns) hit 32 distinct banks.
+// 128 x 128 fp8 tile transpose through LDS (the two-layout casts below).  Row-major phase (c128_put): thread t holds
+// tile rows 16 i + (t >> 4), i = 0 .. 7, columns 8 (t & 15) .. + 7 -- one load instruction of a wave reads 4 whole
+// tile rows (8 whole 128-byte lines of bf16) and one row-major fp8 store writes 4 whole 128-byte lines.  Transposed
+// phase (t128_get_store): thread t emits output rows 4 kq .. 4 kq + 3 (kq = t >> 3) over tile rows 16 ns .. 16 ns +
+// 15 (ns = t & 7): the 8 ns of one kq are adjacent lanes, so one store instruction of a wave writes 8 whole 128-byte
+// output rows.  LDS word column c of tile row n sits at c ^ sw(n), so the column reads of a 32-lane half (4 kq x 8
+// ns) hit 32 distinct banks.
+// Measured, round 5 (profiles/bench/ab_fp8_cast_coalesced_r5.log): the earlier row-pair mapping (thread pair t, t + 1
+// on the two 64-column halves of tile row t >> 1, so one load instruction touched 64 lines 16 bytes at a time) ran the
+// two-layout cast at 4.4-4.5 TB/s and the SwiGLU casts at 4.1-4.2; this mapping 4.9 / 4.8-4.9 TB/s (the same bytes),
+// fp8 Llama step 191.5-192.9 k -> 195.7-196.4 k tok/s.  Prefetching the next tile's bf16 rows in the SwiGLU casts
+// measured the same and is not kept.
 // Plain (temporal) loads and stores in the 128 x 128 casts.  Measured and dropped, round 5: the non-temporal hint
 // (common.h ld_stream / st_stream, which took the softmax-CE kernel from 5.1 to 5.5 TB/s) halved these kernels -- the
 // two-layout cast 4.5 -> 2.5 TB/s, the SwiGLU casts 4.0-4.2 -> 1.8-1.9 TB/s, the fp8 Llama step 192.0 k -> 166.6 k
@@ -158,11 +165,6 @@ __device__ __forceinline__ void st16(uint8_t* p, unsigned a, unsigned b, unsigne
 
 constexpr int T128_TS = 132;  // LDS row stride (bytes): 33 words
 __device__ __forceinline__ int t128_sw(int n) { return ((n >> 4) & 7) << 2; }
-
-__device__ __forceinline__ void t128_put(uint8_t* tile, const unsigned (&q)[16], int r, int hc) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) *reinterpret_cast<unsigned*>(&tile[r * T128_TS + 4 * ((hc / 4 + i) ^ t128_sw(r))]) = q[i];
-}
 
 // dst = output row 4 kq of the transposed tile at column 16 ns; ld = output row stride (bytes)
 __device__ __forceinline__ void t128_get_store(const uint8_t* tile, int kq, int ns, uint8_t* dst, long ld) {
@@ -192,63 +194,6 @@ __device__ __forceinline__ void t128_get_store(const uint8_t* tile, int kq, int 
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_s_barrier();
-}
-
-// The same two-layout cast on 128 x 128 tiles (N, K multiples of 128): every output row segment a thread group writes
-// is a whole 128-byte line in both layouts (the 64 x 64 kernel writes 64-byte halves, 3.4-3.5 TB/s effective against
-// 5.4-5.5 for the one-layout cast, profiles/bench/cast_bench_r4.log), and each thread keeps eight 16-byte loads in
-// flight.  Transposed reads: a thread takes one 32-bit word (4 k values) from each of 16 tile rows and turns every 4
-// x 4 byte block around with v_perm_b32, so it stores 16 consecutive n for each of its 4 output rows.
-template <int FMT>
-__global__ void __launch_bounds__(256) cast_fp8_t128_kernel(const __bf16* __restrict__ w, int N, int K,
-                                                            const float* __restrict__ scale, uint8_t* __restrict__ w8,
-                                                            uint8_t* __restrict__ w8t,
-                                                            unsigned* __restrict__ amax_bits) {
-    __shared__ __attribute__((aligned(16))) uint8_t tile[128 * T128_TS];
-    __shared__ float red[4];
-    const int tid = threadIdx.x;
-    const int tiles_k = K / 128, ntiles = (N / 128) * tiles_k;
-    const float sc = *scale;
-    const int r = tid >> 1, hc = (tid & 1) * 64;  // load / row-major phase: tile row r, columns hc .. hc + 63
-    const int kq = tid >> 3, ns = tid & 7;  // transposed phase (t128_get_store)
-    float am = 0.f;
-    // the next tile's rows are loaded as soon as this tile's are converted, so they are in flight through the
-    // stores and the LDS transpose; the LDS hand-offs use raw barriers behind lgkmcnt(0) only (__syncthreads would
-    // also wait for those loads)
-    u16x8 a[8];
-    auto load = [&](int tt) {
-        const int n0 = (tt / tiles_k) * 128, k0 = (tt % tiles_k) * 128;
-        const __bf16* src = w + (long)(n0 + r) * K + k0 + hc;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = ld8(src + 8 * i);
-    };
-    if (blockIdx.x < ntiles) load(blockIdx.x);
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int n0 = (t / tiles_k) * 128, k0 = (t % tiles_k) * 128;
-        unsigned q[16];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            float v[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                v[j] = bf2f(a[i][j]);
-                am = fmaxf(am, fabsf(v[j]));
-            }
-            q[2 * i] = pack4_fp8<FMT>(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc);
-            q[2 * i + 1] = pack4_fp8<FMT>(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc);
-        }
-        if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);
-        uint8_t* dst = w8 + (long)(n0 + r) * K + k0 + hc;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            st16(dst + 16 * i, q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
-        lds_barrier();  // the previous tile's transposed reads are done
-        t128_put(tile, q, r, hc);
-        lds_barrier();
-        t128_get_store(tile, kq, ns, w8t + (long)(k0 + 4 * kq) * N + n0 + 16 * ns, N);
-    }
-    am = block_max(am, red);
-    if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
 
 // SwiGLU with the two-layout fp8 cast fused in (the fp8 weight-gradient path, where no bf16 copy of these tensors
@@ -335,38 +280,107 @@ __global__ void __launch_bounds__(256) swiglu_cast_fp8_t_kernel(const __bf16* __
     if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
 }
 
-// The SwiGLU + two-layout cast on 128 x 128 tiles (M and F multiples of 128; the t128 helpers above): whole 128-byte
-// output lines in both layouts, as cast_fp8_t128_kernel.  Values, rounding and amax as swiglu_cast_fp8_t_kernel.
+// q[2 i], q[2 i + 1]: fp8 words cw, cw + 1 of tile row r0 + 16 i (the row-major phase above)
+__device__ __forceinline__ void c128_put(uint8_t* tile, const unsigned (&q)[16], int r0, int cw) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r = r0 + 16 * i;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) *reinterpret_cast<unsigned*>(&tile[r * T128_TS + 4 * ((cw + j) ^ t128_sw(r))]) = q[2 * i + j];
+    }
+}
+
+// The two-layout cast on 128 x 128 tiles (N, K multiples of 128): every output row segment a thread group writes is a
+// whole 128-byte line in both layouts (the 64 x 64 kernel writes 64-byte halves, 3.4-3.5 TB/s effective against
+// 5.4-5.5 for the one-layout cast, profiles/bench/cast_bench_r4.log), and the next tile's loads are issued as soon as
+// this tile's values are converted, so they are in flight through the stores and the LDS transpose (raw barriers
+// behind lgkmcnt(0) only: __syncthreads would also wait for those loads).  Transposed reads: a thread takes one 32-bit
+// word (4 k values) from each of 16 tile rows and turns every 4 x 4 byte block around with v_perm_b32, so it stores 16
+// consecutive n for each of its 4 output rows.
+template <int FMT>
+__global__ void __launch_bounds__(256) cast_fp8_c128_kernel(const __bf16* __restrict__ w, int N, int K,
+                                                            const float* __restrict__ scale, uint8_t* __restrict__ w8,
+                                                            uint8_t* __restrict__ w8t,
+                                                            unsigned* __restrict__ amax_bits) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[128 * T128_TS];
+    __shared__ float red[4];
+    const int tid = threadIdx.x;
+    const int tiles_k = K / 128, ntiles = (N / 128) * tiles_k;
+    const float sc = *scale;
+    const int r0 = tid >> 4, c8 = (tid & 15) * 8;
+    const int kq = tid >> 3, ns = tid & 7;
+    float am = 0.f;
+    u16x8 a[8];
+    auto load = [&](int tt) {
+        const int n0 = (tt / tiles_k) * 128, k0 = (tt % tiles_k) * 128;
+        const __bf16* src = w + (long)(n0 + r0) * K + k0 + c8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = ld8(src + (long)16 * i * K);
+    };
+    if (blockIdx.x < ntiles) load(blockIdx.x);
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int n0 = (t / tiles_k) * 128, k0 = (t % tiles_k) * 128;
+        unsigned q[16];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                v[j] = bf2f(a[i][j]);
+                am = fmaxf(am, fabsf(v[j]));
+            }
+            q[2 * i] = pack4_fp8<FMT>(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc);
+            q[2 * i + 1] = pack4_fp8<FMT>(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc);
+        }
+        if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);
+        uint8_t* dst = w8 + (long)(n0 + r0) * K + k0 + c8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) *reinterpret_cast<uint2*>(dst + (long)16 * i * K) = uint2{q[2 * i], q[2 * i + 1]};
+        lds_barrier();  // the previous tile's transposed reads are done
+        c128_put(tile, q, r0, c8 / 4);
+        lds_barrier();
+        t128_get_store(tile, kq, ns, w8t + (long)(k0 + 4 * kq) * N + n0 + 16 * ns, N);
+    }
+    am = block_max(am, red);
+    if (tid == 0 && amax_bits) atomicMax(amax_bits, __float_as_uint(am));
+}
+
+// The SwiGLU + two-layout cast on 128 x 128 tiles (M and F multiples of 128).  Values, rounding and amax as
+// swiglu_cast_fp8_t_kernel; the thread mapping of cast_fp8_c128_kernel.
 template <int MODE, int FMT>
-__global__ void __launch_bounds__(256) swiglu_cast_fp8_t128_kernel(const __bf16* __restrict__ gu,
+__global__ void __launch_bounds__(256) swiglu_cast_fp8_c128_kernel(const __bf16* __restrict__ gu,
                                                                    const __bf16* __restrict__ dout, int M, int F,
                                                                    const float* __restrict__ scale,
                                                                    uint8_t* __restrict__ o8, uint8_t* __restrict__ o8t,
                                                                    unsigned* __restrict__ amax_bits) {
-    constexpr int NO = MODE == 0 ? 1 : 2;  // output column blocks per tile: a, or dg and du
+    constexpr int NO = MODE == 0 ? 1 : 2;
     __shared__ __attribute__((aligned(16))) uint8_t tile[NO][128 * T128_TS];
     __shared__ float red[4];
     const int tid = threadIdx.x;
     const int tiles_f = F / 128, ntiles = (M / 128) * tiles_f;
-    const long W = (long)NO * F;  // output row length
+    const long W = (long)NO * F;
     const float sc = *scale;
-    const int r = tid >> 1, hc = (tid & 1) * 64;
+    const int r0 = tid >> 4, c8 = (tid & 15) * 8;
     const int kq = tid >> 3, ns = tid & 7;
     float am = 0.f;
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int m0 = (t / tiles_f) * 128, f0 = (t % tiles_f) * 128;
-        const __bf16* row = gu + (long)(m0 + r) * 2 * F + f0 + hc;
-        u16x8 g[8], u[8], d[MODE == 1 ? 8 : 1];
+    u16x8 g[8], u[8], d[MODE == 1 ? 8 : 1];
+    auto load = [&](int tt) {
+        const int m0 = (tt / tiles_f) * 128, f0 = (tt % tiles_f) * 128;
+        const __bf16* row = gu + (long)(m0 + r0) * 2 * F + f0 + c8;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            g[i] = ld8(row + 8 * i);
-            u[i] = ld8(row + F + 8 * i);
+            g[i] = ld8(row + (long)16 * i * 2 * F);
+            u[i] = ld8(row + (long)16 * i * 2 * F + F);
         }
         if constexpr (MODE == 1) {
-            const __bf16* dr = dout + (long)(m0 + r) * F + f0 + hc;
+            const __bf16* dr = dout + (long)(m0 + r0) * F + f0 + c8;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) d[i] = ld8(dr + 8 * i);
+            for (int i = 0; i < 8; ++i) d[i] = ld8(dr + (long)16 * i * F);
         }
+    };
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int m0 = (t / tiles_f) * 128, f0 = (t % tiles_f) * 128;
+        load(t);
         unsigned q[NO][16];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -394,14 +408,14 @@ __global__ void __launch_bounds__(256) swiglu_cast_fp8_t128_kernel(const __bf16*
         }
 #pragma unroll
         for (int o = 0; o < NO; ++o) {
-            uint8_t* dst = o8 + (long)(m0 + r) * W + (long)o * F + f0 + hc;
+            uint8_t* dst = o8 + (long)(m0 + r0) * W + (long)o * F + f0 + c8;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                st16(dst + 16 * i, q[o][4 * i], q[o][4 * i + 1], q[o][4 * i + 2], q[o][4 * i + 3]);
+            for (int i = 0; i < 8; ++i)
+                *reinterpret_cast<uint2*>(dst + (long)16 * i * W) = uint2{q[o][2 * i], q[o][2 * i + 1]};
         }
         lds_barrier();  // the previous tile's transposed reads are done
 #pragma unroll
-        for (int o = 0; o < NO; ++o) t128_put(tile[o], q[o], r, hc);
+        for (int o = 0; o < NO; ++o) c128_put(tile[o], q[o], r0, c8 / 4);
         lds_barrier();
 #pragma unroll
         for (int o = 0; o < NO; ++o)
@@ -414,7 +428,7 @@ __global__ void __launch_bounds__(256) swiglu_cast_fp8_t128_kernel(const __bf16*
 // Residual add + RMSNorm with an fp8 output (the fp8 weight-gradient path, where the normalised activation only
 // feeds fp8 GEMMs): s = x + d (bf16, stored: the residual stream; d == nullptr: s = x, not stored), rstd stored,
 // and y = s * rstd * w -- rounded to bf16 exactly as add_rmsnorm_fwd / rmsnorm_fwd store it -- written only as
-// e4m3 [M][N] (scale, amax folded in); transpose_fp8_t128_kernel then writes [N][M].  One wave per row, C 16-byte
+// e4m3 [M][N] (scale, amax folded in); transpose_fp8_c128_kernel then writes [N][M].  One wave per row, C 16-byte
 // chunks per lane (N / 8 <= 64 C).  Against the norm + two-layout cast pair it drops the bf16 y write and its re-read.
 template <int C>
 __global__ void __launch_bounds__(256) add_rmsnorm_fp8_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ d,
@@ -476,27 +490,28 @@ __global__ void __launch_bounds__(256) add_rmsnorm_fp8_kernel(const __bf16* __re
     if (threadIdx.x == 0) atomicMax(amax_bits, __float_as_uint(am));
 }
 
-// fp8 [M][N] -> [N][M] (M, N multiples of 128) through the 128 x 128 tile helpers above
-__global__ void __launch_bounds__(256) transpose_fp8_t128_kernel(const uint8_t* __restrict__ a, uint8_t* __restrict__ at,
+// fp8 [M][N] -> [N][M] (M, N multiples of 128) through the 128 x 128 tile helpers above: thread t reads tile rows
+// 32 i + (t >> 3), i = 0 .. 3, bytes 16 (t & 7) .. + 15, so one load instruction of a wave reads 8 whole 128-byte rows
+__global__ void __launch_bounds__(256) transpose_fp8_c128_kernel(const uint8_t* __restrict__ a, uint8_t* __restrict__ at,
                                                                  int M, int N) {
     __shared__ __attribute__((aligned(16))) uint8_t tile[128 * T128_TS];
     const int tid = threadIdx.x;
     const int tiles_n = N / 128, ntiles = (M / 128) * tiles_n;
-    const int r = tid >> 1, hc = (tid & 1) * 64, kq = tid >> 3, ns = tid & 7;
+    const int r0 = tid >> 3, cw = (tid & 7) * 4, kq = tid >> 3, ns = tid & 7;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int m0 = (t / tiles_n) * 128, n0 = (t % tiles_n) * 128;
-        const uint8_t* src = a + (long)(m0 + r) * N + n0 + hc;
-        unsigned q[16];
+        const uint8_t* src = a + (long)(m0 + r0) * N + n0 + 4 * cw;
+        uint4 q[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = *reinterpret_cast<const uint4*>(src + (long)32 * i * N);
+        lds_barrier();  // the previous tile's transposed reads are done
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const uint4 u = *reinterpret_cast<const uint4*>(src + 16 * i);
-            q[4 * i] = u.x;
-            q[4 * i + 1] = u.y;
-            q[4 * i + 2] = u.z;
-            q[4 * i + 3] = u.w;
+            const int r = r0 + 32 * i;
+            const unsigned w[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) *reinterpret_cast<unsigned*>(&tile[r * T128_TS + 4 * ((cw + j) ^ t128_sw(r))]) = w[j];
         }
-        lds_barrier();  // the previous tile's transposed reads are done
-        t128_put(tile, q, r, hc);
         lds_barrier();
         t128_get_store(tile, kq, ns, at + (long)(n0 + 4 * kq) * M + m0 + 16 * ns, M);
     }
@@ -546,10 +561,10 @@ void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8
         const int nt = (N / 128) * (K / 128);
         const int g = nt < 2048 ? nt : 2048;
         if (fmt == 0)
-            cast_fp8_t128_kernel<0><<<g, 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8, (uint8_t*)w8t,
+            cast_fp8_c128_kernel<0><<<g, 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8, (uint8_t*)w8t,
                                                       amax_bits);
         else
-            cast_fp8_t128_kernel<1><<<g, 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8, (uint8_t*)w8t,
+            cast_fp8_c128_kernel<1><<<g, 256, 0, s>>>((const __bf16*)w, N, K, scale, (uint8_t*)w8, (uint8_t*)w8t,
                                                       amax_bits);
         return;
     }
@@ -569,10 +584,10 @@ void launch_swiglu_cast_fp8_t(int mode, const void* gu, const void* dout, int M,
         const int nt = (M / 128) * (F / 128);
         const int g = nt < 2048 ? nt : 2048;
         if (mode == 0)
-            swiglu_cast_fp8_t128_kernel<0, 0><<<g, 256, 0, s>>>((const __bf16*)gu, nullptr, M, F, scale,
+            swiglu_cast_fp8_c128_kernel<0, 0><<<g, 256, 0, s>>>((const __bf16*)gu, nullptr, M, F, scale,
                                                                 (uint8_t*)o8, (uint8_t*)o8t, amax_bits);
         else
-            swiglu_cast_fp8_t128_kernel<1, 1><<<g, 256, 0, s>>>((const __bf16*)gu, (const __bf16*)dout, M, F, scale,
+            swiglu_cast_fp8_c128_kernel<1, 1><<<g, 256, 0, s>>>((const __bf16*)gu, (const __bf16*)dout, M, F, scale,
                                                                 (uint8_t*)o8, (uint8_t*)o8t, amax_bits);
         return;
     }
@@ -600,7 +615,7 @@ void launch_add_rmsnorm_cast_fp8_t(const void* x, const void* d, const void* w, 
     else ARF(4);
 #undef ARF
     const int nt = (M / 128) * (N / 128);
-    transpose_fp8_t128_kernel<<<nt < 2048 ? nt : 2048, 256, 0, s>>>((const uint8_t*)y8, (uint8_t*)y8t, M, N);
+    transpose_fp8_c128_kernel<<<nt < 2048 ? nt : 2048, 256, 0, s>>>((const uint8_t*)y8, (uint8_t*)y8t, M, N);
 }
 
 void launch_update_scales(unsigned* amax_cur, float* hist, float* scale, float* inv_scale, int n, int H, int pos,

@@ -923,9 +923,9 @@ def test_cast_fp8_and_amax(gpu_device, dtype, n, fmt):
     assert amax.view(torch.float32).item() == x.float().abs().max().item()
 
 
-# (192, 320): the 64 x 64 kernel; the others the 128 x 128 one, (4096, 1024) / (8192, 4096) with more tiles than the
-# grid (stride loop)
-@pytest.mark.parametrize("N,K", [(192, 320), (4096, 1024), (384, 256), (8192, 4096)])
+# (192, 320): the 64 x 64 kernel; the others the 128 x 128 one, (8192, 4224) with more tiles than the grid (2112 >
+# 2048: stride loop)
+@pytest.mark.parametrize("N,K", [(192, 320), (4096, 1024), (384, 256), (8192, 4096), (8192, 4224)])
 @pytest.mark.parametrize("fmt", [torch.float8_e4m3fn, torch.float8_e5m2])
 def test_cast_fp8_transposed(gpu_device, N, K, fmt):
     """Two-layout cast (weights; activations and gradients of the fp8 weight-gradient GEMM): both layouts from one
@@ -945,7 +945,8 @@ def test_cast_fp8_transposed(gpu_device, N, K, fmt):
     assert am == float(w.float().abs().max())
 
 
-@pytest.mark.parametrize("M,F", [(256, 192), (1024, 512)])
+# (256, 192): the 64 x 64 kernel; (32768, 1408): 2816 tiles of 128 x 128, more than the grid (stride loop)
+@pytest.mark.parametrize("M,F", [(256, 192), (1024, 512), (32768, 1408)])
 def test_swiglu_cast_fp8_transposed(gpu_device, M, F):
     """SwiGLU with the two-layout fp8 cast fused (fp8.hip swiglu_cast_fp8_t): forward a = silu(g) u as e4m3 [M, F] and
     [F, M], backward [dg | du] as e5m2 [M, 2F] and [2F, M] -- against the two-pass form (swiglu_fwd / swiglu_bwd to
