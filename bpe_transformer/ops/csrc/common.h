@@ -33,6 +33,17 @@ __device__ __forceinline__ float fast_sigmoid(float x) {
     return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
 
+// Two elements at once: the arithmetic on the packed fp32 VALU (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32, two
+// lanes' worth per instruction), the transcendentals per element -- the same operations and rounding as
+// fast_sigmoid, for epilogues that run no MFMAs beside them (explicit vectors: files built without the SLP
+// vectorizer still get the packed forms).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 fast_sigmoid2(f32x2 x) {
+    const f32x2 t = x * -1.4426950408889634f;
+    const f32x2 e = 1.f + f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+    return f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

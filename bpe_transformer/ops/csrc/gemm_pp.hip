@@ -487,6 +487,11 @@ __device__ long long g_gpp_stamps[65536 * 8];
 // bf16-rounded products exactly as rope_qk_kernel (rope.hip) applies it to the stored activation: interleaved
 // pairs, position = row % S, fp32 cos / sin tables [S][D / 2].  Saves the separate in-place pass over Q / K.
 enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2, EPI_ROPE = 3 };
+// 1: the SwiGLU epilogues' arithmetic on the packed fp32 VALU, two elements per instruction (common.h
+// fast_sigmoid2; bitwise the same results); 0: one element per instruction (A/B variant builds)
+#ifndef BPE_GPP_PK
+#define BPE_GPP_PK 1
+#endif
 struct Epi {
     const __bf16* gu;
     __bf16* dgu;  // EPI_SWIGLU_BWD: dgu out; EPI_SWIGLU_FWD: gu out
@@ -554,6 +559,19 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
                 const u16x8 v = *reinterpret_cast<const u16x8*>(stg + i * 512 + ((c ^ (i & 15)) << 4));
                 const long ro = (long)(i0 + r0 + i) * ep.ld + j0 + c * 8;
                 u16x8 dg, du;
+#if BPE_GPP_PK
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {  // pairs on the packed fp32 VALU (same math and rounding)
+                    const f32x2 gg = {bf2f(gv[q][e]), bf2f(gv[q][e + 1])}, uu = {bf2f(uv[q][e]), bf2f(uv[q][e + 1])};
+                    const f32x2 d = {bf2f(v[e]), bf2f(v[e + 1])};
+                    const f32x2 sg = fast_sigmoid2(gg);
+                    const f32x2 a = d * (gg * sg), b = d * uu * sg * (1.f + gg * (1.f - sg));
+                    du[e] = f2bf(a.x);
+                    du[e + 1] = f2bf(a.y);
+                    dg[e] = f2bf(b.x);
+                    dg[e + 1] = f2bf(b.y);
+                }
+#else
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const float gg = bf2f(gv[q][e]), uu = bf2f(uv[q][e]), d = bf2f(v[e]);
@@ -561,6 +579,7 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
                     du[e] = f2bf(d * (gg * sg));
                     dg[e] = f2bf(d * uu * sg * (1.f + gg * (1.f - sg)));
                 }
+#endif
                 if (st_on) {
                     *reinterpret_cast<u16x8*>(ep.dgu + ro) = dg;
                     *reinterpret_cast<u16x8*>(ep.dgu + ro + ep.F) = du;
@@ -578,11 +597,21 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
                 const u16x8 gv = *reinterpret_cast<const u16x8*>(stg + i * 512 + ((c ^ (i & 15)) << 4));
                 const u16x8 uv = *reinterpret_cast<const u16x8*>(stg + i * 512 + (((16 + c) ^ (i & 15)) << 4));
                 u16x8 av;
+#if BPE_GPP_PK
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    const f32x2 gg = {bf2f(gv[e]), bf2f(gv[e + 1])};
+                    const f32x2 a = gg * fast_sigmoid2(gg) * f32x2{bf2f(uv[e]), bf2f(uv[e + 1])};
+                    av[e] = f2bf(a.x);
+                    av[e + 1] = f2bf(a.y);
+                }
+#else
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const float gg = bf2f(gv[e]);
                     av[e] = f2bf(gg * fast_sigmoid(gg) * bf2f(uv[e]));
                 }
+#endif
                 const long r = i0 + r0 + i;
                 // gu is next read by the backward, long after this step's forward: streaming stores
                 if (st_on) {
