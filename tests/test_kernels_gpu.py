@@ -129,6 +129,32 @@ def test_cross_entropy(gpu_device, V, dtype):
     assert abs(ops.cross_entropy(big, tb).item() - ref.item()) < 1e-3
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cross_entropy_target_positions(gpu_device, dtype):
+    """Targets in the unaligned head, the body and the scalar tail of odd-length rows (V = 50257: row r starts at
+    element 50257 r), and ignored rows: the register kernel writes softmax * scale everywhere and stores the target's
+    "- scale" once per row after the row's other stores."""
+    V = 50257
+    torch.manual_seed(5)
+    x = torch.randn(24, V, device=gpu_device, dtype=dtype, requires_grad=True)
+    t = torch.tensor([0, 1, 2, 3, 5, 7, 8, 9, 15, 16, 4000, 25000, V - 9, V - 8, V - 7, V - 2, V - 1,
+                      -100, 6, V - 3, 12345, -100, 31, 63], device=gpu_device)
+    loss = ops.cross_entropy(x, t)
+    loss.backward()
+    xr = x.detach().float().cpu().requires_grad_(True)
+    lr_ = torch.nn.functional.cross_entropy(xr, t.cpu(), ignore_index=-100)
+    lr_.backward()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert abs(loss.item() - lr_.item()) < tol
+    assert rel(x.grad.cpu(), xr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+    g, gr = x.grad.float().cpu(), xr.grad
+    rows = torch.arange(24)
+    ok = t.cpu() != -100
+    # the target entries themselves (negative: p - 1), and the ignored rows all zero
+    assert torch.allclose(g[rows[ok], t.cpu()[ok]], gr[rows[ok], t.cpu()[ok]], rtol=2e-2, atol=1e-6)
+    assert g[~ok].abs().max().item() == 0.0
+
+
 def test_cross_entropy_ignore_index(gpu_device):
     torch.manual_seed(0)
     x = torch.randn(16, 100, device=gpu_device, requires_grad=True)
