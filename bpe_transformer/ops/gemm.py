@@ -123,7 +123,7 @@ def use_pp(n: int, k: int, t: int) -> bool:
 def _candidates(n: int, k: int, t: int) -> list[str]:
     c = []
     if use_pp(n, k, t):
-        c.append("pp")
+        c += ["pp", "ppt"]
     if use_tile256(n, k, t):
         c.append("hip256")
     elif supported(n, k, t):
@@ -143,6 +143,10 @@ def _run(route: str, g: Tensor, dy: Tensor, x: Tensor) -> None:
     t = dy.shape[0]
     if route == "pp":
         ops().gemm_pp(dy, False, x, False, g, 1.0, choose_splits_pp(n, k, t))
+    elif route == "ppt":
+        # X^T materialised (ops.transpose_bf16): B K-major, the ping-pong kernel's MN x K layout -- ahead of the
+        # token-major x token-major one on the LM head (benchmarks/dw_ppt.py, profiles/bench/dw_ppt_r5.log)
+        ops().gemm_pp(dy, False, ops().transpose_bf16(x), True, g, 1.0, choose_splits_pp(n, k, t))
     elif route == "hip256":
         ops().gemm(dy, False, x, False, g, 1.0, choose_splits_256(n, k, t), 256)
     elif route == "hip128":

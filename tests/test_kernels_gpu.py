@@ -622,6 +622,23 @@ def test_weight_grad_shapes(gpu_device, shape):
     assert rel(g, ref) < 1e-2
 
 
+@pytest.mark.parametrize("route", ["pp", "ppt", "hip256"])
+@pytest.mark.parametrize("shape", [(2304, 768, 8192), (1024, 2048, 4096)])
+def test_weight_grad_routes(gpu_device, route, shape):
+    """Each dW route of ops.gemm on its own (ppt: the ping-pong kernel on a transposed copy of X), accumulating into
+    g, against the fp32 product."""
+    from bpe_transformer.ops.gemm import _run
+
+    n, k, t = shape
+    torch.manual_seed(1)
+    dy = torch.randn(t, n, device=gpu_device, dtype=torch.bfloat16)
+    x = torch.randn(t, k, device=gpu_device, dtype=torch.bfloat16)
+    g = torch.randn(n, k, device=gpu_device, dtype=torch.bfloat16)
+    ref = g.float() + dy.float().t() @ x.float()
+    _run(route, g, dy, x)
+    assert rel(g, ref) < 1e-2
+
+
 def test_weight_grad_accumulate(gpu_device):
     from bpe_transformer.ops.gemm import accumulate_weight_grad
 
