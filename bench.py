@@ -94,6 +94,10 @@ def main() -> int:
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = the plumbing config path (fp32, no HIP kernels), e.g. --model tinystories-17m --seq 256")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--no-dp-check", action="store_true",
+                    help="N>1: skip the untimed replica-consistency step after warmup (default: run it)")
+    ap.add_argument("--debug-corrupt-rank", type=int, default=-1,
+                    help=argparse.SUPPRESS)  # tests: perturb this rank's weights before the consistency step
     args = ap.parse_args()
     if args.batch is None:
         if args.model in DEFAULT_TOKENS:
@@ -139,6 +143,20 @@ def main() -> int:
 
     for i in range(args.warmup):
         engine.train_step(batch(i))
+    # N > 1: one more untimed step with the replica-consistency detector on (parallel/ddp.py check_consistency):
+    # per-bucket fp64 checksums of the all-reduced gradients and of the updated weights compared across ranks; a
+    # mismatch raises, so the first multi-GPU record can only be written by replicas that stayed bit-identical
+    dp_check = None
+    if engine.ddp is not None and not args.no_dp_check:
+        if args.debug_corrupt_rank == info.rank:
+            with torch.no_grad():
+                engine.flat.data[:64].add_(1.0)
+        prev_every = engine.ddp_check_every
+        engine.ddp_check_every = 1
+        engine.train_step(batch(args.warmup))
+        sync()
+        engine.ddp_check_every = prev_every
+        dp_check = "grad+data bit-identical across ranks" if not engine.zero else "data bit-identical across ranks"
     sync()
     engine.phase_times()  # drop the warmup steps' events
     if on_gpu:
@@ -191,6 +209,23 @@ def main() -> int:
         "allreduce_dtype": (str(engine.ddp.comm_dtype if hasattr(engine.ddp, "comm_dtype") else
                                 engine.flat.grad.dtype).replace("torch.", "") if engine.ddp is not None else None),
     }
+    if engine.ddp is not None:
+        import torch.distributed as dist
+
+        bk = engine.ddp.buckets
+        esz = engine.flat.grad.element_size()
+        out["dist"] = {
+            "world_size": dist.get_world_size(),
+            "backend": dist.get_backend(),
+            "collective": "reduce-scatter + all-gather (ZeRO-1)" if engine.zero else "all-reduce (AVG)",
+            "buckets": len(bk),
+            "bucket_mb": [round((e - s_) * esz / 2**20, 2) for s_, e in bk],
+            "comm_dtype": str(getattr(engine.ddp, "comm_dtype", engine.flat.grad.dtype)).replace("torch.", ""),
+            "consistency_check": dp_check,
+        }
+    if phases:
+        out["phases_ms"] = phases  # max over ranks; comm_ms = the all-reduce wait left exposed after the backward
+        out["comm_ms"] = phases.get("comm_ms")
     if on_gpu:
         # peak HBM allocated by PyTorch's caching allocator over the timed steps (max over ranks), and reserved
         out["peak_mem_gb"] = round(all_reduce_max(torch.cuda.max_memory_allocated(dev) / 1e9, dev), 2)
@@ -198,6 +233,7 @@ def main() -> int:
         from bpe_transformer.ops import gemm as _gemm
 
         out["dw_gemm_routes"] = _gemm.routes_summary()  # weight-gradient kernel per shape (ops/tuning/dw_routes.json)
+        out["dw_gemm_groups"] = _gemm.groups_summary()  # grouped dW launches: shapes -> split count
     if info.is_main:
         if phases:  # max over ranks of each phase's mean ms per step (comm_ms = exposed collective wait)
             print(json.dumps({"phases_ms_per_step_max_over_ranks": phases}), file=sys.stderr, flush=True)

@@ -21,8 +21,11 @@ backward: the mirror image, with
   * the SwiGLU backward fused into the epilogue of the dY @ W2 GEMM (our
     ping-pong MFMA kernel): the gate gradient da never goes to HBM;
   * weight gradients ACCUMULATED IN PLACE into the flat gradient buffer
-    (``param.main_grad``, set by the training engine) by the per-shape dW
-    route of ops/gemm.py -- no temporary dW, no AccumulateGrad add kernels;
+    (``param.main_grad``, set by the training engine) -- no temporary dW, no
+    AccumulateGrad add kernels -- with the dW GEMMs that are ready together
+    grouped into one split-K launch each (W2 + [W1;W3] after the SwiGLU
+    backward, Wo + [Wq;Wk;Wv] after the attention backward: ops/gemm.py
+    ``accumulate_weight_grads``), else by the per-shape route of ops/gemm.py;
   * the fused [Wq;Wk;Wv] and [W1;W3] weights and their gradients as zero-copy
     views of the flat buffers when the parameters are adjacent there (no
     torch.cat / split);
@@ -50,6 +53,7 @@ from torch import Tensor
 from ..ops._ext import ops as hip
 from ..ops.attention import prerotate_default
 from ..ops.fp8 import add_rmsnorm_cast_t, norm_cast_ok, rope_ok, swiglu_bwd_cast_t, swiglu_cast_ok, swiglu_fwd_cast_t
+from ..ops import gemm as _gemm
 from ..ops.gemm import accumulate_weight_grad
 
 
@@ -257,6 +261,21 @@ class FusedBlockFn(torch.autograd.Function):
                     grads[id(p)] = dw[off : off + n]
                     off += n
 
+        def acc_weights(sets: list[tuple[list[Tensor], Tensor, Tensor]]) -> None:
+            """:func:`acc_weight` for several projections whose gradients are ready together: one grouped split-K
+            launch (ops/gemm.py ``accumulate_weight_grads``) when every stacked weight's gradient slots are adjacent
+            in the flat buffer, else one launch each."""
+            if main and _gemm._GROUP:
+                views = [_adjacent_view([p.main_grad for p in ps]) for ps, _, _ in sets]
+                if all(v is not None for v in views):
+                    _gemm.accumulate_weight_grads([(v, g_out, x_in) for v, (_, g_out, x_in) in zip(views, sets)])
+                    for ps, _, _ in sets:
+                        for p in ps:
+                            _notify(p)
+                    return
+            for ps, g_out, x_in in sets:
+                acc_weight(ps, g_out, x_in)
+
         fp8 = ctx.meta[7]
         w8s = getattr(ctx, "w8s", None)
         xt8s = getattr(ctx, "xt8s", None)
@@ -324,9 +343,11 @@ class FusedBlockFn(torch.autograd.Function):
         # ---- FFN
         dgu_q = None
         if w8s is None and _fuse_swiglu_bwd(dy, w2, gu):
-            acc_weight([w2], dy, a)
             # da = dy @ W2 with the SwiGLU backward in the GEMM epilogue (csrc/gemm_pp.hip): da never reaches HBM
             dgu = hip().gemm_swiglu_bwd(dy, w2.detach(), gu)
+            # the W2 and [W1; W3] weight gradients, both ready now, in one grouped split-K launch
+            acc_weights([([w2], dy, a), ([w1, w3], dgu, h2)])
+            dh2 = dx(dgu, [w1, w3], 2)
         else:
             da = proj(dy, [w2], 3, a)
             if xt8s is not None and _FP8_SWIGLU_CAST and swiglu_cast_ok(gu):
@@ -335,17 +356,24 @@ class FusedBlockFn(torch.autograd.Function):
                 dgu_q = swiglu_bwd_cast_t(fp8[2], da, gu, fp8[3] + 2)
             else:
                 dgu = hip().swiglu_bwd(da, gu)
-        dh2 = proj(dgu, [w1, w3], 2, h2, gq=dgu_q)
+            dh2 = proj(dgu, [w1, w3], 2, h2, gq=dgu_q)
         # with flat gradient slots the norm weights' gradients are added there by the column-sum kernel itself
         nacc = main and _NORM_DW_ACC
         dxm, dln2 = hip().rmsnorm_bwd(dh2, xm, ln2.detach(), r2, dxm_out, ln2.main_grad if nacc else None)
         # ---- attention
-        do = proj(dxm, [wo], 1, o)
+        # bf16 weight gradients: Wo's waits for the attention backward, so that it runs in one grouped launch with
+        # [Wq; Wk; Wv]'s (dxm stays alive until the ln1 backward anyway)
+        group_attn = xt8s is None and main and _gemm._GROUP
+        do = dx(dxm, [wo], 1) if group_attn else proj(dxm, [wo], 1, o)
         q, k, v = qkv[:, : H * D], qkv[:, H * D : (H + Hkv) * D], qkv[:, (H + Hkv) * D :]
         dqkv = hip().fa_bwd(do, q, k, v, o, lse, cos, sin, B, S, H, Hkv, D, True, use_rope, scale, ctx.prerotated,
                             ctx.dq_acc)
         ctx.dq_acc = None
-        dh1 = proj(dqkv, [wq, wk, wv], 0, h1)
+        if group_attn:
+            acc_weights([([wo], dxm, o), ([wq, wk, wv], dqkv, h1)])
+            dh1 = dx(dqkv, [wq, wk, wv], 0)
+        else:
+            dh1 = proj(dqkv, [wq, wk, wv], 0, h1)
         dx2, dln1 = hip().rmsnorm_bwd(dh1, x2, ln1.detach(), r1, dxm, ln1.main_grad if nacc else None)
         dxd = dx2 if ctx.has_xd else None
         if main:

@@ -103,9 +103,12 @@ class TransformerLM(nn.Module):
         dev = self.lm_head.weight.device
         L = len(self.layers)
         self.fp8_state = Fp8State(8 * L, dev, history=history, margin=margin)
-        # gradients: a 2x margin (e5m2 spans ~2^32, so the headroom costs nothing measurable); with margin 1 the
-        # Llama-shape parity run saturated its gradient casts by up to 2.9x at a loss-spike step, with 2 once by 1.5x
-        # (benchmarks/fp8_spike_probe.py, profiles/bench/fp8_spike_probe_margins_r5.log)
+        # gradients: a 2x margin by default (changed in round 5 from the e4m3 margin: a caller that wants a gradient
+        # margin below 2 now has to pass grad_margin).  e5m2 spans ~2^32, so the headroom costs nothing measurable;
+        # with margin 1 the Llama-shape parity run saturated its gradient casts by up to 2.9x at a loss-spike step,
+        # with 2 once by 1.5x (benchmarks/fp8_spike_probe.py, profiles/bench/fp8_spike_probe_margins_r5.log).  The
+        # margin bounds that saturation; it is not shown to remove the spike (step 18 of the parity run: loss
+        # 5.7844 -> 5.7836), whose cause stays unpinned.
         self.fp8_grad_state = (Fp8State(4 * L, dev, history=history, margin=max(margin, grad_margin), fmt="e5m2")
                                if dgrad else None)
         for i, layer in enumerate(self.layers):

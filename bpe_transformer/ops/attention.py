@@ -60,12 +60,17 @@ class _MaskedSDPAFn(torch.autograd.Function):
 def scaled_dot_product_attention(Q: Tensor, K: Tensor, V: Tensor, mask: Tensor | None = None,
                                  scale: float | None = None) -> Tensor:
     """``softmax(Q K^T * scale + (mask ? 0 : -inf)) V`` (scale 1/sqrt(d_k) by default) with any leading dims and a
-    boolean mask (True = attend; an int / float mask counts nonzero as attend) broadcastable to ``[..., q, k]``.
+    boolean mask (True = attend; an integer 0/1 mask counts nonzero as attend) broadcastable to ``[..., q, k]``.
+    A floating-point mask is refused: torch reads one as ADDITIVE (0 = attend, -inf = block), the opposite of the
+    nonzero-means-attend reading, and the reference contract (``tests/adapters.py:96``) takes boolean masks only.
     GPU fp32 / bf16 tensors run ``csrc/masked_sdpa.hip`` (fp32 math, head dims up to 128, at most 65535 batch-heads);
     anything else the oracle formula (``ops.reference``, with the same mask semantics)."""
     d_k = Q.shape[-1]
-    if mask is not None and mask.dtype != torch.bool:  # 0/1 int or float masks: nonzero = attend, on every path
-        mask = mask != 0
+    if mask is not None and mask.dtype != torch.bool:
+        if mask.is_floating_point():
+            raise TypeError("scaled_dot_product_attention: a floating-point mask is ambiguous (torch reads it as "
+                            "additive); pass a boolean mask (True = attend)")
+        mask = mask != 0  # 0/1 integer masks: nonzero = attend, on every path
     # the HIP kernel's grid.y is the batch-head count: at most 65535 (more falls back like other unsupported inputs)
     if not (Q.is_cuda and Q.dtype in (torch.float32, torch.bfloat16) and K.dtype == Q.dtype and V.dtype == Q.dtype
             and d_k <= 128 and V.shape[-1] <= 128 and Q.shape[:-2] == K.shape[:-2] == V.shape[:-2]

@@ -46,6 +46,7 @@
 #include "fa_common.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace bpe {
@@ -808,6 +809,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
                 const long j = j0 + 64 * wl + 16 * jb + 4 * (l >> 4);
                 if (st_on) *reinterpret_cast<f32x4*>(sp + i * N + j) = F8 != 0 ? acc[ib][jb] * osc : acc[ib][jb];
             }
+        GPP_STAMP(4);
     } else {
         epilogue_bf16<EPI, F8, 1>(acc, smem, g, wl, l, tid, i0, j0, jb, C, ldc, beta, ep, st_on, false, blockIdx.x);
         GPP_STAMP(4);
@@ -925,6 +927,174 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
         i0 = i0n;
         j0 = j0n;
         jb = jbn;
+    }
+}
+
+// Grouped weight gradients: the dW GEMMs of one layer that become ready together (W2 + [W1; W3] after the
+// SwiGLU-backward GEMM, Wo + [Wq; Wk; Wv] after the attention backward) in ONE split-K launch.  Each problem p is
+// dW_p[M_p][N_p] += dY_p^T X_p with dY_p [R][M_p] and X_p [R][N_p] token-major (or X_p^T [N_p][R] when BKM: the
+// transposed-copy route) over the same R tokens; their tiles are concatenated into one tile list and every tile
+// is split over K the same `splits` ways.  Why: a layer's dW shapes have 9-48 output tiles each, and a tile count
+// times a split count rarely fills whole waves of 256 CUs -- alone, GPT-2's W2 / W13 / Wo / Wqkv dW ran 240 / 240 /
+// 243 / 243 workgroups for 256 CUs, 5-6 % of the chip idle, plus a separate reduce launch each
+// (profiles/bench/dw_stamps_r6.log).  Grouped, the tiles x splits product is chosen for the whole set
+// (ops/gemm.py choose_splits_group).  The workgroup order is split-major with consecutive work ids on one XCD,
+// so the workgroups that read the same tokens (one split) share their dY / X rows in that XCD's L2.  Partials
+// go to each problem's fp32 slab region [splits][M_p][N_p] and dwg_reduce_kernel sums them in split order:
+// deterministic, bitwise equal to the single-problem split-K kernel at the same split count.
+constexpr int DWG_MAX = 4;
+struct DwGroup {
+    const __bf16* A[DWG_MAX];
+    const __bf16* B[DWG_MAX];
+    long lda[DWG_MAX], ldb[DWG_MAX];
+    long slab_off[DWG_MAX];  // float offset of problem p's slab region [splits][M_p][N_p]
+    int M[DWG_MAX], N[DWG_MAX];
+    int tile_end[DWG_MAX];  // inclusive prefix sums of the problems' tile counts
+    int np, ntiles, splits, R;
+    int prio;
+};
+
+template <bool BKM>
+__global__ void __launch_bounds__(NT, 1) gemm_pp_dwg_kernel(DwGroup gp, float* __restrict__ slab) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = w >> 2, wl = w & 3;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    const int split = wid / gp.ntiles, gt = wid % gp.ntiles;
+    // the problem of global tile gt, selected with constant indices only (no dynamic indexing of the kernarg
+    // arrays, which hipcc would copy to scratch)
+    const __bf16* A = gp.A[0];
+    const __bf16* B = gp.B[0];
+    long lda = gp.lda[0], ldb = gp.ldb[0], soff = gp.slab_off[0];
+    int M = gp.M[0], N = gp.N[0], t0 = 0;
+#pragma unroll
+    for (int q = 1; q < DWG_MAX; ++q) {
+        if (q < gp.np && gt >= gp.tile_end[q - 1]) {
+            A = gp.A[q];
+            B = gp.B[q];
+            lda = gp.lda[q];
+            ldb = gp.ldb[q];
+            soff = gp.slab_off[q];
+            M = gp.M[q];
+            N = gp.N[q];
+            t0 = gp.tile_end[q - 1];
+        }
+    }
+    const int tile = gt - t0, tiles_n = N / BT;
+    const int i0 = (tile / tiles_n) * BT, j0 = (tile % tiles_n) * BT;
+    const int nkt = gp.R / BK;
+    const int kb = (int)((long)split * nkt / gp.splits);
+    const int nk = (int)((long)(split + 1) * nkt / gp.splits) - kb;
+    GPP_STAMP(0);
+    GPP_STAMP_VAL(6, wid);
+#ifdef BPE_GPP_STAMPS
+    {
+        unsigned xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        GPP_STAMP_VAL(7, (long long)(xcc & 15));
+        GPP_STAMP_VAL(5, (long long)hw);
+    }
+#endif
+    if (gp.prio && g == 1) __builtin_amdgcn_s_setprio(1);
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // BKM (X^T copy, B K-major): the forward GEMM's spread schedule (1); both token-major: the weight-gradient
+    // one with a DMA piece inside each MFMA section (2) -- the same choices as the single-problem routes
+    constexpr bool SPLIT = !BKM;
+    const SpreadOff so = spread_offsets<false, BKM>(g, wl, l, (int)lda, (int)ldb);
+    {
+        const long k0 = (long)kb * BK;
+        const __bf16* a0 = tile_ptr<false>(A, lda, i0, k0);
+        const __bf16* b0 = tile_ptr<BKM>(B, ldb, j0, k0);
+        dma_pair(a0, so.a0, smem, so.la0);
+        dma_pair(b0, so.b0, smem + OPB, so.lb0);
+        dma_pair(b0, so.b1, smem + OPB, so.lb1);
+        dma_pair(a0, so.a1, smem, so.la1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+    }
+    GPP_STAMP(1);
+    if (g == 1) bar();  // the stagger
+    for (int kt = 0; kt < nk; ++kt) {
+        char* cur = smem + (kt & 1) * STAGE;
+        char* nxt = smem + ((kt + 1) & 1) * STAGE;
+        const long k1 = (long)(kb + kt + 1) * BK;
+        ktile_spread<false, BKM, 0, SPLIT, 0>(cur, nxt, kt + 1 < nk, tile_ptr<false>(A, lda, i0, k1),
+                                              tile_ptr<BKM>(B, ldb, j0, k1), so, g, wl, l, acc, false, kt);
+    }
+    GPP_STAMP(2);
+    if (g == 0) bar();
+    __builtin_amdgcn_s_waitcnt(0x70);
+    bar();
+    float* sp = slab + soff + (long)split * M * N;
+#pragma unroll
+    for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) {
+            const long i = i0 + 128 * g + 16 * ib + (l & 15);
+            const long j = j0 + 64 * wl + 16 * jq + 4 * (l >> 4);
+            *reinterpret_cast<f32x4*>(sp + i * N + j) = acc[ib][jq];
+        }
+    GPP_STAMP(4);
+}
+
+// C_p = beta * C_p + sum over splits of problem p's slab region, in split order (the grouped form of
+// splitk_reduce_kernel: one launch for every problem of a group).  end4[p]: inclusive prefix sums of M_p N_p / 4.
+struct DwOut {
+    void* C[DWG_MAX];
+    long ldc[DWG_MAX];
+    long slab_off[DWG_MAX];
+    long end4[DWG_MAX];
+    int N[DWG_MAX];
+    int np, splits;
+    float beta;
+};
+
+template <typename CT>
+__global__ void __launch_bounds__(256) dwg_reduce_kernel(const float* __restrict__ slab, DwOut o) {
+    const long total4 = o.end4[o.np - 1];
+    for (long t = blockIdx.x * 256L + threadIdx.x; t < total4; t += (long)gridDim.x * 256) {
+        CT* C = (CT*)o.C[0];
+        long ldc = o.ldc[0], soff = o.slab_off[0], b4 = 0, mn = o.end4[0] * 4;
+        int N = o.N[0];
+#pragma unroll
+        for (int q = 1; q < DWG_MAX; ++q) {
+            if (q < o.np && t >= o.end4[q - 1]) {
+                C = (CT*)o.C[q];
+                ldc = o.ldc[q];
+                soff = o.slab_off[q];
+                b4 = o.end4[q - 1];
+                mn = (o.end4[q] - o.end4[q - 1]) * 4;
+                N = o.N[q];
+            }
+        }
+        const long e = (t - b4) * 4;
+        const long i = e / N, j = e % N;
+        const float* sp = slab + soff + e;
+        f32x4 s = *reinterpret_cast<const f32x4*>(sp);
+        for (int k = 1; k < o.splits; ++k) s += *reinterpret_cast<const f32x4*>(sp + (long)k * mn);
+        if constexpr (sizeof(CT) == 4) {
+            f32x4* cp = reinterpret_cast<f32x4*>(C + i * ldc + j);
+            if (o.beta != 0.f) s += o.beta * *cp;
+            *cp = s;
+        } else {
+            u16x4* cp = reinterpret_cast<u16x4*>(C + i * ldc + j);
+            if (o.beta != 0.f) {
+                const u16x4 c = *cp;
+                s[0] += o.beta * bf2f(c[0]);
+                s[1] += o.beta * bf2f(c[1]);
+                s[2] += o.beta * bf2f(c[2]);
+                s[3] += o.beta * bf2f(c[3]);
+            }
+            *cp = u16x4{f2bf(s[0]), f2bf(s[1]), f2bf(s[2]), f2bf(s[3])};
+        }
     }
 }
 
@@ -1173,6 +1343,55 @@ template <bool AK, bool BKM, bool SLAB>
 static void launch_pp(const __bf16* a, long lda, const __bf16* b, long ldb, float* slab, __bf16* c, long ldc,
                       float beta, int M, int N, int R, int splits, hipStream_t s) {
     launch_pp1<AK, BKM, SLAB, BPE_GPP_DIAG>(a, lda, b, ldb, slab, c, ldc, beta, M, N, R, splits, s);
+}
+
+// Grouped weight gradients (gemm_pp_dwg_kernel, then dwg_reduce_kernel): np <= 4 problems C_p[M_p][N_p] =
+// beta C_p + dY_p^T X_p over R tokens, every tile split `splits` ways; slab: splits * sum M_p N_p floats.
+void launch_gemm_pp_dw_group(int np, const void* const* A, const long* lda, const void* const* B, const long* ldb,
+                             int b_kmajor, void* const* C, const long* ldc, const int* M, const int* N, int R,
+                             int splits, float beta, float* slab, int c_f32, hipStream_t s) {
+    DwGroup gp{};
+    DwOut o{};
+    long off = 0, e4 = 0;
+    int tiles = 0;
+    for (int p = 0; p < np; ++p) {
+        gp.A[p] = (const __bf16*)A[p];
+        gp.B[p] = (const __bf16*)B[p];
+        gp.lda[p] = lda[p];
+        gp.ldb[p] = ldb[p];
+        gp.slab_off[p] = o.slab_off[p] = off;
+        gp.M[p] = M[p];
+        gp.N[p] = o.N[p] = N[p];
+        tiles += (M[p] / BT) * (N[p] / BT);
+        gp.tile_end[p] = tiles;
+        off += (long)splits * M[p] * N[p];
+        o.C[p] = C[p];
+        o.ldc[p] = ldc[p];
+        e4 += (long)M[p] * N[p] / 4;
+        o.end4[p] = e4;
+    }
+    gp.np = o.np = np;
+    gp.ntiles = tiles;
+    gp.splits = o.splits = splits;
+    gp.R = R;
+    gp.prio = prio_mode();
+    o.beta = beta;
+    if (b_kmajor) {
+        static bool attr = false;
+        auto* k = &gemm_pp_dwg_kernel<true>;
+        if (!attr) lds_attr(k), attr = true;
+        k<<<tiles * splits, NT, LDS_LAUNCH, s>>>(gp, slab);
+    } else {
+        static bool attr = false;
+        auto* k = &gemm_pp_dwg_kernel<false>;
+        if (!attr) lds_attr(k), attr = true;
+        k<<<tiles * splits, NT, LDS_LAUNCH, s>>>(gp, slab);
+    }
+    const int g = (int)std::min<long>((e4 + 255) / 256, 2048);
+    if (c_f32)
+        dwg_reduce_kernel<float><<<g, 256, 0, s>>>(slab, o);
+    else
+        dwg_reduce_kernel<__bf16><<<g, 256, 0, s>>>(slab, o);
 }
 
 void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,

@@ -87,6 +87,12 @@ bool gemm_pp_shape_ok(int M, int N, int R, int splits);
 void launch_gemm_pp(int a_kmajor, int b_kmajor, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                     float beta, int M, int N, int R, int splits, float* slab, int c_f32, hipStream_t s);
 
+// grouped weight gradients: np <= 4 problems C_p (+)= dY_p^T X_p over the same R tokens in one split-K launch and
+// one ordered reduce (X_p token-major, or X_p^T [N_p][R] with b_kmajor); slab: splits * sum M_p N_p floats
+void launch_gemm_pp_dw_group(int np, const void* const* A, const long* lda, const void* const* B, const long* ldb,
+                             int b_kmajor, void* const* C, const long* ldc, const int* M, const int* N, int R,
+                             int splits, float beta, float* slab, int c_f32, hipStream_t s);
+
 // fp8 x fp8 -> bf16 on the ping-pong kernel with v_mfma_scale_f32_16x16x128_f8f6f4: C = A8 B8^T * sa * sb,
 // A8 [M][K] (fmt_a 0 e4m3 / 1 e5m2), B8 [N][K] e4m3, both K-major; strides in bytes (A, B) / elements (C)
 void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,

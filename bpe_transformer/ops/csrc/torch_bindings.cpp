@@ -411,6 +411,60 @@ void gemm_pp(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kma
                    c32 ? 1 : 0, cur_stream());
 }
 
+// Grouped weight gradients (gemm_pp.hip gemm_pp_dw_group): gs[p] = beta * gs[p] + dys[p]^T xs[p] for up to 4
+// problems over the same R tokens in ONE split-K launch plus one ordered reduce.  dys[p] [R, M_p] token-major;
+// xs[p] [R, N_p] token-major, or X^T [N_p, R] with x_kmajor; gs[p] [M_p, N_p], all bf16 or all fp32.
+void gemm_pp_dw_group(at::TensorList gs, at::TensorList dys, at::TensorList xs, bool x_kmajor, int64_t splits,
+                      double beta) {
+    const int np = (int)gs.size();
+    TORCH_CHECK(np >= 1 && np <= 4 && (int)dys.size() == np && (int)xs.size() == np,
+                "gemm_pp_dw_group: 1-4 problems, one dY and one X per gradient");
+    const bool c32 = gs[0].scalar_type() == at::kFloat;
+    const void* A[4];
+    const void* B[4];
+    void* C[4];
+    long lda[4], ldb[4], ldc[4];
+    int M[4], N[4];
+    const int R = (int)dys[0].size(0);
+    long slab_elems = 0;
+    for (int p = 0; p < np; ++p) {
+        const at::Tensor& g = gs[p];
+        const at::Tensor& dy = dys[p];
+        const at::Tensor& x = xs[p];
+        check_cuda(g, "g");
+        TORCH_CHECK(g.scalar_type() == gs[0].scalar_type() &&
+                        (g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat) &&
+                        dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
+                    "gemm_pp_dw_group: bf16 operands, gradients all bf16 or all fp32");
+        TORCH_CHECK(g.dim() == 2 && dy.dim() == 2 && x.dim() == 2 && g.stride(1) == 1 && dy.stride(1) == 1 &&
+                        x.stride(1) == 1, "gemm_pp_dw_group: 2-D row-major operands required");
+        TORCH_CHECK(dy.device() == g.device() && x.device() == g.device() && g.device() == gs[0].device(),
+                    "gemm_pp_dw_group: operands on different devices");
+        M[p] = (int)g.size(0);
+        N[p] = (int)g.size(1);
+        TORCH_CHECK(dy.size(0) == R && dy.size(1) == M[p], "gemm_pp_dw_group: dY [R, M] with one R for all problems");
+        TORCH_CHECK(x_kmajor ? (x.size(0) == N[p] && x.size(1) == R) : (x.size(0) == R && x.size(1) == N[p]),
+                    "gemm_pp_dw_group: X shape mismatch");
+        TORCH_CHECK(gemm_pp_shape_ok(M[p], N[p], R, (int)splits),
+                    "gemm_pp_dw_group: M, N must be multiples of 256, R of 64 (>= splits)");
+        TORCH_CHECK(dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0 && g.stride(0) % 8 == 0,
+                    "gemm_pp_dw_group: 16-byte row alignment");
+        TORCH_CHECK(dy.stride(0) * 256 < (1L << 31) && x.stride(0) * 256 < (1L << 31),
+                    "gemm_pp_dw_group: leading dimension too large for 32-bit tile offsets");
+        A[p] = dy.data_ptr();
+        B[p] = x.data_ptr();
+        C[p] = g.data_ptr();
+        lda[p] = dy.stride(0);
+        ldb[p] = x.stride(0);
+        ldc[p] = g.stride(0);
+        slab_elems += splits * (long)M[p] * N[p];
+    }
+    DevGuard dg(gs[0].device());
+    auto slab = at::empty({slab_elems}, gs[0].options().dtype(at::kFloat));
+    launch_gemm_pp_dw_group(np, A, lda, B, ldb, x_kmajor ? 1 : 0, C, ldc, M, N, R, (int)splits, (float)beta,
+                            slab.data_ptr<float>(), c32 ? 1 : 0, cur_stream());
+}
+
 // y = (a8 @ b8^T) * sa * sb in bf16: a8 [M, K] e4m3 / e5m2, b8 [N, K] e4m3 (both K-major), sa / sb device fp32
 // scalars (the per-tensor inverse scales); the hand-written fp8 MFMA ping-pong kernel (gemm_pp.hip)
 at::Tensor gemm_fp8(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor& sa, const at::Tensor& sb) {
@@ -1067,6 +1121,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gemm_fp8_rope(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor cos, Tensor sin, int S, int D, "
           "int rot_cols) -> Tensor");
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
+    m.def("gemm_pp_dw_group(Tensor(a!)[] gs, Tensor[] dys, Tensor[] xs, bool x_kmajor, int splits, float beta=1.0) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
     m.def("transpose_bf16(Tensor w) -> Tensor");
@@ -1114,6 +1169,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("scale_", &scale_);
     m.impl("gemm", &gemm);
     m.impl("gemm_pp", &gemm_pp);
+    m.impl("gemm_pp_dw_group", &gemm_pp_dw_group);
     m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
     m.impl("gemm_swiglu_fwd", &gemm_swiglu_fwd);
     m.impl("gemm_qkv_rope", &gemm_qkv_rope);

@@ -1,15 +1,22 @@
-"""Hand-written gfx950 split-K MFMA GEMMs (``csrc/gemm.hip``) for weight gradients.
+"""Weight-gradient GEMMs (``g += dy^T @ x``) on the hand-written gfx950 kernels.
 
 ``accumulate_weight_grad(g, dy, x)`` computes ``g += dy^T @ x`` where
 ``dy: [T, N]`` and ``x: [T, K]`` are token-major activations (T = batch*seq)
 and ``g: [N, K]`` is a view of the flat bf16 gradient buffer.  The reduction
-runs over all T tokens, which for a training step is large (16k-64k) while
-N x K is small: the kernel splits T across workgroups (enough to fill all 256
-CUs) and reduces the fp32 partials deterministically into ``g``.
+runs over all T tokens, which for a training step is large (16k-128k) while
+N x K is small: the kernels split T across workgroups (enough to fill all 256
+CUs) and reduce the fp32 partials deterministically into ``g``.
 
-Two kernels: the 256 x 256 tile (8 waves, LDS-DMA staging, one workgroup per
-CU) for shapes that are multiples of 256, the 128 x 128 tile otherwise.
-Shapes neither covers go to hipBLASLt (``addmm_``).
+Routes per shape (``_run``; the measured choice per training shape is in ``tuning/dw_routes.json``):
+
+* ``pp``  -- the 8-wave ping-pong kernel (``csrc/gemm_pp.hip``), both operands token-major;
+* ``ppt`` -- the same kernel on a transposed copy of X (B K-major);
+* ``hip256`` / ``hip128`` -- the 256 x 256 and 128 x 128 split-K kernels of ``csrc/gemm.hip``;
+* ``blas`` -- hipBLASLt (``addmm_``), for shapes none of the HIP kernels covers.
+
+``accumulate_weight_grads(items)`` runs the dW GEMMs of one layer that are ready at the same time as ONE grouped
+split-K launch (``gemm_pp_dw_group``: the ping-pong kernel over the concatenated tile lists, one ordered reduce),
+so that tiles x splits fills whole waves of the 256 CUs for the set instead of for each shape alone.
 """
 
 from __future__ import annotations
@@ -123,7 +130,9 @@ def use_pp(n: int, k: int, t: int) -> bool:
 def _candidates(n: int, k: int, t: int) -> list[str]:
     c = []
     if use_pp(n, k, t):
-        c += ["pp", "ppt"]
+        c.append("pp")
+        if t * 256 < 2**31:  # ppt's X^T [K][T] has leading dimension T (the kernel's 32-bit tile offsets)
+            c.append("ppt")
     if use_tile256(n, k, t):
         c.append("hip256")
     elif supported(n, k, t):
@@ -207,10 +216,10 @@ def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
     """``g += dy.T @ x`` (bf16 operands, fp32 accumulation; ``g`` bf16 or fp32 -- an fp32 gradient buffer gets the
     fp32 sum, through the kernels' fp32 partial slab and ordered reduce).
 
-    Routes per shape between the 256-tile HIP kernel, the 128-tile HIP kernel and hipBLASLt; the first call
-    for a shape times the candidates (``BPE_GEMM_AUTOTUNE=0``: take the HIP kernel whenever it applies).
-    Measured (benchmarks/gemm_dw.py): the HIP kernel wins every GPT-2-small dW shape 1.4-2.3x; hipBLASLt
-    keeps Llama's 2048 x 5632 one.
+    Routes per shape (module docstring): the shape's entry in ``tuning/dw_routes.json``, else the first call for a
+    shape times the candidates (``BPE_GEMM_AUTOTUNE=0``: take the first HIP candidate).  Measured
+    (benchmarks/gemm_dw.py, dw_ppt.py): the HIP kernels win every GPT-2-small dW shape 1.4-2.3x over hipBLASLt;
+    hipBLASLt keeps Llama's 2048 x 5632 one at 16 384 tokens.
     """
     n, k = g.shape
     t = dy.shape[0]
@@ -240,3 +249,72 @@ def matmul_nt(a: Tensor, b: Tensor, out: Tensor | None = None, beta: float = 0.0
         beta = 0.0
     ops().gemm(a, True, b, True, out, beta, choose_splits(m, n, r), 128)
     return out
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Grouped weight gradients (one split-K launch for the dW GEMMs of a layer that become ready together)
+
+_GROUP = os.environ.get("BPE_DW_GROUP", "1") == "1"  # module flag (A/B runs and tests compare the per-shape routes)
+_group_used: dict[tuple, int] = {}
+
+
+def choose_splits_group(tiles: int, t: int, mn: int, cus: int = _CUS) -> int:
+    """Split count for a grouped launch of ``tiles`` 256 x 256 tiles over ``t`` tokens (``mn`` = sum of the output
+    elements), in units of one K-tile of the loop: every wave of ``cus`` workgroups lasts as long as a split's
+    K-tiles plus a fixed ~6.5 K-tiles (prologue round trip + the 256 KiB fp32 slab store; per-workgroup stamps,
+    profiles/bench/dw_stamps_r6.log), and the slab round trip through HBM costs ~8 bytes per element per split."""
+    nk = t // 64
+    best, best_cost = 1, None
+    for s in range(1, 65):
+        if nk // s < 8:
+            break
+        waves = -(-tiles * s // cus)
+        cost = waves * (-(-nk // s) + 6.5) + (s * mn * 8.4e-7 if s > 1 else 0.0)
+        if best_cost is None or cost < best_cost * 0.99:
+            best, best_cost = s, cost
+    return best
+
+
+def _group_ok(items: list[tuple[Tensor, Tensor, Tensor]]) -> bool:
+    if not (2 <= len(items) <= 4):
+        return False
+    g0, dy0, _ = items[0]
+    t = dy0.shape[0]
+    if not (g0.is_cuda and g0.dtype in (torch.bfloat16, torch.float32) and t % 64 == 0 and t * 256 < 2**31):
+        return False
+    for g, dy, x in items:
+        n, k = g.shape
+        if not (g.dtype == g0.dtype and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+                and g.device == g0.device and dy.shape == (t, n) and x.shape == (t, k) and n % 256 == 0
+                and k % 256 == 0 and g.stride(1) == 1 and dy.stride(1) == 1 and x.stride(1) == 1
+                and g.stride(0) % 8 == 0 and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0
+                and dy.stride(0) * 256 < 2**31 and x.stride(0) * 256 < 2**31
+                and g.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0):
+            return False
+    return True
+
+
+def accumulate_weight_grads(items: list[tuple[Tensor, Tensor, Tensor]]) -> None:
+    """``g += dy^T @ x`` for every ``(g, dy, x)`` of ``items`` (the same token count T for all).
+
+    Two to four eligible shapes (256-multiples, bf16 operands, all-bf16 or all-fp32 gradients) run as one grouped
+    split-K launch of the ping-pong kernel plus one ordered reduce (``gemm_pp_dw_group``); the split count is chosen
+    for the set (:func:`choose_splits_group`), so the result is deterministic and depends on the shapes only (the
+    same on every rank).  Otherwise -- or with ``BPE_DW_GROUP=0`` -- each item takes its per-shape route."""
+    if _GROUP and _group_ok(items):
+        t = items[0][1].shape[0]
+        tiles = sum((g.shape[0] // 256) * (g.shape[1] // 256) for g, _, _ in items)
+        mn = sum(g.numel() for g, _, _ in items)
+        s = choose_splits_group(tiles, t, mn)
+        key = tuple((g.shape[0], g.shape[1]) for g, _, _ in items) + (t,)
+        _group_used[key] = s
+        ops().gemm_pp_dw_group([g for g, _, _ in items], [dy for _, dy, _ in items], [x for _, _, x in items],
+                               False, s, 1.0)
+        return
+    for g, dy, x in items:
+        accumulate_weight_grad(g, dy, x)
+
+
+def groups_summary() -> dict[str, int]:
+    """``{"N,K+N,K+...,T": splits}`` for every grouped dW launch so far in this process (bench output)."""
+    return {"+".join(f"{n},{k}" for n, k in key[:-1]) + f",{key[-1]}": s for key, s in sorted(_group_used.items())}

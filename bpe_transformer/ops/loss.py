@@ -1,9 +1,11 @@
 """Cross-entropy ops (``csrc/cross_entropy.hip``).
 
-``lm_head_cross_entropy`` fuses the LM-head GEMM with softmax-CE.  Two modes:
+``lm_head_cross_entropy`` is the LM head plus softmax-CE as one autograd node (the GEMMs are separate kernels:
+hipBLASLt for the logits and the input gradient, the ping-pong kernel for the weight gradient; the CE is a
+register-resident HIP kernel between them).  Two modes:
 
 * ``"logits"`` (default, fastest measured): the logits buffer is written once
-  by the GEMM, read by the CE kernel which overwrites it IN PLACE with
+  by the hipBLASLt GEMM, read by the CE kernel which overwrites it IN PLACE with
   ``(softmax - onehot) / n``, and the backward is two GEMMs scaled by the
   incoming gradient (applied to the small GEMM outputs, never to the
   [tokens, vocab] buffer).  One [tokens, vocab] bf16 buffer lives from forward

@@ -1,4 +1,4 @@
-"""A pickle READER that constructs only builtin data: ints, bytes, str, lists, tuples and dicts.
+"""A pickle READER that constructs only builtin data: ints, bytes, str, lists, tuples, dicts and sets.
 
 Tokenizer artifacts (``vocab.pkl`` = ``dict[int, bytes]``, ``merges.pkl`` = ``list[tuple[bytes, bytes]]``,
 reference ``bpe_trainer.py:447-472``) are pickles, and files of that format may come from anywhere.  This module
@@ -9,7 +9,8 @@ stack.  Every opcode that could look up a global, call a callable or build an ob
 raises :class:`UnsafePickleError`, so nothing from the file is ever executed.
 
 Covers protocols 2-5 as written by ``pickle.dump`` for these types (``MEMOIZE`` / ``BINPUT`` memo,
-``FRAME``, ``SHORT_BINBYTES`` ... ``BINBYTES8``, ``SETITEMS``, ``APPENDS``, ``TUPLE2``).
+``FRAME``, ``SHORT_BINBYTES`` ... ``BINBYTES8``, ``SETITEMS``, ``APPENDS``, ``TUPLE2``, and the set opcodes
+``EMPTY_SET`` / ``ADDITEMS`` / ``FROZENSET`` of the reference's snapshot pickles).
 """
 
 from __future__ import annotations
@@ -66,6 +67,20 @@ def _loads(data: bytes):
             stack.append([])
         elif name == "EMPTY_TUPLE":
             stack.append(())
+        elif name == "EMPTY_SET":
+            stack.append(set())
+        elif name == "ADDITEMS":
+            k0 = marks.pop()
+            items = stack[k0:]
+            del stack[k0:]
+            if not isinstance(stack[-1], set):
+                raise UnsafePickleError("malformed pickle: ADDITEMS on a non-set")
+            stack[-1].update(items)
+        elif name == "FROZENSET":
+            k0 = marks.pop()
+            items = stack[k0:]
+            del stack[k0:]
+            stack.append(frozenset(items))
         elif name == "MARK":
             marks.append(len(stack))
         elif name == "MEMOIZE":

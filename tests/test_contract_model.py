@@ -42,13 +42,20 @@ def test_4d_scaled_dot_product_attention(numpy_snapshot, q, k, v, mask):
     numpy_snapshot.assert_match(run_scaled_dot_product_attention(q4, k4, v4, m4), atol=1e-6)
 
 
-@pytest.mark.parametrize("mdtype", [torch.int64, torch.float32, torch.uint8])
+@pytest.mark.parametrize("mdtype", [torch.int64, torch.uint8])
 def test_scaled_dot_product_attention_nonbool_mask(q, k, v, mask, mdtype):
-    """A 0/1 int / float mask means the same as the boolean one (nonzero = attend) on every path; the HIP kernel
+    """A 0/1 integer mask means the same as the boolean one (nonzero = attend) on every path; the HIP kernel
     treats it so too (``ops/attention.py``)."""
     ref = run_scaled_dot_product_attention(q, k, v, mask)
     got = run_scaled_dot_product_attention(q, k, v, mask.to(mdtype))
     assert torch.equal(got, ref)
+
+
+def test_scaled_dot_product_attention_float_mask_refused(q, k, v, mask):
+    """A floating-point mask is ambiguous -- torch reads it as additive (0 = attend, -inf = block), the inverse of
+    the nonzero-means-attend reading -- so it is refused instead of silently inverted."""
+    with pytest.raises(TypeError, match="floating-point mask"):
+        run_scaled_dot_product_attention(q, k, v, mask.to(torch.float32))
 
 
 def test_rope(numpy_snapshot, in_embeddings, d_model, theta, n_queries, pos_ids):

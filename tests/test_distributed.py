@@ -191,3 +191,36 @@ def test_bench_contract_two_ranks_cpu(tmp_path, zero):
     assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1 and out["scaling"] == "weak"
     assert out["config"]["parallelism"] == ("dp2-zero1" if zero else "dp2") and out["config"]["global_batch"] == 4
     assert out["value"] > 0 and abs(out["value"] - 2 * 2 * 2 * 32 / (out["ms_per_step"] * 2 / 1000)) < 0.02 * out["value"]
+    # the self-validation the first multi-GPU record carries: world size, backend, bucket layout, wire dtype and the
+    # untimed replica-consistency step's verdict
+    d = out["dist"]
+    assert d["world_size"] == 2 and d["backend"] == "gloo" and d["buckets"] == len(d["bucket_mb"]) >= 1
+    assert d["comm_dtype"] in ("float32", "bfloat16")
+    assert d["consistency_check"] == ("data bit-identical across ranks" if zero else
+                                      "grad+data bit-identical across ranks")
+
+
+@pytest.mark.parametrize("zero", [0])
+def test_bench_refuses_a_corrupted_replica(tmp_path, zero):
+    """A replica whose weights were perturbed before the consistency step makes bench.py fail with the divergence
+    error instead of printing a throughput record.  (Plain data parallelism only: under ZeRO-1 every rank's weights
+    are re-gathered from the owners' shards each step, so a perturbed replica heals and the data check guards the
+    all-gather itself.)"""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--device", "cpu", "--model", "tinystories-17m", "--seq", "32", "--batch", "2",
+           "--steps", "1", "--warmup", "1", "--zero", str(zero), "--debug-corrupt-rank", "1"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode != 0
+    assert "divergence" in r.stderr + r.stdout
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

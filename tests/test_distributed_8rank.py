@@ -133,6 +133,9 @@ def test_bench_contract_eight_ranks_cpu(tmp_path):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 8
     assert out["allreduce_dtype"] == "float32" and out["grad_dtype"] == "float32"  # CPU plumbing config is fp32
+    d = out["dist"]
+    assert d["world_size"] == 8 and d["backend"] == "gloo" and d["buckets"] == len(d["bucket_mb"]) >= 1
+    assert d["consistency_check"] == "grad+data bit-identical across ranks"
     assert abs(out["value"] - 2 * 8 * 16 / (out["ms_per_step"] * 2 / 1000)) < 0.02 * out["value"]
 
 
@@ -166,6 +169,24 @@ def test_allreduce_in_fp32_for_bf16_grads():
     got16 = torch.from_numpy(r16[0][1])
     assert torch.equal(got32, exact)
     assert (got16 != exact).float().mean() > 0.01
+
+
+def test_bf16_wire_error_bound_at_eight_ranks():
+    """The default wire dtype decision (docs/performance.md "Streams and data parallelism"): with bf16 gradients
+    all-reduced in bf16 at N = 8 (gloo adds rank by rank in bf16, as a ring adds hop by hop), the mean lands within
+    2 bf16 ulps of the exact fp32 mean rounded once, and within 1 ulp for most elements -- the size of the rounding
+    every bf16 weight gradient already carries -- so bf16 stays the default wire dtype and ``--comm-dtype fp32``
+    is the exact option."""
+    world = 8
+    r16 = _spawn(_comm_worker, world, None)
+    vals = torch.stack([torch.from_numpy(r16[r][0]) for r in range(world)]).double()
+    exact = (vals.sum(0) / world).float().to(torch.bfloat16).float()
+    got16 = torch.from_numpy(r16[0][1])
+    ulps = (got16.double() - exact.double()).abs() / 2.0**-7  # every value lies in [1, 2): one bf16 ulp is 2^-7
+    for r in range(1, world):  # every rank holds the same result
+        assert torch.equal(torch.from_numpy(r16[r][1]), got16)
+    assert ulps.max() <= 2.0, float(ulps.max())
+    assert (ulps <= 1.0).float().mean() > 0.9, float((ulps <= 1.0).float().mean())
 
 
 def _ckpt_worker(rank, world, port, path, out_q):

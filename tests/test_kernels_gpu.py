@@ -499,6 +499,20 @@ def test_gemm_swiglu_bwd(gpu_device, gpp_mode):
     assert rel(dgu.cpu(), unfused.cpu()) < 2e-2
 
 
+def test_gemm_swiglu_bwd_bitwise_on_exact_products(gpu_device, gpp_mode):
+    """Small-integer dY and W2 make da = dY W2 exact (and exact in bf16), so the fused epilogue (packed two-element
+    fp32 arithmetic, BPE_GPP_PK=1) must give bitwise the unfused ``swiglu_bwd`` of that da on the same gu."""
+    torch.manual_seed(6)
+    M, d, F = 512, 192, 768
+    dy = torch.randint(-2, 3, (M, d), device=gpu_device).to(torch.bfloat16)
+    w2 = torch.randint(-1, 2, (d, F), device=gpu_device).to(torch.bfloat16)
+    gu = torch.randn(M, 2 * F, device=gpu_device, dtype=torch.bfloat16)
+    da = (dy.float() @ w2.float()).to(torch.bfloat16)
+    assert torch.equal(da.float(), dy.float() @ w2.float())  # exact
+    dgu = torch.ops.bpe_hip.gemm_swiglu_bwd(dy, w2, gu)
+    assert torch.equal(dgu, torch.ops.bpe_hip.swiglu_bwd(da.contiguous(), gu))
+
+
 @pytest.mark.parametrize("M,d,F", [(512, 192, 768), (256, 64, 128)])
 def test_gemm_swiglu_fwd(gpu_device, gpp_mode, M, d, F):
     """x @ [W1; W3]^T with a = silu(g) * u in the epilogue.  Small-integer operands make gu exact, so gu must
@@ -574,6 +588,55 @@ def test_gemm_pp_persistent_bitwise_many_tiles(gpu_device):
     for t0, t1 in zip(outs[0], outs[1]):
         assert torch.equal(t0, t1)
     assert rel(outs[1][0].cpu(), (x.float() @ w.float().t()).cpu()) < 1e-2
+
+
+@pytest.mark.parametrize("x_k", [False, True])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_pp_dw_group_exact(gpu_device, x_k, dtype, splits):
+    """Grouped weight gradients on small-integer operands: three problems of different shapes and strides (one a
+    column slice of a wider buffer, like a stacked-weight gradient view) in one launch, every output exact."""
+    torch.manual_seed(3)
+    R = 1216
+    shapes = [(512, 768), (256, 256), (768, 512)]
+    gs, dys, xs, refs = [], [], [], []
+    for i, (m, n) in enumerate(shapes):
+        dy = torch.randint(-1, 2, (R, m), device=gpu_device).to(torch.bfloat16)
+        x = torch.randint(-1, 2, (R, n), device=gpu_device).to(torch.bfloat16)
+        wide = torch.randint(-3, 4, (m, n + 256 * i), device=gpu_device).to(dtype)
+        g = wide[:, 256 * i :]  # a strided view: row stride != N for i > 0
+        refs.append(g.float() + dy.float().t() @ x.float())
+        gs.append(g)
+        dys.append(dy)
+        xs.append(x.t().contiguous() if x_k else x)
+    torch.ops.bpe_hip.gemm_pp_dw_group(gs, dys, xs, x_k, splits, 1.0)
+    for g, ref in zip(gs, refs):
+        assert torch.equal(g.float().cpu(), ref.cpu())
+
+
+def test_gemm_pp_dw_group_bitwise_vs_single(gpu_device):
+    """Random operands at GPT-2-like dW shapes (more workgroups than CUs): the grouped launch runs each tile's
+    split exactly as the single-problem split-K kernel does and reduces in the same split order, so every
+    gradient matches the per-shape ``gemm_pp`` route bitwise; repeated launches are bitwise stable."""
+    from bpe_transformer.ops.gemm import accumulate_weight_grads, choose_splits_group
+
+    torch.manual_seed(4)
+    T = 16384
+    shapes = [(768, 2048), (4096, 768)]  # W2 and [W1; W3] of GPT-2-small: 24 + 48 tiles
+    dys = [torch.randn(T, m, device=gpu_device, dtype=torch.bfloat16) * 0.1 for m, _ in shapes]
+    xs = [torch.randn(T, n, device=gpu_device, dtype=torch.bfloat16) for _, n in shapes]
+    g0 = [torch.randn(m, n, device=gpu_device, dtype=torch.bfloat16) for m, n in shapes]
+    s = choose_splits_group(72, T, sum(m * n for m, n in shapes))
+    single = [g.clone() for g in g0]
+    for g, dy, x in zip(single, dys, xs):
+        torch.ops.bpe_hip.gemm_pp(dy, False, x, False, g, 1.0, s)
+    for _ in range(2):
+        grouped = [g.clone() for g in g0]
+        accumulate_weight_grads(list(zip(grouped, dys, xs)))
+        for a, b in zip(grouped, single):
+            assert torch.equal(a, b)
+    ref = g0[1].float() + dys[1].float().t() @ xs[1].float()
+    assert rel(grouped[1].cpu(), ref.cpu()) < 1e-2
 
 
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])

@@ -314,9 +314,14 @@ def test_fp8_engine_tracks_bf16_engine(gpu_device, monkeypatch, route, wgrad):
     assert rel[-1] < 0.02, rel[-1]
 
 
-def _same_weights_losses(c: Shape, steps, gpu_device, margin: float = 1.0) -> dict:
+def _same_weights_losses(c: Shape, steps, gpu_device, margin: float = 1.0, train: bool = False) -> dict:
     """Train the bf16 engine and, before step s in ``steps``, evaluate batch s on the SAME weights in bf16 and in fp8
-    (scales calibrated on the 16 preceding batches, what the delayed recipe holds at that step)."""
+    (scales calibrated on the 16 preceding batches, what the delayed recipe holds at that step).
+
+    ``train``: evaluate with gradients enabled (no backward, no optimizer step), so the fused block takes its
+    TRAINING forward -- with fp8 weight gradients the two RMSNorms write h1 / h2 only as e4m3 in both layouts
+    (``add_rmsnorm_cast_t``) and the gate writes a only as e4m3 (``swiglu_fwd_cast_t``), kernels an eval-mode forward
+    never runs."""
     ids, vocab = _tokens()
     model = _ours(vocab, c, gpu_device)
     eng = _engine(model, 1, c)
@@ -324,15 +329,15 @@ def _same_weights_losses(c: Shape, steps, gpu_device, margin: float = 1.0) -> di
     out = {}
     for it in range(max(steps) + 1):
         if it in steps:
-            with torch.no_grad():
+            with torch.set_grad_enabled(train):
                 x, y = data[it]
-                lb = float(model.loss(x, y))
-                model.enable_fp8(margin=margin)
+                lb = float(model.loss(x, y).detach())
+                model.enable_fp8(margin=margin, wgrad=True if train else None)
                 for jt in range(max(0, it - 16), it):
-                    model.loss(*data[jt])
+                    model.loss(*data[jt]).detach()
                     for st in model.fp8_states():
                         st.update()
-                l8 = float(model.loss(x, y))
+                l8 = float(model.loss(x, y).detach())
                 for layer in model.layers:
                     layer.fp8 = None
                 model.fp8_state = model.fp8_grad_state = None
@@ -341,12 +346,27 @@ def _same_weights_losses(c: Shape, steps, gpu_device, margin: float = 1.0) -> di
     return out
 
 
-def test_fp8_forward_matches_bf16_on_same_weights(gpu_device):
-    """Per-step bound on the fp8 forward itself: at the steps where the fp8 run's loss departs most from the bf16
-    run's (18, 25, 73: up to 27 %, benchmarks/fp8_spike_probe.py), the fp8 forward on the bf16 run's own weights is
-    within 1 % of the bf16 forward.  The transient gaps of test_fp8_engine_tracks_bf16_engine are therefore the two
-    trajectories' weights, not the rounding of one fp8 step (profiles/parity/fp8_spike_probe_r5.json)."""
-    res = _same_weights_losses(SHAPES["llama"], [18, 25, 73], gpu_device)
+def test_fp8_forward_matches_bf16_on_same_weights(gpu_device, monkeypatch):
+    """Per-step bound on the fp8 TRAINING forward itself: at the steps where the fp8 run's loss departs most from the
+    bf16 run's (18, 25, 73: up to 27 %, benchmarks/fp8_spike_probe.py), the fp8 forward on the bf16 run's own weights
+    -- evaluated with gradients enabled, so through the kernels a training step runs (the fused norm + e4m3 casts
+    and the gate + e4m3 cast, counted here) -- is within 1 % of the bf16 forward.  The transient gaps of
+    test_fp8_engine_tracks_bf16_engine are therefore the two trajectories' weights, not the rounding of one fp8
+    step (profiles/parity/fp8_spike_probe_r5.json)."""
+    from bpe_transformer.models import fused_block as fb
+
+    ran = {"norm8": 0, "swiglu_cast": 0}
+
+    def counted(name, fn):
+        def f(*a, **k):
+            ran[name] += 1
+            return fn(*a, **k)
+        return f
+
+    monkeypatch.setattr(fb, "add_rmsnorm_cast_t", counted("norm8", fb.add_rmsnorm_cast_t))
+    monkeypatch.setattr(fb, "swiglu_fwd_cast_t", counted("swiglu_cast", fb.swiglu_fwd_cast_t))
+    res = _same_weights_losses(SHAPES["llama"], [18, 25, 73], gpu_device, train=True)
     _log("parity_llamashape_L2_fp8_same_weights.json", {str(k): {"bf16": v[0], "fp8": v[1]} for k, v in res.items()})
+    assert ran["norm8"] > 0 and ran["swiglu_cast"] > 0, ran
     for it, (lb, l8) in res.items():
         assert math.isfinite(l8) and abs(l8 - lb) / lb < 0.01, (it, lb, l8)
