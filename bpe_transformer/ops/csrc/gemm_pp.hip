@@ -493,6 +493,54 @@ enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2, EPI_ROPE = 3 };
 #ifndef BPE_GPP_PK
 #define BPE_GPP_PK 1
 #endif
+// SwiGLU-backward epilogue timing diagnostics (variant builds only, numerically wrong): bit 0 = no g / u loads,
+// bit 1 = no dg / du stores
+#ifndef BPE_GPP_EPIDIAG
+#define BPE_GPP_EPIDIAG 0
+#endif
+#ifndef BPE_GPP_DESYNC
+#define BPE_GPP_DESYNC 0
+#endif
+// Store policy of the fused epilogues' outputs (MI355X_MICROARCH store flavours): 0 = plain (the line stays in
+// the XCD's L2), 1 = sc1 (written through and dropped from L2), 2 = nt.  The outputs are 0.6-1.1 GB streams read
+// by later kernels only; kept in L2 they evict the main loop's operand tiles.  Per output, measured per call at
+// GPT-2 B 128 (profiles/bench/ab_epilogue_store_policy_r6.log):
+#ifndef BPE_GPP_SWB_ONETILE  // the SwiGLU-backward GEMM on the one-tile kernel even in persistent mode
+#define BPE_GPP_SWB_ONETILE 0
+#endif
+#ifndef BPE_GPP_POL_SWB  // SwiGLU backward dg / du (sc1: 0.67 vs 0.70-0.71 ms per GPT-2 call)
+#define BPE_GPP_POL_SWB 1
+#endif
+#ifndef BPE_GPP_POL_SWF_GU  // SwiGLU forward gu (nt; sc1 on gu and a: 0.85 vs 0.82 ms)
+#define BPE_GPP_POL_SWF_GU 2
+#endif
+#ifndef BPE_GPP_POL_SWF_A  // SwiGLU forward a
+#define BPE_GPP_POL_SWF_A 0
+#endif
+#ifndef BPE_GPP_POL_ROPE  // QKV + RoPE output (sc1: 0.426-0.428 vs 0.433-0.434 ms)
+#define BPE_GPP_POL_ROPE 1
+#endif
+
+// 16-byte store of v at byte offset off from the wave-uniform base (a buffer resource for the cache-policy forms:
+// built from uniform values, so it lives in SGPRs -- no waterfall)
+template <int POL>
+__device__ __forceinline__ void st16(__bf16* base, unsigned off, const u16x8& v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (POL == 0) {
+        *reinterpret_cast<u16x8*>(reinterpret_cast<char*>(base) + off) = v;
+    } else {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, off, 0, POL == 1 ? 16 : 2);
+    }
+#endif
+}
+#ifndef BPE_GPP_DESYNC_CYC
+#define BPE_GPP_DESYNC_CYC 20000
+#endif
+#ifndef BPE_GPP_DESYNC_ALL
+#define BPE_GPP_DESYNC_ALL 0
+#endif
 struct Epi {
     const __bf16* gu;
     __bf16* dgu;  // EPI_SWIGLU_BWD: dgu out; EPI_SWIGLU_FWD: gu out
@@ -545,6 +593,11 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const long ro = (long)(i0 + r0 + q * 16 + (tid >> 5)) * ep.ld + j0 + c * 8;
+                if (BPE_GPP_EPIDIAG & 1) {  // timing diagnostic: no g / u loads (numerically wrong)
+                    gv[q] = u16x8{(unsigned short)ro, 1, 2, 3, 4, 5, 6, 7};
+                    uv[q] = u16x8{(unsigned short)(ro >> 16), 1, 2, 3, 4, 5, 6, 7};
+                    continue;
+                }
                 gv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro));  // read once
                 uv[q] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F));
             }
@@ -581,9 +634,12 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
                     dg[e] = f2bf(d * uu * sg * (1.f + gg * (1.f - sg)));
                 }
 #endif
-                if (st_on) {
-                    *reinterpret_cast<u16x8*>(ep.dgu + ro) = dg;
-                    *reinterpret_cast<u16x8*>(ep.dgu + ro + ep.F) = du;
+                if (st_on && (!(BPE_GPP_EPIDIAG & 2) || ep.prio == 77)) {  // EPIDIAG 2: no stores (timing)
+                    // offsets from the tile's first output element (wave-uniform base)
+                    __bf16* tb = ep.dgu + (long)(i0 + r0) * ep.ld + j0;
+                    const unsigned o = (unsigned)(((long)i * ep.ld + c * 8) * 2);
+                    st16<BPE_GPP_POL_SWB>(tb, o, dg);
+                    st16<BPE_GPP_POL_SWB>(tb, o + (unsigned)ep.F * 2, du);
                 }
             }
         } else if constexpr (EPI == EPI_SWIGLU_FWD) {
@@ -616,9 +672,12 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
                 const long r = i0 + r0 + i;
                 // gu is next read by the backward, long after this step's forward: streaming stores
                 if (st_on) {
-                    st_stream(reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + jb + c * 8), gv);
-                    st_stream(reinterpret_cast<u16x8*>(ep.dgu + r * ep.ld + ep.F + jb + c * 8), uv);
-                    *reinterpret_cast<u16x8*>(ep.act + r * ep.ld_act + jb + c * 8) = av;
+                    __bf16* tg = ep.dgu + (long)(i0 + r0) * ep.ld + jb;
+                    const unsigned og = (unsigned)(((long)i * ep.ld + c * 8) * 2);
+                    st16<BPE_GPP_POL_SWF_GU>(tg, og, gv);
+                    st16<BPE_GPP_POL_SWF_GU>(tg, og + (unsigned)ep.F * 2, uv);
+                    st16<BPE_GPP_POL_SWF_A>(ep.act + (long)(i0 + r0) * ep.ld_act + jb,
+                                            (unsigned)(((long)i * ep.ld_act + c * 8) * 2), av);
                 }
             }
         } else if constexpr (EPI == EPI_ROPE) {
@@ -653,7 +712,7 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
                         v[2 * j + 1] = f2bf(a * sn[q][j] + b * cs[q][j]);
                     }
                 }
-                if (st_on) *reinterpret_cast<u16x8*>(C + (long)(i0 + r0 + i) * ldc + col) = v;
+                if (st_on) st16<BPE_GPP_POL_ROPE>(C + (long)(i0 + r0) * ldc + j0, (unsigned)(((long)i * ldc + c * 8) * 2), v);
             }
         } else {
             __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -678,6 +737,7 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
         }
     }
 }
+
 
 template <bool AK, bool BKM, bool SLAB, int DIAG, int EPI = EPI_NONE, int SPREAD = 0, int F8 = 0>
 __global__ void __launch_bounds__(NT, 1)
@@ -868,6 +928,16 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
     };
     int t = wid, i0, j0, jb;
     origin(t, i0, j0, jb);
+#if BPE_GPP_DESYNC > 1
+    // desynchronised start (variant builds): the workgroups of an XCD fall into BPE_GPP_DESYNC groups that start
+    // BPE_GPP_DESYNC_CYC shader cycles apart, so that the tiles' epilogue bursts (HBM-bound when every CU stores at
+    // once) interleave with other CUs' main loops for the rest of the launch
+    if (EPI == EPI_SWIGLU_BWD || BPE_GPP_DESYNC_ALL) {
+        const long long t0 = __builtin_amdgcn_s_memtime();
+        const long long wait = (long long)((orig >> 3) % BPE_GPP_DESYNC) * BPE_GPP_DESYNC_CYC;
+        while (__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(8);
+    }
+#endif
     {  // prologue of the first tile: all of its K-tile 0, retired before the first read
         const __bf16* a0 = tile_ptr<AK>(A, lda, i0, 0);
         const __bf16* b0 = tile_ptr<BKM>(B, ldb, jb, 0);
@@ -919,6 +989,10 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
         // the next tile's K-tile 0 (stage st) retired; the stage just read (st ^ 1) is free for the staging
         __builtin_amdgcn_s_waitcnt(0x70);
         bar();
+        // (Measured and dropped, round 6: the SwiGLU-backward epilogue straight from the accumulators -- no LDS
+        // staging, lane pairs swapping halves into 16-byte chunks, every g / u load issued before the first store
+        // -- 0.77 vs 0.69 ms, profiles/bench/ab_swiglu_bwd_reg_epilogue_r6.log: each access instruction then covers
+        // 16 rows x 2 x 32 B instead of 2 rows x 512 B.)
         epilogue_bf16<EPI, F8, 2>(acc, smem + (st ^ 1) * STAGE, g, wl, l, tid, i0, j0, jb, C, ldc, beta, ep, true,
                                   more, t);
         GPP_STAMP_T(t, 4);
@@ -1158,7 +1232,7 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
     const int grid = (M / BT) * (F / BT);
     Epi ep{(const __bf16*)gu, (__bf16*)dgu, ldg, F};
     ep.prio = prio_mode();
-    if (g_persist) {
+    if (g_persist && !BPE_GPP_SWB_ONETILE) {
         static bool pattr = false;
         auto* kp = &gemm_pp_persist_kernel<true, false, EPI_SWIGLU_BWD, 1>;
         if (!pattr) lds_attr(kp), pattr = true;
