@@ -57,7 +57,8 @@ void launch_softmax_bwd(int dtype, const void* dy, const void* y, void* dx, int 
 void launch_cast_fp8(int dtype, int fmt, const void* x, size_t n, const float* scale, void* out,
                      unsigned* amax_bits, hipStream_t s);  // fmt 0 = e4m3fn, 1 = e5m2
 // dst[C, R] = src[R, C]^T, bf16, R and C multiples of 64 (16-byte aligned rows)
-void launch_transpose_bf16(const void* src, long ld_src, void* dst, long ld_dst, int R, int C, hipStream_t s);
+void launch_transpose_bf16(const void* src, long ld_src, void* dst, long ld_dst, int R, int C, hipStream_t s,
+                           const float* scale = nullptr);
 void launch_cast_fp8_t(const void* w, int N, int K, const float* scale, void* w8, void* w8t, unsigned* amax_bits,
                        int fmt, hipStream_t s);
 // SwiGLU + two-layout fp8 cast (fp8.hip): mode 0 a = silu(g) u -> a8 [M][F], a8t [F][M] (e4m3); mode 1 the gate

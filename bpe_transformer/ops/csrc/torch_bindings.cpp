@@ -632,16 +632,23 @@ void cast_fp8(const at::Tensor& x, const at::Tensor& scale, at::Tensor out, at::
                     reinterpret_cast<unsigned*>(amax_bits.data_ptr<int>()), cur_stream());
 }
 
-// W [R][C] bf16 (row stride a multiple of 8) -> W^T [C][R] contiguous
-at::Tensor transpose_bf16(const at::Tensor& w) {
+// W [R][C] bf16 (row stride a multiple of 8) -> W^T [C][R] contiguous; scale (optional 0-dim / one-element fp32 device
+// tensor): bf16(scale * W)^T
+at::Tensor transpose_bf16(const at::Tensor& w, const std::optional<at::Tensor>& scale) {
     check_cuda(w, "w");
     TORCH_CHECK(w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.stride(1) == 1 && w.stride(0) % 8 == 0,
                 "transpose_bf16: bf16 [R, C] with unit column stride and 16-byte row alignment required");
     const int64_t R = w.size(0), C = w.size(1);
     TORCH_CHECK(R % 64 == 0 && C % 64 == 0, "transpose_bf16: R and C must be multiples of 64");
     DevGuard g(w.device());
+    const float* sp = nullptr;
+    if (scale.has_value() && scale->defined()) {
+        TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1 && scale->device() == w.device(),
+                    "transpose_bf16: scale must be a one-element fp32 tensor on w's device");
+        sp = scale->data_ptr<float>();
+    }
     auto out = at::empty({C, R}, w.options());
-    launch_transpose_bf16(w.data_ptr(), w.stride(0), out.data_ptr(), R, (int)R, (int)C, cur_stream());
+    launch_transpose_bf16(w.data_ptr(), w.stride(0), out.data_ptr(), R, (int)R, (int)C, cur_stream(), sp);
     return out;
 }
 
@@ -1124,7 +1131,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gemm_pp_dw_group(Tensor(a!)[] gs, Tensor[] dys, Tensor[] xs, bool x_kmajor, int splits, float beta=1.0) -> ()");
     m.def("gemm(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits, int tile=128) -> ()");
     m.def("cast_fp8(Tensor x, Tensor scale, Tensor(a!) out, Tensor(b!) amax_bits) -> ()");
-    m.def("transpose_bf16(Tensor w) -> Tensor");
+    m.def("transpose_bf16(Tensor w, Tensor? scale=None) -> Tensor");
     m.def("cast_fp8_t(Tensor w, Tensor scale, Tensor(a!) w8, Tensor(b!) w8t, Tensor(c!) amax_bits) -> ()");
     m.def("swiglu_cast_fp8_t(Tensor gu, Tensor? dout, Tensor scale, Tensor(a!) o8, Tensor(b!) o8t, "
           "Tensor(c!) amax_bits) -> ()");

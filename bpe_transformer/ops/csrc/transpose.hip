@@ -13,16 +13,27 @@ namespace bpe {
 
 // one 64 x 64 tile per 256-thread workgroup; thread t reads 16 elements of row t / 4 and writes 16 elements of
 // output row t / 4 (= tile column t / 4)
+// scale (optional, device fp32 scalar): dst = bf16(scale * src)^T -- the LM head's backward folds the loss
+// gradient into the transposed operand copies it makes anyway, instead of two elementwise passes over [T, d]
 __global__ void __launch_bounds__(256) transpose_bf16_kernel(const __bf16* __restrict__ src, long ld_src,
-                                                             __bf16* __restrict__ dst, long ld_dst, int R, int C) {
+                                                             __bf16* __restrict__ dst, long ld_dst, int R, int C,
+                                                             const float* __restrict__ scale) {
     __shared__ u16 tile[64][64 + 2];  // +2: the column reads of one wave spread over the banks
     const int tid = threadIdx.x;
     const int tiles_c = C / 64;
     const int r0 = (blockIdx.x / tiles_c) * 64, c0 = (blockIdx.x % tiles_c) * 64;
     const int r = tid >> 2, c = (tid & 3) * 16;
     const __bf16* sp = src + (long)(r0 + r) * ld_src + c0 + c;
-    const u16x8 a = *reinterpret_cast<const u16x8*>(sp);
-    const u16x8 b = *reinterpret_cast<const u16x8*>(sp + 8);
+    u16x8 a = *reinterpret_cast<const u16x8*>(sp);
+    u16x8 b = *reinterpret_cast<const u16x8*>(sp + 8);
+    if (scale != nullptr) {
+        const float sc = *scale;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            a[j] = f2bf(bf2f(a[j]) * sc);
+            b[j] = f2bf(bf2f(b[j]) * sc);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         tile[r][c + j] = a[j];
@@ -44,7 +55,8 @@ __global__ void __launch_bounds__(256) transpose_bf16_kernel(const __bf16* __res
 
 using namespace bpe;
 
-void launch_transpose_bf16(const void* src, long ld_src, void* dst, long ld_dst, int R, int C, hipStream_t s) {
+void launch_transpose_bf16(const void* src, long ld_src, void* dst, long ld_dst, int R, int C, hipStream_t s,
+                           const float* scale) {
     transpose_bf16_kernel<<<(R / 64) * (C / 64), 256, 0, s>>>((const __bf16*)src, ld_src, (__bf16*)dst, ld_dst, R,
-                                                              C);
+                                                              C, scale);
 }

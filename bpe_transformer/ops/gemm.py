@@ -147,9 +147,15 @@ def _blas_acc(g: Tensor, dy: Tensor, x: Tensor) -> None:
         g.addmm_(dy.t().to(g.dtype), x.to(g.dtype))
 
 
-def _run(route: str, g: Tensor, dy: Tensor, x: Tensor) -> None:
+def _run(route: str, g: Tensor, dy: Tensor, x: Tensor, x_scale: Tensor | None = None) -> None:
     n, k = g.shape
     t = dy.shape[0]
+    if x_scale is not None:
+        if route == "ppt":  # the scale rides on the X^T copy the route makes anyway
+            xt = ops().transpose_bf16(x, x_scale.detach().float().reshape(1).contiguous())
+            ops().gemm_pp(dy, False, xt, True, g, 1.0, choose_splits_pp(n, k, t))
+            return
+        x = x * x_scale.to(x.dtype)
     if route == "pp":
         ops().gemm_pp(dy, False, x, False, g, 1.0, choose_splits_pp(n, k, t))
     elif route == "ppt":
@@ -212,9 +218,11 @@ def routes_summary() -> dict[str, str]:
     return {",".join(str(v) for v in k): r for k, r in sorted(_route.items())}
 
 
-def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
-    """``g += dy.T @ x`` (bf16 operands, fp32 accumulation; ``g`` bf16 or fp32 -- an fp32 gradient buffer gets the
-    fp32 sum, through the kernels' fp32 partial slab and ordered reduce).
+def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor, x_scale: Tensor | None = None) -> None:
+    """``g += dy.T @ (x_scale * x)`` (bf16 operands, fp32 accumulation; ``g`` bf16 or fp32 -- an fp32 gradient
+    buffer gets the fp32 sum, through the kernels' fp32 partial slab and ordered reduce).  ``x_scale``: optional
+    device scalar (the LM head's upstream loss gradient), folded into the X^T copy of the ``ppt`` route, else
+    applied to x first.
 
     Routes per shape (module docstring): the shape's entry in ``tuning/dw_routes.json``, else the first call for a
     shape times the candidates (``BPE_GEMM_AUTOTUNE=0``: take the first HIP candidate).  Measured
@@ -226,7 +234,7 @@ def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
     ok = (g.is_cuda and g.dtype in (torch.bfloat16, torch.float32) and dy.dtype == torch.bfloat16
           and x.dtype == torch.bfloat16 and g.stride(1) == 1 and dy.stride(1) == 1 and x.stride(1) == 1)
     if not ok:
-        _blas_acc(g, dy, x)
+        _blas_acc(g, dy, x if x_scale is None else x * x_scale.to(x.dtype))
         return
     key = (n, k, t) if g.dtype == torch.bfloat16 else (n, k, t, 32)
     route = _route.get(key)
@@ -237,7 +245,7 @@ def accumulate_weight_grad(g: Tensor, dy: Tensor, x: Tensor) -> None:
         key3 = (n, k, t)
         fixed = _static_route.get(key3)
         route = _route[key] = fixed if fixed in cands else _tune(key3, cands, g, dy, x)
-    _run(route, g, dy, x)
+    _run(route, g, dy, x, x_scale)
 
 
 def matmul_nt(a: Tensor, b: Tensor, out: Tensor | None = None, beta: float = 0.0) -> Tensor:
@@ -254,7 +262,7 @@ def matmul_nt(a: Tensor, b: Tensor, out: Tensor | None = None, beta: float = 0.0
 # ---------------------------------------------------------------------------------------------------------------
 # Grouped weight gradients (one split-K launch for the dW GEMMs of a layer that become ready together)
 
-_GROUP = os.environ.get("BPE_DW_GROUP", "1") == "1"  # module flag (A/B runs and tests compare the per-shape routes)
+_GROUP = os.environ.get("BPE_DW_GROUP", "0") == "1"  # opt-in: measured neutral at GPT-2, -2.2 % at Llama (profiles/bench/ab_dw_group_r6.log)
 _group_used: dict[tuple, int] = {}
 
 

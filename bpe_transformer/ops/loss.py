@@ -57,14 +57,17 @@ STREAMED_DEFAULT_CHUNK = 16384
 _HEAD_DX_TN = True  # module flag (tests compare the NN call)
 
 
-def _head_dx(dlogits: Tensor, w: Tensor) -> Tensor:
-    """dh = dlogits @ W in hipBLASLt's TN layout through a transposed copy of W (``ops.transpose_bf16``, as the
-    blocks' input gradients do: models/fused_block.py ``_dx_tn``): 7.24 vs 8.27 ms at GPT-2 B 128 with tuned
-    solutions (profiles/bench/head_dx_layouts_b128.log), +0.65 % end to end."""
+def _head_dx(dlogits: Tensor, w: Tensor, scale: Tensor | None = None) -> Tensor:
+    """dh = dlogits @ (scale * W) in hipBLASLt's TN layout through a transposed copy of W (``ops.transpose_bf16``,
+    as the blocks' input gradients do: models/fused_block.py ``_dx_tn``): 7.24 vs 8.27 ms at GPT-2 B 128 with tuned
+    solutions (profiles/bench/head_dx_layouts_b128.log), +0.65 % end to end.  ``scale`` (the loss's upstream
+    gradient, a device scalar) is applied inside that copy -- no elementwise pass over dh."""
     if (_HEAD_DX_TN and w.dtype == torch.bfloat16 and dlogits.is_cuda and w.stride(1) == 1
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0):
-        return torch.matmul(dlogits, ops().transpose_bf16(w).t())
-    return torch.matmul(dlogits, w)
+        sc = None if scale is None else scale.detach().float().reshape(1).contiguous()
+        return torch.matmul(dlogits, ops().transpose_bf16(w, sc).t())
+    dh = torch.matmul(dlogits, w)
+    return dh if scale is None else dh * scale.to(dh.dtype)
 
 
 class _LMHeadCEFn(torch.autograd.Function):
@@ -103,22 +106,23 @@ class _LMHeadCEFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g: Tensor):
         h, w, dlogits = ctx.saved_tensors
-        gg = g.to(h.dtype)
-        dh = _head_dx(dlogits, w) * gg  # the upstream scale goes on the small operands, never on the logits
-        hs = h * gg
+        # the upstream scale goes on the small operands, never on the logits -- and where the GEMMs read transposed
+        # copies of them anyway (W^T for dh, h^T for dW's "ppt" route) it is applied inside those copies, so no
+        # elementwise pass over the [T, d] tensors runs (two ~75 us kernels per GPT-2 B 128 step before)
+        dh = _head_dx(dlogits, w, g)
         mg = getattr(ctx.w_param, "_bpe_padded_grad" if ctx.padded else "main_grad", None)
         if ctx.padded and mg is None:
-            return dh, torch.matmul(dlogits.t(), hs)[: ctx.w_param.shape[0]], None, None, None
+            return dh, torch.matmul(dlogits.t(), h * g.to(h.dtype))[: ctx.w_param.shape[0]], None, None, None
         if mg is not None:
             # weight gradient accumulated in place into the flat gradient buffer (no temporary, no grad add)
             from .gemm import accumulate_weight_grad
 
-            accumulate_weight_grad(mg, dlogits, hs)
+            accumulate_weight_grad(mg, dlogits, h, x_scale=g)
             cb = getattr(ctx.w_param, "_bpe_grad_ready", None)
             if cb is not None:
                 cb(ctx.w_param)
             return dh, None, None, None, None
-        return dh, torch.matmul(dlogits.t(), hs), None, None, None
+        return dh, torch.matmul(dlogits.t(), h * g.to(h.dtype)), None, None, None
 
 
 class _LMHeadCEStreamedFn(torch.autograd.Function):

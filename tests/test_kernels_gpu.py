@@ -247,6 +247,36 @@ def test_lm_head_ce_no_grad_is_loss_only(gpu_device, mode):
     assert peak < 1024 * V * 2 * 1.5, peak  # one chunk buffer (+ small temporaries), never M x V
 
 
+def test_transpose_bf16_scaled(gpu_device):
+    """The transposed copy with a device scale (the LM head's upstream gradient folded in): bf16(scale * W)^T
+    bitwise, and plain W^T without it."""
+    torch.manual_seed(8)
+    w = torch.randn(192, 320, device=gpu_device, dtype=torch.bfloat16)
+    sc = torch.tensor([0.37], device=gpu_device)
+    h = torch.ops.bpe_hip
+    assert torch.equal(h.transpose_bf16(w), w.t().contiguous())
+    assert torch.equal(h.transpose_bf16(w, sc), (w.float() * 0.37).to(torch.bfloat16).t().contiguous())
+
+
+def test_weight_grad_x_scale_on_the_ppt_route(gpu_device):
+    """accumulate_weight_grad's x_scale on the ppt route (applied in the X^T copy) == the route on a pre-scaled X,
+    bitwise; and the other routes scale X first."""
+    from bpe_transformer.ops.gemm import _run
+
+    torch.manual_seed(9)
+    n, k, t = 512, 256, 2048
+    dy = torch.randn(t, n, device=gpu_device, dtype=torch.bfloat16)
+    x = torch.randn(t, k, device=gpu_device, dtype=torch.bfloat16)
+    sc = torch.tensor(0.5, device=gpu_device)  # the autograd scalar as the LM head sees it (0-dim)
+    xs = (x.float() * 0.5).to(torch.bfloat16)
+    for route in ("ppt", "pp", "blas"):
+        g1 = torch.zeros(n, k, device=gpu_device, dtype=torch.bfloat16)
+        g2 = torch.zeros_like(g1)
+        _run(route, g1, dy, x, sc)
+        _run(route, g2, dy, xs)
+        assert torch.equal(g1, g2), route
+
+
 def test_lm_head_dx_tn_matches_nn(gpu_device, monkeypatch):
     """The LM-head input gradient through the transposed weight copy (hipBLASLt TN layout, the default) equals
     the NN call on the stored weight up to GEMM rounding, and both match the fp32 oracle."""
@@ -614,12 +644,14 @@ def test_gemm_pp_dw_group_exact(gpu_device, x_k, dtype, splits):
         assert torch.equal(g.float().cpu(), ref.cpu())
 
 
-def test_gemm_pp_dw_group_bitwise_vs_single(gpu_device):
+def test_gemm_pp_dw_group_bitwise_vs_single(gpu_device, monkeypatch):
     """Random operands at GPT-2-like dW shapes (more workgroups than CUs): the grouped launch runs each tile's
     split exactly as the single-problem split-K kernel does and reduces in the same split order, so every
     gradient matches the per-shape ``gemm_pp`` route bitwise; repeated launches are bitwise stable."""
+    from bpe_transformer.ops import gemm
     from bpe_transformer.ops.gemm import accumulate_weight_grads, choose_splits_group
 
+    monkeypatch.setattr(gemm, "_GROUP", True)  # the grouped launch is opt-in (BPE_DW_GROUP=1)
     torch.manual_seed(4)
     T = 16384
     shapes = [(768, 2048), (4096, 768)]  # W2 and [W1; W3] of GPT-2-small: 24 + 48 tiles

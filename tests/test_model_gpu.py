@@ -89,6 +89,32 @@ def test_main_grad_path_matches_autograd(gpu_device):
         assert e < 1e-2, (n, float(e))
 
 
+def test_grouped_dw_path_matches_per_shape_routes(gpu_device, monkeypatch):
+    """The opt-in grouped weight-gradient launch (BPE_DW_GROUP=1: W2 + [W1; W3] and Wo + [Wq; Wk; Wv] dW in one
+    split-K launch each, Wo's dW deferred past the attention backward) accumulates the same flat-buffer gradients as
+    the per-shape routes, up to bf16 rounding of split-K partial sums in a different split count."""
+    from bpe_transformer.ops import gemm
+    from bpe_transformer.optim.flat import FlatParameters
+
+    _, a = _pair(gpu_device)
+    b = copy.deepcopy(a)
+    ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    grads = []
+    for model, group in ((a, True), (b, False)):
+        monkeypatch.setattr(gemm, "_GROUP", group)
+        flat = FlatParameters.from_module(model)
+        for s in flat.slots:
+            s.param.main_grad = flat.grad_view(s).view_as(s.param)
+        model.loss(ids, tgt).backward()
+        grads.append([flat.grad_view(s).float().clone() for s in flat.slots])
+    assert gemm.groups_summary(), "the grouped launch did not run"
+    for ga, gb in zip(*grads):
+        assert torch.isfinite(ga).all()
+        e = (ga - gb).norm() / gb.norm().clamp_min(1e-12)
+        assert e < 1e-2, float(e)
+
+
 def test_train_engine_reduces_loss(gpu_device):
     from bpe_transformer.train.engine import TrainEngine
 
