@@ -113,6 +113,35 @@ __device__ __forceinline__ int src_off_sub(int e, int ld) {
     return row * ld + 32 * s + 8 * ql;
 }
 
+// A64 (build define, default on): the MN-major A operand of the spread schedule (the weight gradient's dY) in four
+// [64 k][64 col] sub-images of 8 KiB with 128-byte rows instead of eight [64 k][32 col] ones: a 1-KiB DMA piece is
+// then 8 whole 128-byte lines of 8 token rows instead of 16 half lines of 16 rows (the A pieces the schedule issues
+// are whole 64-column blocks either way, so the schedule is unchanged; B keeps the 32-column halves it needs).  The
+// 32-byte segment of a row is swizzled by a64_f(row), which keeps the ds_read_b64_tr_b16 fragment reads
+// conflict-free (each 32-lane group reads rows {r0..r0+3, r0+8..r0+11} x one 32-byte segment: 8 distinct bank
+// groups; checked exhaustively on the host when the layout was written).
+#ifndef BPE_GPP_A64
+#define BPE_GPP_A64 1
+#endif
+__device__ __forceinline__ int a64_f(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
+__device__ __forceinline__ int sub64_off(int r, int c) {  // byte offset of (k-row r, column c) in the A64 image
+    const int cc = c & 63;
+    return (c >> 6) * 8192 + r * 128 + (((cc >> 4) ^ a64_f(r)) << 5) + ((cc & 15) << 1);
+}
+// source offset (elements from the tile origin) of 16-byte image chunk e (0..2047) of the A64 image: sub-image
+// e >> 9, piece (8 k-rows) (e >> 6) & 7, lane e & 63 -> k-row 8 piece + lane / 8, physical chunk lane & 7
+__device__ __forceinline__ int src_off_sub64(int e, int ld) {
+    const int s = e >> 9, q = (e >> 6) & 7, ln = e & 63;
+    const int row = 8 * q + (ln >> 3), ch = ln & 7;
+    const int lc = (((ch >> 1) ^ a64_f(row)) << 1) | (ch & 1);
+    return row * ld + 64 * s + 8 * lc;
+}
+__device__ __forceinline__ bf16x8 frag_a64(char* img, int tb, int ks, int l) {
+    const int r = 32 * ks + 8 * (l >> 4) + ((l & 15) >> 2);
+    const int c = tb * 16 + 4 * (l & 3);
+    return fa::lds_tr_pair(img, sub64_off(r, c), sub64_off(r + 4, c));
+}
+
 // MFMA operand fragment of 16-row/col block tb, k-step ks: lane l gets X[t = 16 tb + (l & 15)][k = 32 ks + 8 (l >> 4) + j].
 // SUB: MN-major operands use the sub-image layout above (spread schedule) instead of [64][256] 512-byte rows.
 template <bool KM, bool SUB = false>
@@ -201,7 +230,10 @@ __device__ __forceinline__ void load_a(Frags& f, char* img, int g, int m, int l)
 #pragma unroll
     for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) f.a[ib][ks] = frag<AK, SUB>(img, 8 * g + 4 * m + ib, ks, l);
+        for (int ks = 0; ks < 2; ++ks) {
+            if constexpr (!AK && SUB && BPE_GPP_A64) f.a[ib][ks] = frag_a64(img, 8 * g + 4 * m + ib, ks, l);
+            else f.a[ib][ks] = frag<AK, SUB>(img, 8 * g + 4 * m + ib, ks, l);
+        }
 }
 template <bool AK, bool BKM, bool SUB = false>
 __device__ __forceinline__ void load_b(Frags& f, char* img, int wl, int n, int l) {
@@ -359,8 +391,13 @@ __device__ __forceinline__ SpreadOff spread_offsets(int g, int wl, int l, int ld
     o.lb1 = o.lb0 + 256;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        o.a0[j] = spread_src<AK>(o.la0 + 64 * j + l, lda);
-        o.a1[j] = spread_src<AK>(o.la1 + 64 * j + l, lda);
+        if constexpr (!AK && BPE_GPP_A64) {
+            o.a0[j] = src_off_sub64(o.la0 + 64 * j + l, lda);
+            o.a1[j] = src_off_sub64(o.la1 + 64 * j + l, lda);
+        } else {
+            o.a0[j] = spread_src<AK>(o.la0 + 64 * j + l, lda);
+            o.a1[j] = spread_src<AK>(o.la1 + 64 * j + l, lda);
+        }
         o.b0[j] = spread_src<BKM>(o.lb0 + 64 * j + l, ldb);
         o.b1[j] = spread_src<BKM>(o.lb1 + 64 * j + l, ldb);
     }
