@@ -535,16 +535,10 @@ enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2, EPI_ROPE = 3 };
 #ifndef BPE_GPP_EPIDIAG
 #define BPE_GPP_EPIDIAG 0
 #endif
-#ifndef BPE_GPP_DESYNC
-#define BPE_GPP_DESYNC 0
-#endif
 // Store policy of the fused epilogues' outputs (MI355X_MICROARCH store flavours): 0 = plain (the line stays in
 // the XCD's L2), 1 = sc1 (written through and dropped from L2), 2 = nt.  The outputs are 0.6-1.1 GB streams read
 // by later kernels only; kept in L2 they evict the main loop's operand tiles.  Per output, measured per call at
 // GPT-2 B 128 (profiles/bench/ab_epilogue_store_policy_r6.log):
-#ifndef BPE_GPP_SWB_ONETILE  // the SwiGLU-backward GEMM on the one-tile kernel even in persistent mode
-#define BPE_GPP_SWB_ONETILE 0
-#endif
 #ifndef BPE_GPP_POL_SWB  // SwiGLU backward dg / du (sc1: 0.67 vs 0.70-0.71 ms per GPT-2 call)
 #define BPE_GPP_POL_SWB 1
 #endif
@@ -572,12 +566,6 @@ __device__ __forceinline__ void st16(__bf16* base, unsigned off, const u16x8& v)
     }
 #endif
 }
-#ifndef BPE_GPP_DESYNC_CYC
-#define BPE_GPP_DESYNC_CYC 20000
-#endif
-#ifndef BPE_GPP_DESYNC_ALL
-#define BPE_GPP_DESYNC_ALL 0
-#endif
 struct Epi {
     const __bf16* gu;
     __bf16* dgu;  // EPI_SWIGLU_BWD: dgu out; EPI_SWIGLU_FWD: gu out
@@ -965,16 +953,6 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
     };
     int t = wid, i0, j0, jb;
     origin(t, i0, j0, jb);
-#if BPE_GPP_DESYNC > 1
-    // desynchronised start (variant builds): the workgroups of an XCD fall into BPE_GPP_DESYNC groups that start
-    // BPE_GPP_DESYNC_CYC shader cycles apart, so that the tiles' epilogue bursts (HBM-bound when every CU stores at
-    // once) interleave with other CUs' main loops for the rest of the launch
-    if (EPI == EPI_SWIGLU_BWD || BPE_GPP_DESYNC_ALL) {
-        const long long t0 = __builtin_amdgcn_s_memtime();
-        const long long wait = (long long)((orig >> 3) % BPE_GPP_DESYNC) * BPE_GPP_DESYNC_CYC;
-        while (__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(8);
-    }
-#endif
     {  // prologue of the first tile: all of its K-tile 0, retired before the first read
         const __bf16* a0 = tile_ptr<AK>(A, lda, i0, 0);
         const __bf16* b0 = tile_ptr<BKM>(B, ldb, jb, 0);
@@ -1269,7 +1247,7 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
     const int grid = (M / BT) * (F / BT);
     Epi ep{(const __bf16*)gu, (__bf16*)dgu, ldg, F};
     ep.prio = prio_mode();
-    if (g_persist && !BPE_GPP_SWB_ONETILE) {
+    if (g_persist) {
         static bool pattr = false;
         auto* kp = &gemm_pp_persist_kernel<true, false, EPI_SWIGLU_BWD, 1>;
         if (!pattr) lds_attr(kp), pattr = true;
