@@ -579,7 +579,27 @@ struct Epi {
     const float* cosT = nullptr;  // EPI_ROPE: [S][D / 2] tables, S, head dim, rotated column count
     const float* sinT = nullptr;
     int S = 0, D = 0, rot_cols = 0;
+    int gm = 0;  // tile order (tile_rc): 0 = row-major, gm > 0 = column-major within bands of gm row blocks
 };
+
+// Output tile t -> (row block ti, column block tj).  gm 0: row-major.  gm > 0: the tile grid cut into bands of gm
+// row blocks, column-major inside a band, so the 32 consecutive work ids of one XCD in a round cover 32 / gm
+// columns x gm rows instead of 32 / tiles_n rows x every column: when 256 is a multiple of gm x tiles_n, an XCD
+// then keeps the same B column blocks in every round and its L2 holds them, instead of re-reading all of B (3.5-6.3
+// MiB at GPT-2 K = 768, more than the 4 MiB L2) every round.
+__device__ __forceinline__ void tile_rc(int t, int tiles_m, int tiles_n, int gm, int& ti, int& tj) {
+    if (gm <= 0) {
+        ti = t / tiles_n;
+        tj = t % tiles_n;
+        return;
+    }
+    const int band = t / (gm * tiles_n);
+    const int r0 = band * gm;
+    const int rows = tiles_m - r0 < gm ? tiles_m - r0 : gm;
+    const int wb = t - band * gm * tiles_n;
+    ti = r0 + wb % rows;
+    tj = wb / rows;
+}
 
 // bf16 epilogue: the tile is staged through LDS at stg as [256 / NPASS][512 B] images (16-byte chunk c of row i at
 // c ^ (i & 15)) and written back as whole rows.  NPASS 1: the whole tile at once (128 KiB, the one-tile kernel);
@@ -780,9 +800,11 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     const int tiles_n = N / BT;
     const int ntiles = (M / BT) * tiles_n;
     const int split = wid / ntiles, tile = wid % ntiles;
-    const int i0 = (tile / tiles_n) * BT, j0 = (tile % tiles_n) * BT;
+    int ti, tj;
+    tile_rc(tile, M / BT, tiles_n, ep.gm, ti, tj);
+    const int i0 = ti * BT, j0 = tj * BT;
     // B tile origin: EPI_SWIGLU_FWD tiles 128 g columns (+ the matching u columns, offset F rows in B)
-    const int jb = EPI == EPI_SWIGLU_FWD ? (tile % tiles_n) * (BT / 2) : j0;
+    const int jb = EPI == EPI_SWIGLU_FWD ? tj * (BT / 2) : j0;
     const int nkt = R / BK;
     const int kb = (int)((long)split * nkt / splits);
     const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
@@ -947,9 +969,11 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
     }
     // tile t: output origin (i0, j0) and B origin jb (EPI_SWIGLU_FWD: 128 g columns + the matching u columns)
     auto origin = [&](int t, int& i0, int& j0, int& jb) {
-        i0 = (t / tiles_n) * BT;
-        j0 = (t % tiles_n) * BT;
-        jb = EPI == EPI_SWIGLU_FWD ? (t % tiles_n) * (BT / 2) : j0;
+        int ti, tj;
+        tile_rc(t, M / BT, tiles_n, ep.gm, ti, tj);
+        i0 = ti * BT;
+        j0 = tj * BT;
+        jb = EPI == EPI_SWIGLU_FWD ? tj * (BT / 2) : j0;
     };
     int t = wid, i0, j0, jb;
     origin(t, i0, j0, jb);
@@ -1212,6 +1236,25 @@ int gpp_persist_config(int mode) {
     return prev;
 }
 
+// Tile order of the one-pass GEMMs (Epi::gm, tile_rc): 0 = row-major; n > 0 = column-major within bands of n row
+// blocks; -2 = auto: bands of 2 row blocks up to 10 column tiles, 4 above.  Measured per GEMM at GPT-2 B 128 and
+// Llama s2048 (benchmarks/gemm_tile_order.py, profiles/bench/gemm_tile_order_r6.log): the SwiGLU forward -9 / -10 %,
+// the plain W13 forward -4 / -7 %, the Llama SwiGLU backward -3 %, QKV + RoPE -1.5 % at 9 column tiles with 2 (4
+// is 2 % slower there).  Set at run time for A/B (gpp_order_config, or BPE_GPP_GM in the environment); the split-K
+// weight-gradient launches keep row-major, the fp8 ones too in auto mode (order_fp8).
+static int g_gm = [] {
+    const char* e = getenv("BPE_GPP_GM");
+    return e && *e ? atoi(e) : -2;
+}();
+int gpp_order_config(int gm) {
+    const int prev = g_gm;
+    if (gm >= 0 || gm < -1) g_gm = gm < -1 ? -2 : gm;
+    return prev;
+}
+static int order_for(int tiles_n) { return g_gm >= 0 ? g_gm : (tiles_n <= 10 ? 2 : 4); }
+// the fp8 one-pass GEMMs stay row-major in auto mode: the Llama fp8 s4096 step ran 0.5 % slower with the bf16 rule
+static int order_fp8() { return g_gm >= 0 ? g_gm : 0; }
+
 static int num_cus() {
     static int n[16] = {};
     int dev = 0;
@@ -1247,6 +1290,7 @@ void launch_gemm_pp_swiglu_bwd(const void* dY, long ldy, const void* W2, long ld
     const int grid = (M / BT) * (F / BT);
     Epi ep{(const __bf16*)gu, (__bf16*)dgu, ldg, F};
     ep.prio = prio_mode();
+    ep.gm = order_for(F / BT);
     if (g_persist) {
         static bool pattr = false;
         auto* kp = &gemm_pp_persist_kernel<true, false, EPI_SWIGLU_BWD, 1>;
@@ -1270,6 +1314,7 @@ void launch_gemm_pp_swiglu_fwd(const void* X, long ldx, const void* W13, long ld
     const int grid = (M / BT) * (F / (BT / 2));
     Epi ep{nullptr, (__bf16*)gu, ldg, F, (__bf16*)act, lda_};
     ep.prio = prio_mode();
+    ep.gm = order_for(F / (BT / 2));
     if (g_persist) {
         static bool pattr = false;
         auto* kp = &gemm_pp_persist_kernel<true, true, EPI_SWIGLU_FWD, 1>;
@@ -1286,6 +1331,7 @@ void launch_gemm_pp_rope(const void* X, long ldx, const void* W, long ldw, void*
                          const float* cosT, const float* sinT, int S, int D, int rot_cols, hipStream_t s) {
     Epi ep{};
     ep.prio = prio_mode();
+    ep.gm = order_for(N / BT);
     ep.cosT = cosT;
     ep.sinT = sinT;
     ep.S = S;
@@ -1321,6 +1367,7 @@ void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, 
     }
     Epi ep{};
     ep.prio = prio_mode();
+    ep.gm = order_fp8();
     ep.sa = sa;
     ep.sb = sb;
     // the fp8 rows as bf16 rows of half the length: R = K / 2 "bf16" elements = K / 128 K-tiles of 128 fp8
@@ -1345,6 +1392,7 @@ void launch_gemm_fp8_rope(const void* A, long lda, const void* B, long ldb, void
                           int rot_cols, hipStream_t s) {
     Epi ep{};
     ep.prio = prio_mode();
+    ep.gm = order_fp8();
     ep.sa = sa;
     ep.sb = sb;
     ep.cosT = cosT;
@@ -1403,6 +1451,7 @@ static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, fl
     const int grid = (M / BT) * (N / BT) * splits;
     Epi ep{};
     ep.prio = prio_mode();
+    ep.gm = SLAB ? 0 : order_for(N / BT);
     if constexpr (!SLAB && DIAG == 0 && SPREAD != 0) {
         if (g_persist) {
             static bool pattr = false;

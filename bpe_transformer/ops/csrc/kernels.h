@@ -199,6 +199,8 @@ bool gpp_read_phase_stamps(long long* host, int n);
 // gemm_pp: 1 = persistent kernel for the one-pass bf16 / fp8 GEMMs, 0 = one tile per workgroup; -1 queries.
 // Returns the previous mode.
 int gpp_persist_config(int mode);
+// tile order of the one-pass ping-pong GEMMs: 0 = row-major, n > 0 = column-major in bands of n row blocks; -1 reads
+int gpp_order_config(int gm);
 // C = beta * C + (A8 . B8^T) * sa * sb over `splits` fp32 partials (slab [splits][M][N]); C bf16 or fp32 (c_f32)
 void launch_gemm_fp8_splitk(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                             int fmt_a, const float* sa, const float* sb, float beta, int splits, float* slab,

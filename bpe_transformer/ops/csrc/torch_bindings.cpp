@@ -826,6 +826,7 @@ int64_t fa_fwd_config_op(int64_t ver) { return fa_fwd_config((int)ver); }
 int64_t fa_bwd_config_op(int64_t mode) { return fa_bwd_config((int)mode); }
 int64_t fa_dq_config_op(int64_t form) { return fa_dq_config((int)form); }
 int64_t gpp_persist_config_op(int64_t mode) { return gpp_persist_config((int)mode); }
+int64_t gpp_order_config_op(int64_t gm) { return gpp_order_config((int)gm); }
 // [n, 8] int64 stamps of the last split-backward kernel (a BPE_FA_STAMPS variant build), or an empty tensor
 at::Tensor fa_stamps_op(int64_t n) {
     auto t = at::empty({n, 8}, at::TensorOptions().dtype(at::kLong));
@@ -1156,6 +1157,7 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gpp_stamps(int n) -> Tensor", &gpp_stamps_op);
     m.def("gpp_phase_stamps(int n) -> Tensor", &gpp_phase_stamps_op);
     m.def("gpp_persist_config(int mode=-1) -> int", &gpp_persist_config_op);
+    m.def("gpp_order_config(int gm=-1) -> int", &gpp_order_config_op);
     m.def("fa_fwd_config(int ver=0) -> int", &fa_fwd_config_op);
 }
 

@@ -620,6 +620,41 @@ def test_gemm_pp_persistent_bitwise_many_tiles(gpu_device):
     assert rel(outs[1][0].cpu(), (x.float() @ w.float().t()).cpu()) < 1e-2
 
 
+@pytest.mark.parametrize("persist", [0, 1, 40])
+def test_gemm_pp_tile_order_bitwise(gpu_device, persist):
+    """Column-major tile bands (gpp_order_config gm > 0) only change which workgroup computes a tile: plain, QKV +
+    RoPE, SwiGLU-forward and SwiGLU-backward outputs must equal the row-major ones bitwise, including the ragged
+    last band (33 row blocks) and, at persist = 40, many tiles per workgroup."""
+    h = torch.ops.bpe_hip
+    torch.manual_seed(6)
+    M, d, F, S, D = 8448, 768, 1024, 256, 64
+    x = torch.randn(M, d, device=gpu_device, dtype=torch.bfloat16)
+    w = (0.05 * torch.randn(2304, d, device=gpu_device)).to(torch.bfloat16)
+    w13 = (0.05 * torch.randn(2 * F, d, device=gpu_device)).to(torch.bfloat16)
+    w2 = (0.05 * torch.randn(d, F, device=gpu_device)).to(torch.bfloat16)
+    dy = torch.randn(M, d, device=gpu_device, dtype=torch.bfloat16)
+    ang = torch.arange(S, device=gpu_device, dtype=torch.float32)[:, None] * torch.rand(D // 2, device=gpu_device)
+    cos, sin = torch.cos(ang).contiguous(), torch.sin(ang).contiguous()
+    outs = {}
+    prev_p, prev_o = h.gpp_persist_config(persist), h.gpp_order_config(-1)
+    try:
+        for gm in (0, 2, 4, 8, 16):
+            h.gpp_order_config(gm)
+            c = torch.empty(M, 2304, device=gpu_device, dtype=torch.bfloat16)
+            h.gemm_pp(x, True, w, True, c, 0.0, 1)
+            q = h.gemm_qkv_rope(x, w, cos, sin, S, D, 1536)
+            gu, a = h.gemm_swiglu_fwd(x, w13)
+            dgu = h.gemm_swiglu_bwd(dy, w2, gu)
+            outs[gm] = (c, q, gu, a, dgu)
+    finally:
+        h.gpp_persist_config(prev_p)
+        h.gpp_order_config(prev_o)
+    for gm in (2, 4, 8, 16):
+        for t0, t1 in zip(outs[0], outs[gm]):
+            assert torch.equal(t0, t1), gm
+    assert rel(outs[0][0].cpu(), (x.float() @ w.float().t()).cpu()) < 1e-2
+
+
 @pytest.mark.parametrize("x_k", [False, True])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("splits", [1, 3])
