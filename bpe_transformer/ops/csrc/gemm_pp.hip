@@ -1451,7 +1451,7 @@ static void launch_pp1s(const __bf16* a, long lda, const __bf16* b, long ldb, fl
     const int grid = (M / BT) * (N / BT) * splits;
     Epi ep{};
     ep.prio = prio_mode();
-    ep.gm = SLAB ? 0 : order_for(N / BT);
+    ep.gm = SLAB ? (g_gm >= 0 ? g_gm : 0) : order_for(N / BT);
     if constexpr (!SLAB && DIAG == 0 && SPREAD != 0) {
         if (g_persist) {
             static bool pattr = false;
