@@ -83,18 +83,22 @@ def _fuse_swiglu_bwd(dy: Tensor, w2: Tensor, gu: Tensor) -> bool:
 
 
 _FUSE_SWIGLU_FWD = True  # module flag (tests compare the unfused path)
-_FUSE_SWIGLU_FWD_MAX_D = int(os.environ.get("BPE_FUSE_SWIGLU_FWD_MAX_D", "1024"))  # d_model cap (A/B knob)
+_FUSE_SWIGLU_FWD_MAX_D = int(os.environ.get("BPE_FUSE_SWIGLU_FWD_MAX_D", "0"))  # d_model cap override (A/B knob)
 
 
 def _fuse_swiglu_fwd(x: Tensor, w13: Tensor) -> bool:
     """The W13 GEMM with a = silu(g) * u in its epilogue (csrc/gemm_pp.hip EPI_SWIGLU_FWD): tokens in multiples
-    of 256, d_ff of 128, d_model of 64 up to 1024.  Past that the library GEMM's lead over the ping-pong kernel
-    outgrows the saved gate pass: GPT-2 (d 768) +0.7 % end to end, Llama-1.1B (d 2048) -1.2 % at B 8 and -0.9 % at
-    B 32 (profiles/bench/ab_e2e_swiglu_fwd_fused_b128.log, ab_llama_swiglu_fwd_fused.log,
-    ab_llama_swiglu_fused_b32.log; ``BPE_FUSE_SWIGLU_FWD_MAX_D`` moves the cap for such A/Bs)."""
-    return (_FUSE_SWIGLU_FWD and x.dtype == torch.bfloat16 and x.shape[0] % 256 == 0 and x.shape[1] % 64 == 0
-            and x.shape[1] <= _FUSE_SWIGLU_FWD_MAX_D and w13.shape[0] % 256 == 0 and x.stride(1) == 1
-            and w13.stride(1) == 1)
+    of 256, d_ff of 128, d_model of 64; d_model up to 1024 at any token count, wider at >= 65 536 tokens.  Below
+    that the library GEMM's lead over the ping-pong kernel outgrew the saved gate pass at d 2048: Llama-1.1B -1.2 %
+    at B 8 (profiles/bench/ab_llama_swiglu_fwd_fused.log) and, until round 6, -0.6-0.9 % at B 32
+    (ab_llama_swiglu_fused_b32.log, ab_llama_swiglu_fwd_fused_r5.log).  With the L2-aware tile order (gemm_pp.hip
+    tile_rc: the fused GEMM 2.46 -> 2.25 ms at Llama s2048 B 32) the fused form wins there, +0.2 % end to end
+    (profiles/bench/ab_llama_swiglu_fwd_fused_r6.log).  GPT-2 (d 768): +0.7 % (ab_e2e_swiglu_fwd_fused_b128.log).
+    ``BPE_FUSE_SWIGLU_FWD_MAX_D`` > 0 replaces the rule with a plain d_model cap for A/Bs."""
+    d, t = x.shape[1], x.shape[0]
+    wide_ok = d <= _FUSE_SWIGLU_FWD_MAX_D if _FUSE_SWIGLU_FWD_MAX_D > 0 else (d <= 1024 or t >= 65536)
+    return (_FUSE_SWIGLU_FWD and x.dtype == torch.bfloat16 and t % 256 == 0 and d % 64 == 0 and wide_ok
+            and w13.shape[0] % 256 == 0 and x.stride(1) == 1 and w13.stride(1) == 1)
 
 
 _FUSE_QKV_ROPE = True  # module flag (tests and A/B runs compare the unfused path)

@@ -49,3 +49,21 @@ def test_ppt_candidate_only_when_the_transpose_fits_32_bit_offsets():
     big = 2**31 // 256 + 64  # X^T's leading dimension T times 256 rows past 2^31
     cands = gemm._candidates(2304, 768, big - big % 64)
     assert "ppt" not in cands and "pp" in cands
+
+
+def test_swiglu_forward_fusion_rule(monkeypatch):
+    """The fused [W1;W3] + gate GEMM: d_model <= 1024 at any token count; wider only at >= 65 536 tokens per
+    micro-batch (where the L2-aware tile order made it win, profiles/bench/ab_llama_swiglu_fwd_fused_r6.log); an
+    explicit BPE_FUSE_SWIGLU_FWD_MAX_D cap replaces the rule."""
+    from bpe_transformer.models import fused_block as fb
+
+    def probe(t, d, f):
+        x = torch.empty(t, d, device="meta", dtype=torch.bfloat16)
+        return fb._fuse_swiglu_fwd(x, torch.empty(2 * f, d, device="meta", dtype=torch.bfloat16))
+
+    monkeypatch.setattr(fb, "_FUSE_SWIGLU_FWD_MAX_D", 0)
+    assert probe(131072, 768, 2048) and probe(512, 768, 2048)
+    assert probe(65536, 2048, 5632) and not probe(16384, 2048, 5632)
+    assert not probe(65536 + 64, 2048, 5632)  # tokens not a multiple of the 256-row tiles
+    monkeypatch.setattr(fb, "_FUSE_SWIGLU_FWD_MAX_D", 1024)
+    assert not probe(65536, 2048, 5632) and probe(256, 1024, 512)
