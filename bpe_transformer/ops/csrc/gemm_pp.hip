@@ -404,15 +404,31 @@ __device__ __forceinline__ SpreadOff spread_offsets(int g, int wl, int l, int ld
     return o;
 }
 
-__device__ __forceinline__ void dma_one(const __bf16* tile0, int off, char* img, int lbase) {
-    __builtin_amdgcn_global_load_lds((gbl_void*)(tile0 + off), (lds_void*)(img + lbase * 16), 16, 0, 0);
+// Cache policy of the in-loop LDS-DMA loads per operand (variant builds; 0 = default, 2 = nt: the line is the first
+// evicted from the XCD's L2).  Measured and left at 0 (profiles/bench/ab_dma_policy_r6.log): nt on A (activations)
+// -2 to -3 % on the MN x MN weight-gradient GEMMs on one box, +1 to +6 % on another, and slower K-major forward /
+// QKV + RoPE / ppt LM-head GEMMs (end to end -0.6-0.9 %); nt on B (weights, re-read every round) slower everywhere.
+#ifndef BPE_GPP_DMA_POL_A
+#define BPE_GPP_DMA_POL_A 0
+#endif
+#ifndef BPE_GPP_DMA_POL_B
+#define BPE_GPP_DMA_POL_B 0
+#endif
+
+template <int POL>
+__device__ __forceinline__ void dma_ld(const __bf16* src, char* dst) {
+    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, POL);
 }
 
+template <int POL = 0>
+__device__ __forceinline__ void dma_one(const __bf16* tile0, int off, char* img, int lbase) {
+    dma_ld<POL>(tile0 + off, img + lbase * 16);
+}
+
+template <int POL = 0>
 __device__ __forceinline__ void dma_pair(const __bf16* tile0, const int (&off)[2], char* img, int lbase) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_global_load_lds((gbl_void*)(tile0 + off[j]), (lds_void*)(img + (lbase + 64 * j) * 16), 16,
-                                         0, 0);
+    for (int j = 0; j < 2; ++j) dma_ld<POL>(tile0 + off[j], img + (lbase + 64 * j) * 16);
 }
 
 // SPLIT (spread mode 2, the weight-gradient layout): the second piece of each
@@ -430,6 +446,7 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     Frags f;
     char* Ac = cur;
     char* Bc = cur + OPB;
+    constexpr int PA = BPE_GPP_DMA_POL_A, PB = BPE_GPP_DMA_POL_B;
     if (DIAG == 1) dma = false;
     // one phase: fragment reads (done by the caller), pieces of (tile, off, img, lbase), wait, barrier, MFMAs
     // RELAX: phase 2 (m1, n1) retires nothing that a read before phase 3's barrier needs (its own A rows of K-tile
@@ -437,11 +454,12 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
     // so it waits vmcnt(6) and leaves the piece pair issued two load sections ago in flight one section longer
     auto phase = [&](const __bf16* t0, const int (&off)[2], char* img, int lb, int m, int n, bool last_nodma_wait2,
                      bool relax = false) {
+        const bool is_a = img == nxt;  // the A image sits at the stage origin, B at + OPB
         const int ph = 2 * m + (m ? 1 - n : n);  // (m0,n0) 0, (m0,n1) 1, (m1,n1) 2, (m1,n0) 3
         (void)ph;
         if (dma) {
-            if constexpr (SPLIT) dma_one(t0, off[0], img, lb);
-            else dma_pair(t0, off, img, lb);
+            if constexpr (SPLIT) is_a ? dma_one<PA>(t0, off[0], img, lb) : dma_one<PB>(t0, off[0], img, lb);
+            else is_a ? dma_pair<PA>(t0, off, img, lb) : dma_pair<PB>(t0, off, img, lb);
         }
         if (first && m == 0) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -461,7 +479,7 @@ __device__ __forceinline__ void ktile_spread(char* __restrict__ cur, char* __res
             mma_half<F8>(acc, f, m, n, 0);
             if (dma) {
                 __builtin_amdgcn_sched_barrier(0);
-                dma_one(t0, off[1], img, lb + 64);
+                is_a ? dma_one<PA>(t0, off[1], img, lb + 64) : dma_one<PB>(t0, off[1], img, lb + 64);
                 __builtin_amdgcn_sched_barrier(0);
             }
             mma_half<F8>(acc, f, m, n, 1);
@@ -846,10 +864,10 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
             const long k0 = (long)kb * BK;
             const __bf16* a0 = tile_ptr<AK>(A, lda, i0, k0);
             const __bf16* b0 = tile_ptr<BKM>(B, ldb, jb, k0);
-            dma_pair(a0, so.a0, smem, so.la0);
-            dma_pair(b0, so.b0, smem + OPB, so.lb0);
-            dma_pair(b0, so.b1, smem + OPB, so.lb1);
-            dma_pair(a0, so.a1, smem, so.la1);
+            dma_pair<BPE_GPP_DMA_POL_A>(a0, so.a0, smem, so.la0);
+            dma_pair<BPE_GPP_DMA_POL_B>(b0, so.b0, smem + OPB, so.lb0);
+            dma_pair<BPE_GPP_DMA_POL_B>(b0, so.b1, smem + OPB, so.lb1);
+            dma_pair<BPE_GPP_DMA_POL_A>(a0, so.a1, smem, so.la1);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bar();
         }
@@ -980,10 +998,10 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
     {  // prologue of the first tile: all of its K-tile 0, retired before the first read
         const __bf16* a0 = tile_ptr<AK>(A, lda, i0, 0);
         const __bf16* b0 = tile_ptr<BKM>(B, ldb, jb, 0);
-        dma_pair(a0, so.a0, smem, so.la0);
-        dma_pair(b0, so.b0, smem + OPB, so.lb0);
-        dma_pair(b0, so.b1, smem + OPB, so.lb1);
-        dma_pair(a0, so.a1, smem, so.la1);
+        dma_pair<BPE_GPP_DMA_POL_A>(a0, so.a0, smem, so.la0);
+        dma_pair<BPE_GPP_DMA_POL_B>(b0, so.b0, smem + OPB, so.lb0);
+        dma_pair<BPE_GPP_DMA_POL_B>(b0, so.b1, smem + OPB, so.lb1);
+        dma_pair<BPE_GPP_DMA_POL_A>(a0, so.a1, smem, so.la1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();
     }
@@ -1126,10 +1144,10 @@ __global__ void __launch_bounds__(NT, 1) gemm_pp_dwg_kernel(DwGroup gp, float* _
         const long k0 = (long)kb * BK;
         const __bf16* a0 = tile_ptr<false>(A, lda, i0, k0);
         const __bf16* b0 = tile_ptr<BKM>(B, ldb, j0, k0);
-        dma_pair(a0, so.a0, smem, so.la0);
-        dma_pair(b0, so.b0, smem + OPB, so.lb0);
-        dma_pair(b0, so.b1, smem + OPB, so.lb1);
-        dma_pair(a0, so.a1, smem, so.la1);
+        dma_pair<BPE_GPP_DMA_POL_A>(a0, so.a0, smem, so.la0);
+        dma_pair<BPE_GPP_DMA_POL_B>(b0, so.b0, smem + OPB, so.lb0);
+        dma_pair<BPE_GPP_DMA_POL_B>(b0, so.b1, smem + OPB, so.lb1);
+        dma_pair<BPE_GPP_DMA_POL_A>(a0, so.a1, smem, so.la1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();
     }
