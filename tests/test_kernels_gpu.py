@@ -1317,14 +1317,17 @@ def test_gemm_fp8_persistent_bitwise_many_tiles(gpu_device):
     cos, sin = R.rope_tables(D, S, 10000.0, device=gpu_device)
     ref_rope = ref.clone()
     h.rope_qk_(ref_rope, cos, sin, M // S, S, H, Hkv, D)
-    prev = h.gpp_persist_config(0)
+    prev, prev_o = h.gpp_persist_config(0), h.gpp_order_config(-1)
     try:
         for mode in (0, 1, 3, 1, 1):
             h.gpp_persist_config(mode)
-            assert torch.equal(h.gemm_fp8(a8, b8, sa, sb), ref), mode
-            assert torch.equal(h.gemm_fp8_rope(a8, b8, sa, sb, cos, sin, S, D, (H + Hkv) * D), ref_rope), mode
+            for gm in (0, 2, 4):  # explicit tile orders (the fp8 GEMMs are row-major in auto mode)
+                h.gpp_order_config(gm)
+                assert torch.equal(h.gemm_fp8(a8, b8, sa, sb), ref), (mode, gm)
+                assert torch.equal(h.gemm_fp8_rope(a8, b8, sa, sb, cos, sin, S, D, (H + Hkv) * D), ref_rope), (mode, gm)
     finally:
         h.gpp_persist_config(prev)
+        h.gpp_order_config(prev_o)
     # split-K weight-gradient form: 16 x 10 output tiles x 4 splits over K = 16384 tokens, fp32 C, beta = 1
     Mw, Kw = 4096, 16384
     aw = torch.randint(-2, 3, (Mw, Kw), generator=g).float()
