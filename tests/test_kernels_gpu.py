@@ -543,7 +543,7 @@ def test_gemm_swiglu_bwd_bitwise_on_exact_products(gpu_device, gpp_mode):
     assert torch.equal(dgu, torch.ops.bpe_hip.swiglu_bwd(da.contiguous(), gu))
 
 
-@pytest.mark.parametrize("M,d,F", [(512, 192, 768), (256, 64, 128)])
+@pytest.mark.parametrize("M,d,F", [(512, 192, 768), (256, 64, 128), (512, 2048, 5632)])  # + Llama-1.1B width
 def test_gemm_swiglu_fwd(gpu_device, gpp_mode, M, d, F):
     """x @ [W1; W3]^T with a = silu(g) * u in the epilogue.  Small-integer operands make gu exact, so gu must
     equal the plain product bitwise and a must equal the unfused swiglu_fwd of it; random operands are
