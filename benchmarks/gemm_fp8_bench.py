@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--tokens", type=int, default=16384,
                     help="M of the Llama shapes (16384 = s4096 B4; 65536 = s4096 B16, the bench default)")
+    ap.add_argument("--orders", type=int, nargs="*", default=[], help="extra hand-kernel arms at these tile orders")
     a = ap.parse_args()
     h = ops()
     for name, (M, N, K) in SHAPES.items():
@@ -36,10 +37,12 @@ def main():
         x8, w8 = x.to(fa), w.to(torch.float8_e4m3fn)
         one = torch.ones(1, device="cuda")
         arms = {
-            "hip_fp8": lambda: h.gemm_fp8(x8, w8, one, one),
+            "hip_fp8": lambda: (h.gpp_order_config(0), h.gemm_fp8(x8, w8, one, one))[1],
             "lib_fp8": lambda: torch._scaled_mm(x8, w8.t(), scale_a=one[0], scale_b=one[0], out_dtype=torch.bfloat16),
             "bf16": lambda: x @ w.t(),
         }
+        for gm in a.orders:  # the hand kernel under explicit column-major tile orders (gemm_pp.hip tile_rc)
+            arms[f"hip_fp8_gm{gm}"] = (lambda gm=gm: (h.gpp_order_config(gm), h.gemm_fp8(x8, w8, one, one))[1])
         ref = x8.float() @ w8.float().t()
         err = float(((h.gemm_fp8(x8, w8, one, one).float() - ref).norm() / ref.norm()).item())
         times = {k: [] for k in arms}

@@ -15,7 +15,8 @@ forward (x = xr + xd: the previous block's residual and its not-yet-added FFN ou
     g2 = a @ W2^T                     hipBLASLt; the block returns (xm, g2), added by the next norm
     (fp8 with fp8 weight gradients: the two norms write h1 / h2 and the gate writes a only as e4m3 in both
     layouts, and the gate's backward writes its gradient only as e5m2 in both layouts: ops/fp8.py
-    add_rmsnorm_cast_t, swiglu_fwd_cast_t / swiglu_bwd_cast_t)
+    add_rmsnorm_cast_t, swiglu_fwd_cast_t / swiglu_bwd_cast_t; the W13 GEMM itself writes a's two e4m3 layouts
+    when the shapes allow, ops/fp8.py matmul_swiglu)
 
 backward: the mirror image, with
   * the SwiGLU backward fused into the epilogue of the dY @ W2 GEMM (our
@@ -52,7 +53,8 @@ from torch import Tensor
 
 from ..ops._ext import ops as hip
 from ..ops.attention import prerotate_default
-from ..ops.fp8 import add_rmsnorm_cast_t, norm_cast_ok, rope_ok, swiglu_bwd_cast_t, swiglu_cast_ok, swiglu_fwd_cast_t
+from ..ops.fp8 import (add_rmsnorm_cast_t, matmul_swiglu, norm_cast_ok, rope_ok, swiglu_bwd_cast_t, swiglu_cast_ok,
+                       swiglu_fwd_cast_t, swiglu_gemm_ok)
 from ..ops import gemm as _gemm
 from ..ops.gemm import accumulate_weight_grad
 
@@ -209,15 +211,24 @@ class FusedBlockFn(torch.autograd.Function):
             h2 = None
         else:
             xm, h2, r2 = hip().add_rmsnorm_fwd(x2, g1, ln2, eps)
+        aq = None  # fp8: a already quantised (both layouts) by the fused W13 GEMM
         if fp8 is None and _fuse_swiglu_fwd(h2, w_13):
             gu, a = hip().gemm_swiglu_fwd(h2, w_13)  # the gate in the GEMM epilogue: no second pass over gu
+        elif (fp8 is not None and xt8s is not None and _FP8_SWIGLU_CAST and h2q is not None
+              and swiglu_gemm_ok(h2q[0], w_13)):
+            # fp8 with weight gradients: W13 GEMM + gate + two-layout e4m3 cast of a in one kernel (the
+            # bookkeeping of mm(): the e4m3 W^T for the input gradient, X^T for the weight gradient)
+            gu, w8t13, xt813, aq = matmul_swiglu(st, h2q, w_13, s0 + 2, s0 + 6, s0 + 3)
+            w8s.append(w8t13)
+            xt8s.append(xt813)
+            a = None
         else:
             gu = mm(h2, w_13, 2, xq=h2q) if fp8 is not None else torch.matmul(h2, w_13.t())
             a = None if xt8s is not None and _FP8_SWIGLU_CAST and swiglu_cast_ok(gu) else hip().swiglu_fwd(gu)
         if a is None:
             # fp8 weight gradients: a = silu(g) u is written only as the W2 GEMM's fp8 operand, in both layouts,
-            # by one pass over gu (no bf16 a, no separate cast)
-            g2 = mm(None, w2.detach(), 3, xq=swiglu_fwd_cast_t(fp8[0], gu, fp8[1] + 3))
+            # by one pass over gu (no bf16 a, no separate cast) -- or already by the fused W13 GEMM
+            g2 = mm(None, w2.detach(), 3, xq=aq if aq is not None else swiglu_fwd_cast_t(fp8[0], gu, fp8[1] + 3))
         else:
             g2 = mm(a, w2.detach(), 3) if fp8 is not None else torch.matmul(a, w2.t())
         ctx.w8s = w8s if w8s else None

@@ -166,4 +166,26 @@ __host__ __forceinline__ int stream_grid(size_t work_items, int block, int cap =
     return (int)g;
 }
 
+constexpr float FP8_E4M3_MAX = 448.f;     // OCP e4m3fn: activations / weights
+constexpr float FP8_E5M2_MAX = 57344.f;   // OCP e5m2: gradients (wider range, 2 mantissa bits)
+
+// FMT 0 = e4m3fn (v_cvt_pk_fp8_f32), 1 = e5m2 (v_cvt_pk_bf8_f32); saturating: clamp before the convert
+template <int FMT>
+__device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
+    constexpr float M = FMT == 0 ? FP8_E4M3_MAX : FP8_E5M2_MAX;
+    a = fminf(fmaxf(a, -M), M);
+    b = fminf(fmaxf(b, -M), M);
+    c = fminf(fmaxf(c, -M), M);
+    d = fminf(fmaxf(d, -M), M);
+    int w;
+    if constexpr (FMT == 0) {
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);  // bytes 0,1
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);   // bytes 2,3
+    } else {
+        w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+        w = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
+    }
+    return (unsigned)w;
+}
+
 }  // namespace bpe

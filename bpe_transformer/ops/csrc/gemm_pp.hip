@@ -542,7 +542,15 @@ __device__ long long g_gpp_stamps[65536 * 8];
 // EPI_ROPE: the QKV projection with RoPE on its Q / K columns (output columns [0, rot_cols)), applied to the
 // bf16-rounded products exactly as rope_qk_kernel (rope.hip) applies it to the stored activation: interleaved
 // pairs, position = row % S, fp32 cos / sin tables [S][D / 2].  Saves the separate in-place pass over Q / K.
-enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2, EPI_ROPE = 3 };
+// EPI_SWIGLU_FWD8: the fp8 forward [W1; W3] GEMM (e4m3 x e4m3) with the SwiGLU gate AND its two-layout e4m3 cast
+// in the epilogue: writes gu (bf16, for the backward), a8 = e4m3(a * scale) [M][F] and a8t [F][M] (the W2 GEMM's
+// operands) and folds max |a| into the slot's amax -- the swiglu_cast_fp8 pass over gu (0.43 ms per Llama layer at
+// 65 536 tokens) disappears.  Same values, rounding and amax as launch_gemm_fp8 + swiglu_cast_fp8_t (bitwise).
+// Persistent kernel only (the a8 tile is transposed through 18 KiB of LDS past the two stages).
+enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2, EPI_ROPE = 3, EPI_SWIGLU_FWD8 = 4 };
+constexpr bool is_swf(int e) { return e == EPI_SWIGLU_FWD || e == EPI_SWIGLU_FWD8; }
+constexpr int A8T_STRIDE = 144;               // bytes per token row of the a8 transpose tile (conflict-free reads)
+constexpr int A8T_BYTES = 128 * A8T_STRIDE;   // one pass: 128 token rows x 128 a columns
 // 1: the SwiGLU epilogues' arithmetic on the packed fp32 VALU, two elements per instruction (common.h
 // fast_sigmoid2; bitwise the same results); 0: one element per instruction (A/B variant builds)
 #ifndef BPE_GPP_PK
@@ -597,6 +605,11 @@ struct Epi {
     const float* cosT = nullptr;  // EPI_ROPE: [S][D / 2] tables, S, head dim, rotated column count
     const float* sinT = nullptr;
     int S = 0, D = 0, rot_cols = 0;
+    uint8_t* a8 = nullptr;        // EPI_SWIGLU_FWD8: a8 [M][F], a8t [F][M] (ld M), the slot's scale and amax bits
+    uint8_t* a8t = nullptr;
+    long ld_a8t = 0;
+    const float* a_scale = nullptr;
+    unsigned* a_amax = nullptr;
     int gm = 0;  // tile order (tile_rc): 0 = row-major, gm > 0 = column-major within bands of gm row blocks
 };
 
@@ -627,7 +640,8 @@ __device__ __forceinline__ void tile_rc(int t, int tiles_m, int tiles_n, int gm,
 template <int EPI, int F8, int NPASS>
 __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* stg, int g, int wl, int l, int tid,
                                               int i0, int j0, int jb, __bf16* C, long ldc, float beta, const Epi& ep,
-                                              bool st_on, bool tail, int sid) {
+                                              bool st_on, bool tail, int sid, char* xtra = nullptr,
+                                              float* amx = nullptr) {
     constexpr int RP = BT / NPASS;  // tile rows per pass
     float osc = 1.f;  // F8: the product of the operands' inverse scales (device-resident, one load)
     if constexpr (F8 != 0) osc = ep.sa[0] * ep.sb[0];
@@ -743,6 +757,60 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
                                             (unsigned)(((long)i * ep.ld_act + c * 8) * 2), av);
                 }
             }
+        } else if constexpr (EPI == EPI_SWIGLU_FWD8) {
+            // as EPI_SWIGLU_FWD for gu; a = bf16(silu(g) u) (swiglu_cast_fp8_c128_kernel's values) is cast to e4m3
+            // with the slot's scale, stored row-major from registers and, through the a8 tile in LDS (xtra), as
+            // a8t; max |a| accumulates in *amx (one atomic per workgroup, by the caller)
+            static_assert(NPASS == 2, "the a8 transpose tile covers one 128-row pass");
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            bar();
+            if (h == 0) GPP_STAMP_T(sid, 3);
+            const int c = tid & 15;
+            const float sc = ep.a_scale[0];
+            float am = *amx;
+#pragma unroll 2
+            for (int q = 0; q < 8 / NPASS; ++q) {
+                const int i = q * 32 + (tid >> 4);
+                const u16x8 gv = *reinterpret_cast<const u16x8*>(stg + i * 512 + ((c ^ (i & 15)) << 4));
+                const u16x8 uv = *reinterpret_cast<const u16x8*>(stg + i * 512 + (((16 + c) ^ (i & 15)) << 4));
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float gg = bf2f(gv[e]);
+                    v[e] = bf2f(f2bf(gg * fast_sigmoid(gg) * bf2f(uv[e])));
+                    am = fmaxf(am, fabsf(v[e]));
+                }
+                const uint2 q8 = {pack4_fp8<0>(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc),
+                                  pack4_fp8<0>(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc)};
+                if (st_on) {
+                    __bf16* tg = ep.dgu + (long)(i0 + r0) * ep.ld + jb;
+                    const unsigned og = (unsigned)(((long)i * ep.ld + c * 8) * 2);
+                    st16<BPE_GPP_POL_SWF_GU>(tg, og, gv);
+                    st16<BPE_GPP_POL_SWF_GU>(tg, og + (unsigned)ep.F * 2, uv);
+                    *reinterpret_cast<uint2*>(ep.a8 + (long)(i0 + r0 + i) * ep.F + jb + c * 8) = q8;
+                }
+                *reinterpret_cast<uint2*>(xtra + i * A8T_STRIDE + c * 8) = q8;
+            }
+            *amx = am;
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            bar();
+            // a8t rows jb + 4 f4 + j (j < 4), tokens i0 + r0 + 8 tg .. + 7: 8 words of 4 columns -> 4 x 8 bytes
+            const int f4 = tid & 31, tg = tid >> 5;
+            unsigned wv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) wv[k] = *reinterpret_cast<const unsigned*>(xtra + (8 * tg + k) * A8T_STRIDE + 4 * f4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                unsigned lo = 0, hi = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    lo |= ((wv[k] >> (8 * j)) & 0xffu) << (8 * k);
+                    hi |= ((wv[k + 4] >> (8 * j)) & 0xffu) << (8 * k);
+                }
+                if (st_on)
+                    *reinterpret_cast<uint2*>(ep.a8t + (long)(jb + 4 * f4 + j) * ep.ld_a8t + i0 + r0 + 8 * tg) =
+                        uint2{lo, hi};
+            }
         } else if constexpr (EPI == EPI_ROPE) {
             // this thread's 8 columns are one quarter of a pair block of one head: the cos / sin loads of its rows
             // (positions) are issued before the barrier, like the SwiGLU-backward operands
@@ -822,7 +890,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
     tile_rc(tile, M / BT, tiles_n, ep.gm, ti, tj);
     const int i0 = ti * BT, j0 = tj * BT;
     // B tile origin: EPI_SWIGLU_FWD tiles 128 g columns (+ the matching u columns, offset F rows in B)
-    const int jb = EPI == EPI_SWIGLU_FWD ? tj * (BT / 2) : j0;
+    const int jb = is_swf(EPI) ? tj * (BT / 2) : j0;
     const int nkt = R / BK;
     const int kb = (int)((long)split * nkt / splits);
     const int nk = (int)((long)(split + 1) * nkt / splits) - kb;
@@ -848,7 +916,7 @@ gemm_pp_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __restrict_
 
     if constexpr (SPR) {
         SpreadOff so = spread_offsets<AK, BKM>(g, wl, l, (int)lda, (int)ldb);
-        if constexpr (EPI == EPI_SWIGLU_FWD) {
+        if constexpr (is_swf(EPI)) {
             // group g DMAs B rows [128 g, +128) of the tile: group 1's are the u rows, F - 128 rows further on
             static_assert(BKM, "SwiGLU forward: B = [W1; W3] is K-major");
             if (g == 1) {
@@ -974,7 +1042,7 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
     const int nk = R / BK;
     if (ep.prio && g == 1) __builtin_amdgcn_s_setprio(1);
     SpreadOff so = spread_offsets<AK, BKM>(g, wl, l, (int)lda, (int)ldb);
-    if constexpr (EPI == EPI_SWIGLU_FWD) {
+    if constexpr (is_swf(EPI)) {
         static_assert(BKM, "SwiGLU forward: B = [W1; W3] is K-major");
         if (g == 1) {
             const int du = (ep.F - BT / 2) * (int)ldb;
@@ -991,7 +1059,7 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
         tile_rc(t, M / BT, tiles_n, ep.gm, ti, tj);
         i0 = ti * BT;
         j0 = tj * BT;
-        jb = EPI == EPI_SWIGLU_FWD ? tj * (BT / 2) : j0;
+        jb = is_swf(EPI) ? tj * (BT / 2) : j0;
     };
     int t = wid, i0, j0, jb;
     origin(t, i0, j0, jb);
@@ -1007,6 +1075,7 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
     }
     int st = 0;  // the stage holding the current K-tile
     f32x4 acc[8][4];
+    float amx = 0.f;  // EPI_SWIGLU_FWD8: this thread's max |a| over its tiles
 #ifdef BPE_GPP_STAMPS
     unsigned xcc_id, hw_id;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
@@ -1051,13 +1120,27 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
         // -- 0.77 vs 0.69 ms, profiles/bench/ab_swiglu_bwd_reg_epilogue_r6.log: each access instruction then covers
         // 16 rows x 2 x 32 B instead of 2 rows x 512 B.)
         epilogue_bf16<EPI, F8, 2>(acc, smem + (st ^ 1) * STAGE, g, wl, l, tid, i0, j0, jb, C, ldc, beta, ep, true,
-                                  more, t);
+                                  more, t, smem + LDS_LAUNCH, &amx);
         GPP_STAMP_T(t, 4);
         if (!more) break;
         t = tn;
         i0 = i0n;
         j0 = j0n;
         jb = jbn;
+    }
+    if constexpr (EPI == EPI_SWIGLU_FWD8) {  // the workgroup's max |a|: one atomic per workgroup (256 per launch)
+        float m = amx;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        float* red = reinterpret_cast<float*>(smem + LDS_LAUNCH);
+        __syncthreads();  // every wave is done with the a8 tile
+        if (l == 0) red[w] = m;
+        __syncthreads();
+        if (tid == 0) {
+#pragma unroll
+            for (int i = 1; i < NT / 64; ++i) m = fmaxf(m, red[i]);
+            atomicMax(ep.a_amax, __float_as_uint(m));  // amax >= 0: the bit pattern orders as the float
+        }
     }
 }
 
@@ -1430,6 +1513,36 @@ void launch_gemm_fp8_rope(const void* A, long lda, const void* B, long ldb, void
     if (!attr) lds_attr(k), attr = true;
     k<<<(M / BT) * (N / BT), NT, LDS_LAUNCH, s>>>((const __bf16*)A, lda / 2, (const __bf16*)B, ldb / 2, nullptr,
                                                   (__bf16*)C, ldc, 0.f, M, N, K / 2, 1, ep);
+}
+
+// gu = (X8 . W13_8^T) * sa * sb (e4m3 x e4m3, K-major; W13_8 = [W1; W3] [2F][K]) with a = silu(g) u cast to e4m3
+// (scale a_scale) in both layouts a8 [M][F], a8t [F][M] and max |a| folded into *a_amax (EPI_SWIGLU_FWD8).  M a
+// multiple of 256, F of 128, K of 128.  Always the persistent kernel (g_persist >= 2 caps its grid, as elsewhere).
+void launch_gemm_fp8_swiglu(const void* A8, long lda, const void* B8, long ldb, void* gu, long ldg, void* a8,
+                            void* a8t, int M, int F, int K, const float* sa, const float* sb, const float* a_scale,
+                            unsigned* a_amax, hipStream_t s) {
+    Epi ep{nullptr, (__bf16*)gu, ldg, F};
+    ep.prio = prio_mode();
+    // bands of 8 row blocks: the Llama fp8 W13 GEMM 1.17 vs 1.32 ms row-major (profiles/bench/fp8_gemm_orders_r6.log)
+    ep.gm = g_gm >= 0 ? g_gm : 8;
+    ep.sa = sa;
+    ep.sb = sb;
+    ep.a8 = (uint8_t*)a8;
+    ep.a8t = (uint8_t*)a8t;
+    ep.ld_a8t = M;
+    ep.a_scale = a_scale;
+    ep.a_amax = a_amax;
+    auto* kp = &gemm_pp_persist_kernel<true, true, EPI_SWIGLU_FWD8, 1, 1>;
+    static bool pattr = false;
+    if (!pattr) {
+        (void)hipFuncSetAttribute((const void*)kp, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_LAUNCH + A8T_BYTES);
+        pattr = true;
+    }
+    const int ntiles = (M / BT) * (F / (BT / 2));
+    const int cap = g_persist >= 2 ? g_persist : num_cus();
+    kp<<<ntiles < cap ? ntiles : cap, NT, LDS_LAUNCH + A8T_BYTES, s>>>((const __bf16*)A8, lda / 2,
+                                                                       (const __bf16*)B8, ldb / 2, (__bf16*)nullptr,
+                                                                       0L, 0.f, M, 2 * F, K / 2, ep);
 }
 
 // C = beta * C + (A8 . B8^T) * sa * sb, split over K into `splits` fp32 partials (slab [splits][M][N]) summed in a

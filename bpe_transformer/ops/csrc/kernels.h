@@ -96,6 +96,10 @@ void launch_gemm_pp_dw_group(int np, const void* const* A, const long* lda, cons
 
 // fp8 x fp8 -> bf16 on the ping-pong kernel with v_mfma_scale_f32_16x16x128_f8f6f4: C = A8 B8^T * sa * sb,
 // A8 [M][K] (fmt_a 0 e4m3 / 1 e5m2), B8 [N][K] e4m3, both K-major; strides in bytes (A, B) / elements (C)
+// gu = (X8 . W13_8^T) * sa * sb with a = silu(g) u cast to e4m3 in both layouts + amax (fused fp8 SwiGLU forward)
+void launch_gemm_fp8_swiglu(const void* A8, long lda, const void* B8, long ldb, void* gu, long ldg, void* a8,
+                            void* a8t, int M, int F, int K, const float* sa, const float* sb, const float* a_scale,
+                            unsigned* a_amax, hipStream_t s);
 void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                      int fmt_a, const float* sa, const float* sb, hipStream_t s);
 

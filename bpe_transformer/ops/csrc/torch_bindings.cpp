@@ -490,6 +490,40 @@ at::Tensor gemm_fp8(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor
     return y;
 }
 
+// gu = (x8 @ w8^T) * sa * sb (e4m3 x e4m3; w8 = [W1; W3] e4m3 [2F, K]) with a = silu(g) * u cast to e4m3 with
+// a_scale in both layouts (a8 [M, F], a8t [F, M]) and max |a| folded into a_amax: the fp8 W13 GEMM and the
+// swiglu_cast_fp8_t pass in one kernel (gemm_pp.hip EPI_SWIGLU_FWD8)
+at::Tensor gemm_fp8_swiglu(const at::Tensor& x8, const at::Tensor& w8, const at::Tensor& sa, const at::Tensor& sb,
+                           const at::Tensor& a_scale, at::Tensor a8, at::Tensor a8t, at::Tensor a_amax) {
+    check_cuda(x8, "x8");
+    check_cuda(w8, "w8");
+    TORCH_CHECK(x8.scalar_type() == at::kFloat8_e4m3fn && w8.scalar_type() == at::kFloat8_e4m3fn,
+                "gemm_fp8_swiglu: e4m3 operands");
+    TORCH_CHECK(x8.dim() == 2 && w8.dim() == 2 && x8.is_contiguous() && w8.is_contiguous() && x8.size(1) == w8.size(1),
+                "gemm_fp8_swiglu: x8 [M, K] and w8 [2F, K] contiguous with a common K");
+    const int64_t M = x8.size(0), F = w8.size(0) / 2, K = x8.size(1);
+    TORCH_CHECK(w8.size(0) == 2 * F && M % 256 == 0 && F % 128 == 0 && K % 128 == 0 && K > 0,
+                "gemm_fp8_swiglu: M a multiple of 256, F of 128, K of 128");
+    TORCH_CHECK(K * 256 < (1L << 32) && 2 * F * K < (1L << 32), "gemm_fp8_swiglu: operand offsets exceed 32 bits");
+    TORCH_CHECK(a8.is_contiguous() && a8t.is_contiguous() && a8.scalar_type() == at::kFloat8_e4m3fn &&
+                    a8t.scalar_type() == at::kFloat8_e4m3fn && a8.dim() == 2 && a8.size(0) == M && a8.size(1) == F &&
+                    a8t.dim() == 2 && a8t.size(0) == F && a8t.size(1) == M && a8.device() == x8.device() &&
+                    a8t.device() == x8.device(),
+                "gemm_fp8_swiglu: a8 [M, F] and a8t [F, M] e4m3 on the operands' device");
+    TORCH_CHECK(sa.scalar_type() == at::kFloat && sb.scalar_type() == at::kFloat && a_scale.scalar_type() == at::kFloat &&
+                    sa.numel() >= 1 && sb.numel() >= 1 && a_scale.numel() == 1 && a_amax.scalar_type() == at::kInt &&
+                    a_amax.numel() == 1 && sa.device() == x8.device() && sb.device() == x8.device() &&
+                    a_scale.device() == x8.device() && a_amax.device() == x8.device(),
+                "gemm_fp8_swiglu: fp32 device scalars sa, sb, a_scale and one int32 amax slot");
+    DevGuard g(x8.device());
+    auto gu = at::empty({M, 2 * F}, x8.options().dtype(at::kBFloat16));
+    launch_gemm_fp8_swiglu(x8.data_ptr(), x8.stride(0), w8.data_ptr(), w8.stride(0), gu.data_ptr(), gu.stride(0),
+                           a8.data_ptr(), a8t.data_ptr(), (int)M, (int)F, (int)K, sa.data_ptr<float>(),
+                           sb.data_ptr<float>(), a_scale.data_ptr<float>(),
+                           reinterpret_cast<unsigned*>(a_amax.data_ptr<int>()), cur_stream());
+    return gu;
+}
+
 // qkv = (a8 @ b8^T) * sa * sb (e4m3 x e4m3) with RoPE on output columns [0, rot_cols) in the epilogue
 at::Tensor gemm_fp8_rope(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor& sa, const at::Tensor& sb,
                          const at::Tensor& cos, const at::Tensor& sin, int64_t S, int64_t D, int64_t rot_cols) {
@@ -1126,6 +1160,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int S, int D, int rot_cols) -> Tensor");
     m.def("gemm_fp8_acc(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor(a!) c, float beta, int splits) -> ()");
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb) -> Tensor");
+    m.def("gemm_fp8_swiglu(Tensor x8, Tensor w8, Tensor sa, Tensor sb, Tensor a_scale, Tensor(a!) a8, Tensor(b!) a8t, "
+          "Tensor(c!) a_amax) -> Tensor");
     m.def("gemm_fp8_rope(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor cos, Tensor sin, int S, int D, "
           "int rot_cols) -> Tensor");
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
@@ -1184,6 +1220,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("gemm_qkv_rope", &gemm_qkv_rope);
     m.impl("gemm_fp8_acc", &gemm_fp8_acc);
     m.impl("gemm_fp8", &gemm_fp8);
+    m.impl("gemm_fp8_swiglu", &gemm_fp8_swiglu);
     m.impl("gemm_fp8_rope", &gemm_fp8_rope);
     m.impl("cast_fp8", &cast_fp8);
     m.impl("transpose_bf16", &transpose_bf16);

@@ -11,9 +11,12 @@ Recipe (BASELINE.json "Llama-style 1.1B fp8 MFMA path"):
       - every weight gradient: the hand kernel's split-K form
         (:func:`wgrad_acc`, ``gemm_fp8_acc``), 2.29-2.64 vs the library's
         1.65-2.09 PF/s (``profiles/bench/fp8_wgrad_r4.log``);
-      - the O / W13 / W2 forward and every input gradient: hipBLASLt's
-        ``torch._scaled_mm``, which leads the hand kernel by 11-17 % at these
-        shapes (``profiles/bench/gemm_fp8_persistent_vs_lib_r4.log``).  The route
+      - the W13 forward with weight gradients on: the hand kernel with the
+        SwiGLU gate and its two-layout e4m3 cast in the epilogue
+        (:func:`matmul_swiglu`; round 6);
+      - the O / W2 forward (and W13 without fused casts) and every input
+        gradient: hipBLASLt's ``torch._scaled_mm``, which leads the hand kernel
+        by 3-12 % at these shapes (``profiles/bench/fp8_gemm_orders_r6.log``).  The route
         table ``ops/tuning/fp8_routes.json`` sends only its listed shapes (two
         16 384-token ones) to the hand kernel; ``BPE_FP8_GEMM=hip`` / ``lib`` force
         one path for all of :func:`mm_fp8`;
@@ -266,6 +269,40 @@ def swiglu_fwd_cast_t(state: Fp8State, gu: Tensor, slot: int) -> tuple[Tensor, T
     a8t = torch.empty(F, M, dtype=state.dtype, device=gu.device)
     ops().swiglu_cast_fp8_t(gu, None, state.scale[slot : slot + 1], a8, a8t, state.amax[slot : slot + 1])
     return a8, a8t
+
+
+# BPE_FP8_SWIGLU_GEMM=0: the fp8 W13 GEMM (routed, hipBLASLt at the bench shapes) then swiglu_fwd_cast_t, instead
+# of the hand kernel with the gate and its two-layout cast in the epilogue (swiglu_gemm_ok / matmul_swiglu)
+_SWIGLU_GEMM = os.environ.get("BPE_FP8_SWIGLU_GEMM", "1") == "1"
+
+
+def swiglu_gemm_ok(x8: Tensor, w13: Tensor) -> bool:
+    """Shapes the fused fp8 W13 + SwiGLU + two-layout cast kernel takes: tokens a multiple of 256, d_ff of 128,
+    d_model of 128, 32-bit operand offsets; never under ``BPE_FP8_GEMM=lib``."""
+    M, K = x8.shape
+    F2 = w13.shape[0]
+    return (_SWIGLU_GEMM and _MODE != "lib" and x8.dtype == FP8 and x8.is_contiguous() and M % 256 == 0
+            and F2 % 256 == 0 and K % 128 == 0 and K * 256 < 2**32 and F2 * K < 2**32)
+
+
+def matmul_swiglu(state: Fp8State, xq: tuple[Tensor, Tensor], w13: Tensor, x_slot: int, w_slot: int, a_slot: int):
+    """The fp8 W13 projection with the SwiGLU gate fused: ``gu = x8 @ w13_8.T`` (bf16, kept for the backward) and
+    ``a = silu(g) * u`` written only in e4m3, both layouts, slot ``a_slot`` (csrc/gemm_pp.hip EPI_SWIGLU_FWD8) --
+    the values of :meth:`Fp8State.matmul` + :func:`swiglu_fwd_cast_t` on the hand kernel, without the pass over gu.
+    ``xq`` = (x8, xt8) from the producer (the fused norm cast).  Returns ``(gu, w8t, xt8, (a8, a8t))``."""
+    x8, xt8 = xq
+    if _t_ok(w13):
+        w8, w8t = state.cast_t(w13, w_slot)
+    else:
+        w8 = state.cast(w13, w_slot)
+        w8t = w8.t().contiguous()
+    M, F = x8.shape[0], w13.shape[0] // 2
+    a8 = torch.empty(M, F, dtype=state.dtype, device=x8.device)
+    a8t = torch.empty(F, M, dtype=state.dtype, device=x8.device)
+    gu = ops().gemm_fp8_swiglu(x8, w8.contiguous(), state.inv_scale[x_slot : x_slot + 1],
+                               state.inv_scale[w_slot : w_slot + 1], state.scale[a_slot : a_slot + 1], a8, a8t,
+                               state.amax[a_slot : a_slot + 1])
+    return gu, w8t, xt8, (a8, a8t)
 
 
 def swiglu_bwd_cast_t(state: Fp8State, da: Tensor, gu: Tensor, slot: int) -> tuple[Tensor, Tensor]:

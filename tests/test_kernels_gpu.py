@@ -1295,6 +1295,45 @@ def test_gemm_fp8_exact(gpu_device, gpp_mode, M, N, K, fmt_a):
     assert torch.equal(y.cpu(), ref)
 
 
+@pytest.mark.parametrize("M,F,K,persist", [(512, 384, 256, 1), (4096, 640, 512, 40), (1024, 5632, 2048, 1)])
+def test_gemm_fp8_swiglu_matches_gemm_then_cast(gpu_device, M, F, K, persist):
+    """The fused fp8 W13 GEMM + SwiGLU + two-layout e4m3 cast (gemm_fp8_swiglu, EPI_SWIGLU_FWD8) against the unfused
+    pair it replaces -- the hand fp8 GEMM on [W1; W3] then swiglu_cast_fp8_t over its gu: the same per-element
+    MFMA sequence and the same gate / cast arithmetic, so gu, a8, a8t and the recorded amax must match BITWISE (random
+    data), including many tiles per workgroup (persist = 40) and the Llama-1.1B width (F 5632, K 2048)."""
+    h = torch.ops.bpe_hip
+    torch.manual_seed(11)
+    x8 = torch.randn(M, K, device=gpu_device).to(torch.float8_e4m3fn)
+    w8 = (4 * torch.randn(2 * F, K, device=gpu_device)).to(torch.float8_e4m3fn)
+    sp = 1.0 / (4.0 * K**0.5)  # gu ~ N(0, 1)
+    sx = torch.tensor([0.25], device=gpu_device)
+    sw = torch.tensor([sp / 0.25], device=gpu_device)
+    sc = torch.tensor([4.0], device=gpu_device)  # the gate output's cast scale
+    prev = h.gpp_persist_config(persist)
+    try:
+        amax_f = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+        a8 = torch.empty(M, F, dtype=torch.float8_e4m3fn, device=gpu_device)
+        a8t = torch.empty(F, M, dtype=torch.float8_e4m3fn, device=gpu_device)
+        gu = h.gemm_fp8_swiglu(x8, w8, sx, sw, sc, a8, a8t, amax_f)
+        gu_ref = h.gemm_fp8(x8, w8, sx, sw)
+    finally:
+        h.gpp_persist_config(prev)
+    amax_r = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+    a8_r = torch.empty_like(a8)
+    a8t_r = torch.empty_like(a8t)
+    h.swiglu_cast_fp8_t(gu_ref, None, sc, a8_r, a8t_r, amax_r)
+    assert torch.equal(gu, gu_ref)
+    assert torch.equal(a8.view(torch.uint8), a8_r.view(torch.uint8))
+    assert torch.equal(a8t.view(torch.uint8), a8t_r.view(torch.uint8))
+    assert torch.equal(a8t.view(torch.uint8), a8.view(torch.uint8).t())
+    assert int(amax_f) == int(amax_r) and int(amax_f) != 0
+    # and against the fp32 oracle of the gate
+    ref = (x8.float() @ w8.float().t()) * (sx * sw)
+    g, u = ref[:, :F], ref[:, F:]
+    a = g * torch.sigmoid(g) * u
+    assert rel(a8.float().cpu() / 4.0, a.cpu()) < 0.08
+
+
 def test_gemm_fp8_persistent_bitwise_many_tiles(gpu_device):
     """The fp8 kernels at production tile counts (640 output tiles: every persistent workgroup walks 2-3 of them, the
     3-workgroup form ~213), on small-integer operands whose products are exact: the one-tile, persistent and

@@ -320,8 +320,8 @@ def _same_weights_losses(c: Shape, steps, gpu_device, margin: float = 1.0, train
 
     ``train``: evaluate with gradients enabled (no backward, no optimizer step), so the fused block takes its
     TRAINING forward -- with fp8 weight gradients the two RMSNorms write h1 / h2 only as e4m3 in both layouts
-    (``add_rmsnorm_cast_t``) and the gate writes a only as e4m3 (``swiglu_fwd_cast_t``), kernels an eval-mode forward
-    never runs."""
+    (``add_rmsnorm_cast_t``) and the gate writes a only as e4m3 (``swiglu_fwd_cast_t``, or the fused W13 GEMM's
+    epilogue, ``matmul_swiglu``), kernels an eval-mode forward never runs."""
     ids, vocab = _tokens()
     model = _ours(vocab, c, gpu_device)
     eng = _engine(model, 1, c)
@@ -355,7 +355,7 @@ def test_fp8_forward_matches_bf16_on_same_weights(gpu_device, monkeypatch):
     step (profiles/parity/fp8_spike_probe_r5.json)."""
     from bpe_transformer.models import fused_block as fb
 
-    ran = {"norm8": 0, "swiglu_cast": 0}
+    ran = {"norm8": 0, "swiglu_cast": 0, "swiglu_gemm": 0}
 
     def counted(name, fn):
         def f(*a, **k):
@@ -365,8 +365,10 @@ def test_fp8_forward_matches_bf16_on_same_weights(gpu_device, monkeypatch):
 
     monkeypatch.setattr(fb, "add_rmsnorm_cast_t", counted("norm8", fb.add_rmsnorm_cast_t))
     monkeypatch.setattr(fb, "swiglu_fwd_cast_t", counted("swiglu_cast", fb.swiglu_fwd_cast_t))
+    # the gate's e4m3 cast runs either as its own pass or, by default, in the fused fp8 W13 GEMM's epilogue
+    monkeypatch.setattr(fb, "matmul_swiglu", counted("swiglu_gemm", fb.matmul_swiglu))
     res = _same_weights_losses(SHAPES["llama"], [18, 25, 73], gpu_device, train=True)
     _log("parity_llamashape_L2_fp8_same_weights.json", {str(k): {"bf16": v[0], "fp8": v[1]} for k, v in res.items()})
-    assert ran["norm8"] > 0 and ran["swiglu_cast"] > 0, ran
+    assert ran["norm8"] > 0 and ran["swiglu_cast"] + ran["swiglu_gemm"] > 0, ran
     for it, (lb, l8) in res.items():
         assert math.isfinite(l8) and abs(l8 - lb) / lb < 0.01, (it, lb, l8)
