@@ -1,6 +1,8 @@
 """The fp8 W13 projection with the SwiGLU gate and its two-layout e4m3 cast fused into the hand kernel's epilogue
 (``gemm_fp8_swiglu``, gemm_pp.hip EPI_SWIGLU_FWD8) against the unfused pair the fp8 path ran before: the W13 GEMM
-(hipBLASLt ``_scaled_mm``, or the hand kernel) then ``swiglu_cast_fp8_t`` over gu.  Llama-1.1B widths.
+(hipBLASLt ``_scaled_mm``, or the hand kernel) then ``swiglu_cast_fp8_t`` over gu; and the backward: the W2 input
+gradient with the SwiGLU backward + e5m2 two-layout cast fused (``gemm_fp8_swiglu_bwd``, EPI_SWIGLU_BWD8) against
+``_scaled_mm`` then ``swiglu_cast_fp8_t(gu, da)``.  Llama-1.1B widths.
 
     python benchmarks/fp8_swiglu_gemm.py [--tokens 65536]
 
@@ -48,6 +50,22 @@ def main():
             "fused": lambda: h.gemm_fp8_swiglu(x8, w8, sx, sw, sc, a8, a8t, amax),
             "lib_gemm_only": lambda: torch._scaled_mm(x8, w8.t(), scale_a=sx[0], scale_b=sw[0],
                                                       out_dtype=torch.bfloat16)}
+    # backward: da = g8 @ W2 (e5m2 x e4m3) then the SwiGLU backward + e5m2 two-layout cast, vs fused
+    g8 = torch.randn(M, K, device="cuda").to(torch.float8_e5m2)
+    w2t8 = (4 * torch.randn(F, K, device="cuda")).to(torch.float8_e4m3fn)
+    gu = torch.randn(M, 2 * F, device="cuda").to(torch.bfloat16)
+    d8 = torch.empty(M, 2 * F, dtype=torch.float8_e5m2, device="cuda")
+    d8t = torch.empty(2 * F, M, dtype=torch.float8_e5m2, device="cuda")
+    dsc = torch.tensor([64.0], device="cuda")
+
+    def bwd_lib_then_cast():
+        da = torch._scaled_mm(g8, w2t8.t(), scale_a=sx[0], scale_b=sw[0], out_dtype=torch.bfloat16)
+        h.swiglu_cast_fp8_t(gu, da, dsc, d8, d8t, amax)
+
+    arms["bwd_lib_gemm_then_cast"] = bwd_lib_then_cast
+    arms["bwd_fused"] = lambda: h.gemm_fp8_swiglu_bwd(g8, w2t8, sx, sw, gu, dsc, d8, d8t, amax)
+    arms["bwd_lib_gemm_only"] = lambda: torch._scaled_mm(g8, w2t8.t(), scale_a=sx[0], scale_b=sw[0],
+                                                         out_dtype=torch.bfloat16)
     for f in arms.values():
         f()
     torch.cuda.synchronize()

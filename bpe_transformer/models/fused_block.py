@@ -53,8 +53,8 @@ from torch import Tensor
 
 from ..ops._ext import ops as hip
 from ..ops.attention import prerotate_default
-from ..ops.fp8 import (add_rmsnorm_cast_t, matmul_swiglu, norm_cast_ok, rope_ok, swiglu_bwd_cast_t, swiglu_cast_ok,
-                       swiglu_fwd_cast_t, swiglu_gemm_ok)
+from ..ops.fp8 import (add_rmsnorm_cast_t, grads_swiglu, matmul_swiglu, norm_cast_ok, rope_ok, swiglu_bwd_cast_t,
+                       swiglu_bwd_gemm_ok, swiglu_cast_ok, swiglu_fwd_cast_t, swiglu_gemm_ok)
 from ..ops import gemm as _gemm
 from ..ops.gemm import accumulate_weight_grad
 
@@ -363,6 +363,19 @@ class FusedBlockFn(torch.autograd.Function):
             # the W2 and [W1; W3] weight gradients, both ready now, in one grouped split-K launch
             acc_weights([([w2], dy, a), ([w1, w3], dgu, h2)])
             dh2 = dx(dgu, [w1, w3], 2)
+        elif (xt8s is not None and _FP8_SWIGLU_CAST and swiglu_cast_ok(gu)
+              and swiglu_bwd_gemm_ok(dy, w8s[3], gu)):
+            # fp8 weight gradients: one e5m2 cast of dy feeds W2's weight gradient and the hand kernel whose
+            # epilogue turns da (never stored) into [dg | du] in e5m2, both layouts (the W13 projection's operands)
+            view = _adjacent_view([w2.main_grad]) if main else None
+            dgu_q, dw2 = grads_swiglu(fp8[2], dy, fp8[3] + 3, w8s[3], fp8[0], fp8[1] + 4 + 3, xt8s[3], fp8[0],
+                                      fp8[1] + 3, view, gu, fp8[3] + 2)
+            if view is None:
+                acc_dw([w2], dw2)
+            else:
+                _notify(w2)
+            dgu = None
+            dh2 = proj(dgu, [w1, w3], 2, h2, gq=dgu_q)
         else:
             da = proj(dy, [w2], 3, a)
             if xt8s is not None and _FP8_SWIGLU_CAST and swiglu_cast_ok(gu):

@@ -547,7 +547,14 @@ __device__ long long g_gpp_stamps[65536 * 8];
 // operands) and folds max |a| into the slot's amax -- the swiglu_cast_fp8 pass over gu (0.43 ms per Llama layer at
 // 65 536 tokens) disappears.  Same values, rounding and amax as launch_gemm_fp8 + swiglu_cast_fp8_t (bitwise).
 // Persistent kernel only (the a8 tile is transposed through 18 KiB of LDS past the two stages).
-enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2, EPI_ROPE = 3, EPI_SWIGLU_FWD8 = 4 };
+// EPI_SWIGLU_BWD8: the fp8 input-gradient GEMM da = dY8 . W2_8 (e5m2 x e4m3, both K-major) with the SwiGLU backward
+// AND the two-layout e5m2 cast of its result in the epilogue: reads g / u from gu, writes dgu8 = e5m2([dg | du] *
+// scale) [M][2F] and dgu8t [2F][M] and folds max(|dg|, |du|) into the slot's amax -- neither da nor a bf16 dgu
+// reaches HBM, and the swiglu_cast_fp8 backward pass (0.71 ms per Llama layer) disappears.  Same values as the hand
+// fp8 GEMM + swiglu_cast_fp8_t (bitwise).  Persistent kernel only (the transposes go through the A8T tile).  Opt-in
+// (ops/fp8.py BPE_FP8_SWIGLU_BWD_GEMM): 1.89 vs 1.34 ms per Llama layer against hipBLASLt + the cast pass -- the
+// epilogue's 512 KiB of traffic per tile serialises behind the main loop, and the kernel spills 476 B per lane.
+enum { EPI_NONE = 0, EPI_SWIGLU_BWD = 1, EPI_SWIGLU_FWD = 2, EPI_ROPE = 3, EPI_SWIGLU_FWD8 = 4, EPI_SWIGLU_BWD8 = 5 };
 constexpr bool is_swf(int e) { return e == EPI_SWIGLU_FWD || e == EPI_SWIGLU_FWD8; }
 constexpr int A8T_STRIDE = 144;               // bytes per token row of the a8 transpose tile (conflict-free reads)
 constexpr int A8T_BYTES = 128 * A8T_STRIDE;   // one pass: 128 token rows x 128 a columns
@@ -757,6 +764,89 @@ __device__ __forceinline__ void epilogue_bf16(const f32x4 (&acc)[8][4], char* st
                                             (unsigned)(((long)i * ep.ld_act + c * 8) * 2), av);
                 }
             }
+        } else if constexpr (EPI == EPI_SWIGLU_BWD8) {
+            // in two 64-row halves (registers: one half's g / u and e5m2 results at a time); per half, dg then du go
+            // through the 64 x 256 byte transpose tile (xtra, rows of 272 bytes) into dgu8t
+            static_assert(NPASS == 2, "the transpose tile covers half of one 128-row pass");
+            constexpr int QB = 4;  // 16-row groups per half
+            constexpr int TS = 272;  // transpose-tile row stride (bytes)
+            const int c = tid & 31;
+            u16x8 gv[QB], uv[QB];
+            auto load_gu = [&](int b) {
+#pragma unroll
+                for (int qq = 0; qq < QB; ++qq) {
+                    const long ro = (long)(i0 + r0 + (b * QB + qq) * 16 + (tid >> 5)) * ep.ld + j0 + c * 8;
+                    gv[qq] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro));
+                    uv[qq] = ld_stream(reinterpret_cast<const u16x8*>(ep.gu + ro + ep.F));
+                }
+            };
+            load_gu(0);  // the first half's operands before the barrier (as EPI_SWIGLU_BWD)
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            bar();
+            if (h == 0) GPP_STAMP_T(sid, 3);
+            const float sc = ep.a_scale[0];
+            float am = *amx;
+            const long W = 2L * ep.F;  // dgu8 row length
+            const int f4 = tid & 63, tg = tid >> 6;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                if (b == 1) load_gu(1);
+                uint2 qg[QB], qu[QB];  // e5m2 dg / du of this thread's 8 columns in rows (b QB + qq) 16 + (tid >> 5)
+#pragma unroll
+                for (int qq = 0; qq < QB; ++qq) {
+                    const int i = (b * QB + qq) * 16 + (tid >> 5);
+                    const u16x8 v = *reinterpret_cast<const u16x8*>(stg + i * 512 + ((c ^ (i & 15)) << 4));
+                    float dgv[8], duv[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {  // swiglu_cast_fp8_c128_kernel<1, 1>'s arithmetic, in its order
+                        const float gg = bf2f(gv[qq][e]), uu = bf2f(uv[qq][e]), dd = bf2f(v[e]);
+                        const float sg = fast_sigmoid(gg);
+                        const float silu = gg * sg;
+                        duv[e] = bf2f(f2bf(dd * silu));
+                        dgv[e] = bf2f(f2bf(dd * uu * sg * (1.f + gg * (1.f - sg))));
+                        am = fmaxf(am, fabsf(dgv[e]));
+                        am = fmaxf(am, fabsf(duv[e]));
+                    }
+                    qg[qq] = uint2{pack4_fp8<1>(dgv[0] * sc, dgv[1] * sc, dgv[2] * sc, dgv[3] * sc),
+                                   pack4_fp8<1>(dgv[4] * sc, dgv[5] * sc, dgv[6] * sc, dgv[7] * sc)};
+                    qu[qq] = uint2{pack4_fp8<1>(duv[0] * sc, duv[1] * sc, duv[2] * sc, duv[3] * sc),
+                                   pack4_fp8<1>(duv[4] * sc, duv[5] * sc, duv[6] * sc, duv[7] * sc)};
+                    if (st_on) {
+                        uint8_t* row = ep.a8 + (long)(i0 + r0 + i) * W + j0 + c * 8;
+                        *reinterpret_cast<uint2*>(row) = qg[qq];
+                        *reinterpret_cast<uint2*>(row + ep.F) = qu[qq];
+                    }
+                }
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {  // dg, then du: [64 tokens][256 columns] -> [256 columns][64 tokens]
+                    if (b + o > 0) {  // the previous round's transposed reads are done before the tile is rewritten
+                        __builtin_amdgcn_s_waitcnt(0xc07f);
+                        bar();
+                    }
+#pragma unroll
+                    for (int qq = 0; qq < QB; ++qq)
+                        *reinterpret_cast<uint2*>(xtra + (qq * 16 + (tid >> 5)) * TS + c * 8) = o == 0 ? qg[qq] : qu[qq];
+                    __builtin_amdgcn_s_waitcnt(0xc07f);
+                    bar();
+                    unsigned wv[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        wv[k] = *reinterpret_cast<const unsigned*>(xtra + (8 * tg + k) * TS + 4 * f4);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        unsigned lo = 0, hi = 0;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            lo |= ((wv[k] >> (8 * j)) & 0xffu) << (8 * k);
+                            hi |= ((wv[k + 4] >> (8 * j)) & 0xffu) << (8 * k);
+                        }
+                        if (st_on)
+                            *reinterpret_cast<uint2*>(ep.a8t + ((long)o * ep.F + j0 + 4 * f4 + j) * ep.ld_a8t + i0 + r0 +
+                                                      64 * b + 8 * tg) = uint2{lo, hi};
+                    }
+                }
+            }
+            *amx = am;
         } else if constexpr (EPI == EPI_SWIGLU_FWD8) {
             // as EPI_SWIGLU_FWD for gu; a = bf16(silu(g) u) (swiglu_cast_fp8_c128_kernel's values) is cast to e4m3
             // with the slot's scale, stored row-major from registers and, through the a8 tile in LDS (xtra), as
@@ -1128,7 +1218,7 @@ gemm_pp_persist_kernel(const __bf16* __restrict__ A, long lda, const __bf16* __r
         j0 = j0n;
         jb = jbn;
     }
-    if constexpr (EPI == EPI_SWIGLU_FWD8) {  // the workgroup's max |a|: one atomic per workgroup (256 per launch)
+    if constexpr (EPI == EPI_SWIGLU_FWD8 || EPI == EPI_SWIGLU_BWD8) {  // the workgroup's max: one atomic per workgroup
         float m = amx;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
@@ -1543,6 +1633,35 @@ void launch_gemm_fp8_swiglu(const void* A8, long lda, const void* B8, long ldb, 
     kp<<<ntiles < cap ? ntiles : cap, NT, LDS_LAUNCH + A8T_BYTES, s>>>((const __bf16*)A8, lda / 2,
                                                                        (const __bf16*)B8, ldb / 2, (__bf16*)nullptr,
                                                                        0L, 0.f, M, 2 * F, K / 2, ep);
+}
+
+// da = (G8 . W2t_8^T) * sa * sb (G8 e5m2 [M][K], W2t_8 e4m3 [F][K], both K-major) with the SwiGLU backward over gu
+// ([M][2F] bf16) and the two-layout e5m2 cast of [dg | du] (scale d_scale) into dgu8 [M][2F] / dgu8t [2F][M], the
+// max folded into *d_amax (EPI_SWIGLU_BWD8).  M a multiple of 256, F of 256, K of 128.  Persistent kernel only.
+void launch_gemm_fp8_swiglu_bwd(const void* G8, long ldg8, const void* W8, long ldw8, const void* gu, void* dgu8,
+                                void* dgu8t, int M, int F, int K, const float* sa, const float* sb,
+                                const float* d_scale, unsigned* d_amax, hipStream_t s) {
+    Epi ep{(const __bf16*)gu, nullptr, 2L * F, F};
+    ep.prio = prio_mode();
+    ep.gm = g_gm >= 0 ? g_gm : 8;
+    ep.sa = sa;
+    ep.sb = sb;
+    ep.a8 = (uint8_t*)dgu8;
+    ep.a8t = (uint8_t*)dgu8t;
+    ep.ld_a8t = M;
+    ep.a_scale = d_scale;
+    ep.a_amax = d_amax;
+    auto* kp = &gemm_pp_persist_kernel<true, true, EPI_SWIGLU_BWD8, 1, 2>;
+    static bool pattr = false;
+    if (!pattr) {
+        (void)hipFuncSetAttribute((const void*)kp, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_LAUNCH + A8T_BYTES);
+        pattr = true;
+    }
+    const int ntiles = (M / BT) * (F / BT);
+    const int cap = g_persist >= 2 ? g_persist : num_cus();
+    kp<<<ntiles < cap ? ntiles : cap, NT, LDS_LAUNCH + A8T_BYTES, s>>>((const __bf16*)G8, ldg8 / 2,
+                                                                       (const __bf16*)W8, ldw8 / 2, (__bf16*)nullptr,
+                                                                       0L, 0.f, M, F, K / 2, ep);
 }
 
 // C = beta * C + (A8 . B8^T) * sa * sb, split over K into `splits` fp32 partials (slab [splits][M][N]) summed in a

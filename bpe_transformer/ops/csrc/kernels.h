@@ -100,6 +100,10 @@ void launch_gemm_pp_dw_group(int np, const void* const* A, const long* lda, cons
 void launch_gemm_fp8_swiglu(const void* A8, long lda, const void* B8, long ldb, void* gu, long ldg, void* a8,
                             void* a8t, int M, int F, int K, const float* sa, const float* sb, const float* a_scale,
                             unsigned* a_amax, hipStream_t s);
+// da = G8 . W2t_8^T with the SwiGLU backward and the two-layout e5m2 cast of [dg | du] + amax (fused fp8 backward)
+void launch_gemm_fp8_swiglu_bwd(const void* G8, long ldg8, const void* W8, long ldw8, const void* gu, void* dgu8,
+                                void* dgu8t, int M, int F, int K, const float* sa, const float* sb,
+                                const float* d_scale, unsigned* d_amax, hipStream_t s);
 void launch_gemm_fp8(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                      int fmt_a, const float* sa, const float* sb, hipStream_t s);
 

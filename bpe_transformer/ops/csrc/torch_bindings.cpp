@@ -524,6 +524,42 @@ at::Tensor gemm_fp8_swiglu(const at::Tensor& x8, const at::Tensor& w8, const at:
     return gu;
 }
 
+// the fp8 W2 input gradient with the SwiGLU backward fused: da = (g8 @ w8t^T) * sa * sb (g8 e5m2 [M, K], w8t e4m3
+// [F, K]) never leaves the kernel; [dg | du] from da and gu ([M, 2F] bf16) is written as e5m2 with d_scale in both
+// layouts (dgu8 [M, 2F], dgu8t [2F, M]) and its max folded into d_amax (gemm_pp.hip EPI_SWIGLU_BWD8)
+void gemm_fp8_swiglu_bwd(const at::Tensor& g8, const at::Tensor& w8t, const at::Tensor& sa, const at::Tensor& sb,
+                         const at::Tensor& gu, const at::Tensor& d_scale, at::Tensor dgu8, at::Tensor dgu8t,
+                         at::Tensor d_amax) {
+    check_cuda(g8, "g8");
+    check_cuda(w8t, "w8t");
+    check_cuda(gu, "gu");
+    TORCH_CHECK(g8.scalar_type() == at::kFloat8_e5m2 && w8t.scalar_type() == at::kFloat8_e4m3fn,
+                "gemm_fp8_swiglu_bwd: g8 e5m2, w8t e4m3");
+    TORCH_CHECK(g8.dim() == 2 && w8t.dim() == 2 && g8.is_contiguous() && w8t.is_contiguous() && g8.size(1) == w8t.size(1),
+                "gemm_fp8_swiglu_bwd: g8 [M, K] and w8t [F, K] contiguous with a common K");
+    const int64_t M = g8.size(0), F = w8t.size(0), K = g8.size(1);
+    TORCH_CHECK(M % 256 == 0 && F % 256 == 0 && K % 128 == 0 && K > 0,
+                "gemm_fp8_swiglu_bwd: M and F multiples of 256, K of 128");
+    TORCH_CHECK(K * 256 < (1L << 32) && F * K < (1L << 32), "gemm_fp8_swiglu_bwd: operand offsets exceed 32 bits");
+    TORCH_CHECK(gu.scalar_type() == at::kBFloat16 && gu.is_contiguous() && gu.dim() == 2 && gu.size(0) == M &&
+                    gu.size(1) == 2 * F && gu.device() == g8.device(), "gemm_fp8_swiglu_bwd: gu bf16 [M, 2F]");
+    TORCH_CHECK(dgu8.is_contiguous() && dgu8t.is_contiguous() && dgu8.scalar_type() == at::kFloat8_e5m2 &&
+                    dgu8t.scalar_type() == at::kFloat8_e5m2 && dgu8.dim() == 2 && dgu8.size(0) == M &&
+                    dgu8.size(1) == 2 * F && dgu8t.dim() == 2 && dgu8t.size(0) == 2 * F && dgu8t.size(1) == M &&
+                    dgu8.device() == g8.device() && dgu8t.device() == g8.device(),
+                "gemm_fp8_swiglu_bwd: dgu8 [M, 2F] and dgu8t [2F, M] e5m2 on the operands' device");
+    TORCH_CHECK(sa.scalar_type() == at::kFloat && sb.scalar_type() == at::kFloat && d_scale.scalar_type() == at::kFloat &&
+                    sa.numel() >= 1 && sb.numel() >= 1 && d_scale.numel() == 1 && d_amax.scalar_type() == at::kInt &&
+                    d_amax.numel() == 1 && sa.device() == g8.device() && sb.device() == g8.device() &&
+                    d_scale.device() == g8.device() && d_amax.device() == g8.device(),
+                "gemm_fp8_swiglu_bwd: fp32 device scalars sa, sb, d_scale and one int32 amax slot");
+    DevGuard g(g8.device());
+    launch_gemm_fp8_swiglu_bwd(g8.data_ptr(), g8.stride(0), w8t.data_ptr(), w8t.stride(0), gu.data_ptr(),
+                               dgu8.data_ptr(), dgu8t.data_ptr(), (int)M, (int)F, (int)K, sa.data_ptr<float>(),
+                               sb.data_ptr<float>(), d_scale.data_ptr<float>(),
+                               reinterpret_cast<unsigned*>(d_amax.data_ptr<int>()), cur_stream());
+}
+
 // qkv = (a8 @ b8^T) * sa * sb (e4m3 x e4m3) with RoPE on output columns [0, rot_cols) in the epilogue
 at::Tensor gemm_fp8_rope(const at::Tensor& a8, const at::Tensor& b8, const at::Tensor& sa, const at::Tensor& sb,
                          const at::Tensor& cos, const at::Tensor& sin, int64_t S, int64_t D, int64_t rot_cols) {
@@ -1162,6 +1198,8 @@ TORCH_LIBRARY(bpe_hip, m) {
     m.def("gemm_fp8(Tensor a8, Tensor b8, Tensor sa, Tensor sb) -> Tensor");
     m.def("gemm_fp8_swiglu(Tensor x8, Tensor w8, Tensor sa, Tensor sb, Tensor a_scale, Tensor(a!) a8, Tensor(b!) a8t, "
           "Tensor(c!) a_amax) -> Tensor");
+    m.def("gemm_fp8_swiglu_bwd(Tensor g8, Tensor w8t, Tensor sa, Tensor sb, Tensor gu, Tensor d_scale, "
+          "Tensor(a!) dgu8, Tensor(b!) dgu8t, Tensor(c!) d_amax) -> ()");
     m.def("gemm_fp8_rope(Tensor a8, Tensor b8, Tensor sa, Tensor sb, Tensor cos, Tensor sin, int S, int D, "
           "int rot_cols) -> Tensor");
     m.def("gemm_pp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor(a!) C, float beta, int splits=1) -> ()");
@@ -1221,6 +1259,7 @@ TORCH_LIBRARY_IMPL(bpe_hip, CUDA, m) {
     m.impl("gemm_fp8_acc", &gemm_fp8_acc);
     m.impl("gemm_fp8", &gemm_fp8);
     m.impl("gemm_fp8_swiglu", &gemm_fp8_swiglu);
+    m.impl("gemm_fp8_swiglu_bwd", &gemm_fp8_swiglu_bwd);
     m.impl("gemm_fp8_rope", &gemm_fp8_rope);
     m.impl("cast_fp8", &cast_fp8);
     m.impl("transpose_bf16", &transpose_bf16);

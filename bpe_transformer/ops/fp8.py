@@ -274,6 +274,11 @@ def swiglu_fwd_cast_t(state: Fp8State, gu: Tensor, slot: int) -> tuple[Tensor, T
 # BPE_FP8_SWIGLU_GEMM=0: the fp8 W13 GEMM (routed, hipBLASLt at the bench shapes) then swiglu_fwd_cast_t, instead
 # of the hand kernel with the gate and its two-layout cast in the epilogue (swiglu_gemm_ok / matmul_swiglu)
 _SWIGLU_GEMM = os.environ.get("BPE_FP8_SWIGLU_GEMM", "1") == "1"
+# BPE_FP8_SWIGLU_BWD_GEMM=1: the W2 input gradient with the SwiGLU backward + e5m2 cast fused (swiglu_bwd_gemm_ok).
+# Off by default: bitwise right but 1.89 vs 1.34 ms per Llama layer against hipBLASLt + swiglu_bwd_cast_t (its
+# epilogue moves 512 KiB per tile -- g / u in, dg / du out in two layouts -- behind a 16-K-tile main loop, with
+# register spills), fp8 step -3.6 % (profiles/bench/fp8_swiglu_gemm_r6.log)
+_SWIGLU_BWD_GEMM = os.environ.get("BPE_FP8_SWIGLU_BWD_GEMM", "0") == "1"
 
 
 def swiglu_gemm_ok(x8: Tensor, w13: Tensor) -> bool:
@@ -303,6 +308,42 @@ def matmul_swiglu(state: Fp8State, xq: tuple[Tensor, Tensor], w13: Tensor, x_slo
                                state.inv_scale[w_slot : w_slot + 1], state.scale[a_slot : a_slot + 1], a8, a8t,
                                state.amax[a_slot : a_slot + 1])
     return gu, w8t, xt8, (a8, a8t)
+
+
+def swiglu_bwd_gemm_ok(g: Tensor, w8t: Tensor, gu: Tensor) -> bool:
+    """Shapes the fused fp8 W2 input-gradient + SwiGLU backward + two-layout e5m2 cast kernel takes: tokens and d_ff
+    multiples of 256, d_model of 128, 32-bit operand offsets, bf16 gu [M, 2F] contiguous; not under
+    ``BPE_FP8_GEMM=lib``."""
+    M, K = g.shape
+    F = w8t.shape[0]
+    return (_SWIGLU_BWD_GEMM and _MODE != "lib" and M % 256 == 0 and F % 256 == 0 and K % 128 == 0
+            and K * 256 < 2**32 and F * K < 2**32 and w8t.is_contiguous() and w8t.dtype == FP8
+            and gu.dtype == torch.bfloat16 and gu.is_contiguous() and tuple(gu.shape) == (M, 2 * F))
+
+
+def grads_swiglu(g_state: Fp8State, g: Tensor, g_slot: int, w8t: Tensor, w_state: Fp8State, w_slot: int,
+                 xt8: Tensor, x_state: Fp8State, x_slot: int, dw_out: Tensor | None, gu: Tensor, d_slot: int):
+    """:func:`grads` for the W2 projection with the SwiGLU backward fused into its input gradient: ONE e5m2 cast of
+    g (both layouts) feeds the weight gradient (accumulated into ``dw_out``, or returned) and the hand kernel that
+    forms da = g @ W2 without storing it, applies the SwiGLU backward over ``gu`` and writes [dg | du] only as e5m2
+    in both layouts (slot ``d_slot`` of ``g_state``; csrc/gemm_pp.hip EPI_SWIGLU_BWD8) -- the values of
+    :func:`grads` + :func:`swiglu_bwd_cast_t` on the hand kernel.  Returns ``((dgu8, dgu8t), dW or None)``."""
+    g = g.contiguous()
+    if _t_ok(g):
+        g8, g8t = g_state.cast_t(g, g_slot)
+    else:
+        g8 = g_state.cast(g, g_slot)
+        g8t = g8.t().contiguous()
+    gi = g_state.inv_scale[g_slot]
+    M, F = g8.shape[0], w8t.shape[0]
+    dgu8 = torch.empty(M, 2 * F, dtype=g_state.dtype, device=g.device)
+    dgu8t = torch.empty(2 * F, M, dtype=g_state.dtype, device=g.device)
+    ops().gemm_fp8_swiglu_bwd(g8, w8t, g_state.inv_scale[g_slot : g_slot + 1], w_state.inv_scale[w_slot : w_slot + 1],
+                              gu, g_state.scale[d_slot : d_slot + 1], dgu8, dgu8t, g_state.amax[d_slot : d_slot + 1])
+    if dw_out is not None:
+        wgrad_acc(g8t, xt8, gi, x_state.inv_scale[x_slot], dw_out)
+        return (dgu8, dgu8t), None
+    return (dgu8, dgu8t), mm_fp8(g8t, xt8, gi, x_state.inv_scale[x_slot])
 
 
 def swiglu_bwd_cast_t(state: Fp8State, da: Tensor, gu: Tensor, slot: int) -> tuple[Tensor, Tensor]:

@@ -1334,6 +1334,38 @@ def test_gemm_fp8_swiglu_matches_gemm_then_cast(gpu_device, M, F, K, persist):
     assert rel(a8.float().cpu() / 4.0, a.cpu()) < 0.08
 
 
+@pytest.mark.parametrize("M,F,K,persist", [(512, 512, 256, 1), (4096, 768, 512, 40), (1024, 5632, 2048, 1)])
+def test_gemm_fp8_swiglu_bwd_matches_gemm_then_cast(gpu_device, M, F, K, persist):
+    """The fused fp8 W2 input gradient + SwiGLU backward + two-layout e5m2 cast (gemm_fp8_swiglu_bwd,
+    EPI_SWIGLU_BWD8) against the pair it replaces -- the hand fp8 GEMM da = g8 @ w8t^T (e5m2 x e4m3) then
+    swiglu_cast_fp8_t(gu, da): dgu8, dgu8t and the amax must match BITWISE."""
+    h = torch.ops.bpe_hip
+    torch.manual_seed(12)
+    g8 = torch.randn(M, K, device=gpu_device).to(torch.float8_e5m2)
+    w8t = (4 * torch.randn(F, K, device=gpu_device)).to(torch.float8_e4m3fn)
+    gu = torch.randn(M, 2 * F, device=gpu_device).to(torch.bfloat16)
+    sg = torch.tensor([0.25], device=gpu_device)
+    sw = torch.tensor([1.0 / K**0.5], device=gpu_device)
+    sc = torch.tensor([64.0], device=gpu_device)
+    prev = h.gpp_persist_config(persist)
+    try:
+        amax_f = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+        d8 = torch.empty(M, 2 * F, dtype=torch.float8_e5m2, device=gpu_device)
+        d8t = torch.empty(2 * F, M, dtype=torch.float8_e5m2, device=gpu_device)
+        h.gemm_fp8_swiglu_bwd(g8, w8t, sg, sw, gu, sc, d8, d8t, amax_f)
+        da = h.gemm_fp8(g8, w8t, sg, sw)
+    finally:
+        h.gpp_persist_config(prev)
+    amax_r = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+    d8_r = torch.empty_like(d8)
+    d8t_r = torch.empty_like(d8t)
+    h.swiglu_cast_fp8_t(gu, da, sc, d8_r, d8t_r, amax_r)
+    assert torch.equal(d8.view(torch.uint8), d8_r.view(torch.uint8))
+    assert torch.equal(d8t.view(torch.uint8), d8t_r.view(torch.uint8))
+    assert torch.equal(d8t.view(torch.uint8), d8.view(torch.uint8).t())
+    assert int(amax_f) == int(amax_r) and int(amax_f) != 0
+
+
 def test_gemm_fp8_persistent_bitwise_many_tiles(gpu_device):
     """The fp8 kernels at production tile counts (640 output tiles: every persistent workgroup walks 2-3 of them, the
     3-workgroup form ~213), on small-integer operands whose products are exact: the one-tile, persistent and

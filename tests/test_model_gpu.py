@@ -191,6 +191,49 @@ def test_fp8_swiglu_cast_fused_matches_two_pass(gpu_device, monkeypatch, flag):
         assert e < 2e-2, (n, float(e))
 
 
+def test_fp8_fused_swiglu_gemms_match_separate_passes(gpu_device, monkeypatch):
+    """fp8 weight-gradient path with the SwiGLU gate (and, opt-in, its backward) fused into the hand fp8 GEMMs'
+    epilogues (ops/fp8.py matmul_swiglu / grads_swiglu) against the routed GEMMs + separate cast passes: the loss
+    and every gradient agree (d_model 256, d_ff 512, 256 tokens: the shapes both fused kernels take)."""
+    from bpe_transformer.ops import fp8 as F8
+
+    monkeypatch.setattr(F8, "_SWIGLU_GEMM", True)
+    monkeypatch.setattr(F8, "_SWIGLU_BWD_GEMM", True)
+    _, a = _pair(gpu_device)
+    a.enable_fp8(dgrad=True, wgrad=True)
+    ids = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    tgt = torch.randint(0, 1000, (2, 128), device=gpu_device)
+    a.loss(ids, tgt).backward()  # calibration
+    for s_ in a.fp8_states():
+        s_.update()
+    a.zero_grad()
+    b = copy.deepcopy(a)
+    calls = {"fwd": 0, "bwd": 0}
+    real_f, real_b = F8.swiglu_gemm_ok, F8.swiglu_bwd_gemm_ok
+
+    def count(key, fn):
+        def f(*args):
+            ok = fn(*args)
+            calls[key] += int(ok)
+            return ok
+        return f
+
+    from bpe_transformer.models import fused_block
+    monkeypatch.setattr(fused_block, "swiglu_gemm_ok", count("fwd", real_f))
+    monkeypatch.setattr(fused_block, "swiglu_bwd_gemm_ok", count("bwd", real_b))
+    la = a.loss(ids, tgt)
+    la.backward()
+    assert calls["fwd"] > 0 and calls["bwd"] > 0, calls
+    monkeypatch.setattr(F8, "_SWIGLU_GEMM", False)
+    monkeypatch.setattr(F8, "_SWIGLU_BWD_GEMM", False)
+    lb = b.loss(ids, tgt)
+    lb.backward()
+    assert abs(la.item() - lb.item()) < 1e-2, (la.item(), lb.item())
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        e = (pb.grad.float() - pa.grad.float()).norm() / pa.grad.float().norm().clamp_min(1e-12)
+        assert e < 5e-2, (n, float(e))
+
+
 def test_fp8_engine_reduces_loss(gpu_device):
     from bpe_transformer.train.engine import TrainEngine
 
