@@ -8,10 +8,15 @@
 //   * every weight gradient dW = dY^T X (e5m2 x e4m3): the hand kernel's
 //     split-K form (gemm_fp8_acc, fp32 partials, ordered reduce into the
 //     gradient buffer);
+//   * the W13 forward (with fp8 weight gradients): the hand kernel with the
+//     SwiGLU gate and its two-layout e4m3 cast in the epilogue
+//     (gemm_pp.hip EPI_SWIGLU_FWD8; round 6), replacing swiglu_cast_fp8's
+//     forward pass;
 //   * the other forward and the input-gradient GEMMs: hipBLASLt
-//     (torch._scaled_mm) -- it leads the hand kernel by 11-17 % at the
-//     65 536-token shapes -- except the shapes routed to the hand kernel in
-//     ops/tuning/fp8_routes.json (two 16 384-token shapes).
+//     (torch._scaled_mm) -- it leads the hand kernel by 3-12 % at the
+//     65 536-token shapes (profiles/bench/fp8_gemm_orders_r6.log) -- except
+//     the shapes routed to the hand kernel in ops/tuning/fp8_routes.json (two
+//     16 384-token shapes).
 // The casts here produce their operands:
 //
 //   x8 = sat(x * s)            s = FMAX / (max over the amax history), FMAX = 448 (e4m3) / 57344 (e5m2)
